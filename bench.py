@@ -1,0 +1,146 @@
+#!/usr/bin/env python3
+"""Headline benchmark: 512³ (N=512), τ=1e-3, K=20, L=1, fp64 — the reference's MPI+CUDA config (BASELINE.md,
+readme.md:99-100, report.pdf p.16 §4.4).
+
+One bench "step" = one COMPLETE solve exactly as the reference times it: field init (u⁰, u¹) → 19 leapfrog steps →
+error check vs the analytic solution every 2nd step → global error log on the host. Nothing is cached between solves:
+every solve re-initialises the fields and recomputes all K steps. Warmup solves are untimed (the first one captures
+the hipGraph and sets up the RCCL peer connections).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line. ``value`` = whole-job GCell-updates/s = N³·K / t_solve (reference convention), with
+t_solve the max over ranks of the per-solve wall-clock; ``ms_per_step`` = t_solve in ms; ``vs_baseline`` = value ÷ the
+reference's published total-time GCell/s at the same GPU count (1 GPU: 3.570 = 512³·20/0.752 s; 2 GPUs: 5.316 =
+512³·20/0.505 s; for 4 and 8 GPUs, where the reference publishes nothing, its best number, the 2-GPU 5.316).
+The problem size is fixed as GPUs are added: ``scaling`` is "strong".
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+REF_GCELL = {1: 512**3 * 20 / 0.752 / 1e9, 2: 512**3 * 20 / 0.505 / 1e9}
+REF_FINAL_LINF = 3.960129e-09  # report.pdf p.16 §4.3.1, step 20
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20, help="timed full solves")
+    ap.add_argument("--warmup", type=int, default=3, help="untimed full solves")
+    ap.add_argument("--N", type=int, default=512)
+    ap.add_argument("--tau", type=float, default=1e-3)
+    ap.add_argument("--K", type=int, default=20)
+    ap.add_argument("--L", type=float, default=1.0)
+    ap.add_argument("--decomp", default="slab", help="slab | block | PxQxR")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "torch"])
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--tile-rows", type=int, default=8)
+    ap.add_argument("--cpu", action="store_true", help="CPU backend (contract test without a GPU)")
+    ap.add_argument("--out", default="", help="also append the JSON line to this file")
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from mpi_cuda_amd import ProblemSpec
+    from mpi_cuda_amd.parallel.rccl import init_process_group
+    from mpi_cuda_amd.solver import Solver
+
+    rank, world, local = init_process_group("gloo")
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("bench.py --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    spec = ProblemSpec(N=a.N, tau=a.tau, K=a.K, L=a.L, check_every=2)
+    backend = "cpu" if a.cpu else "hip"
+    transport = ("torch" if world > 1 else "native") if a.cpu else a.transport
+    solver = Solver(spec, backend=backend, transport=transport, decomp=a.decomp, rank=rank, world=world,
+                    device=None if a.cpu else local, overlap=not a.no_overlap, graph=not a.no_graph,
+                    tiling={"ty": a.tile_rows})
+
+    def barrier_sync():
+        if not a.cpu:
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        if not a.cpu:
+            torch.cuda.synchronize()
+
+    r = None
+    for _ in range(a.warmup):
+        r = solver.run()
+    barrier_sync()
+    t0 = time.perf_counter()
+    per = []
+    for _ in range(a.steps):
+        ts = time.perf_counter()
+        r = solver.run()
+        per.append(time.perf_counter() - ts)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed, min(per)], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, best = float(t[0]), float(t[1])
+    ms = elapsed / a.steps * 1e3
+    value = spec.cell_updates / (ms / 1e3) / 1e9
+    base = REF_GCELL.get(world, REF_GCELL[2])
+    final_linf = r.max_err[-1] if r is not None and r.max_err else float("nan")
+    correct = bool(r is not None and r.finite and (a.N != 512 or a.K != 20 or a.tau != 1e-3 or a.L != 1.0
+                                                   or abs(final_linf / REF_FINAL_LINF - 1) < 1e-5))
+    if rank == 0:
+        par = f"{a.decomp}{world}" if world > 1 else "single"
+        dims = "x".join(str(d) for d in solver.dims)
+        line = {
+            "metric": "gcell_updates_per_s_512cube_K20",
+            "value": round(value, 3),
+            "unit": "GCell-updates/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(value / base, 3),
+            "dtype": "fp64",
+            "data": "analytic initial condition sin(pi x)sin(pi y)sin(pi z) (synthetic, as the reference)",
+            "config": {
+                "model": "wave3d leapfrog 7-point fp64 (AICCer1/MPI-CUDA mpigpu-1 config)",
+                "global_batch": 1,
+                "seq_len": a.N + 1,
+                "parallelism": par,
+                "grid": f"{a.N}^3", "N": a.N, "tau": a.tau, "K": a.K, "L": a.L,
+                "decomp": dims, "transport": transport, "graph": bool(not a.no_graph),
+                "overlap": bool(not a.no_overlap),
+            },
+            "wall_clock_s": round(ms / 1e3, 6),
+            "best_solve_s": round(best, 6),
+            "baseline_wall_clock_s": {1: 0.752, 2: 0.505}.get(world),
+            "final_max_err": final_linf,
+            "final_rms_err": r.rms_err[-1] if r is not None and r.rms_err else None,
+            "correct": correct,
+        }
+        s = json.dumps(line)
+        print(s, flush=True)
+        if a.out:
+            with open(a.out, "a") as f:
+                f.write(s + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0 if correct else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

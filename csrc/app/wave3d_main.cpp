@@ -1,0 +1,357 @@
+// wave3d — standalone CLI, compatible with the reference's `mpigpu-1 N tau K 1` / `wave N tau K` invocations.
+//
+//   wave3d N tau K [L] [options]                 one GPU (or --cpu)
+//   wave3d N tau K [L] --np P [options]          P ranks on P GPUs of this node (self-spawned, like `mpirun -np P`)
+//   torchrun --no-python --nproc-per-node P bin/wave3d N tau K [L]   same, under an external launcher
+//
+// Reference CLI and output: report.pdf p.15 §4.2.4 (`mpirun -np 2 ./mpigpu-1 512 0.001 20 1`), p.15-16 §4.3 (per-step
+// "Step %d, t = %f, Max Error = %e, L2 Error = %e" lines), p.16 §4.4 (timing breakdown); SURVEY.md §1.3-1.4, §5.5-5.6.
+// Rank discovery: RANK/WORLD_SIZE/LOCAL_RANK (torchrun), OMPI_COMM_WORLD_*, PMI_RANK/PMI_SIZE, or the
+// built-in --np self-spawn. The RCCL unique id travels through a rendezvous file (single node).
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "wave3d/cpu.hpp"
+#include "wave3d/solver.hpp"
+
+using namespace wave3d;
+
+namespace {
+
+struct Args {
+  Problem prob;
+  bool have_L = false;
+  std::string decomp = "slab";
+  int check_every = 2;
+  bool cpu = false;
+  int threads = 0;
+  bool overlap = true;
+  bool graph = true;
+  bool timers = false;
+  bool force = false;
+  int repeat = 1;
+  int warmup = 0;
+  int np = 0;
+  int tile_rows = 8;
+  std::string json, dump;
+  bool quiet = false;
+};
+
+[[noreturn]] void usage(const char* msg = nullptr) {
+  if (msg) std::fprintf(stderr, "wave3d: %s\n\n", msg);
+  std::fprintf(stderr,
+               "usage: wave3d N tau K [L] [options]\n"
+               "  N        intervals per axis ((N+1)^3 nodes)      tau   time step\n"
+               "  K        number of steps                          L     cube edge (default 1)\n"
+               "options:\n"
+               "  --np P             spawn P ranks on this node (one GPU each)\n"
+               "  --decomp D         slab | block | PxQxR (default slab)\n"
+               "  --check-every C    error check cadence (default 2, as the reference)\n"
+               "  --cpu [--threads T] sequential/OpenMP CPU path\n"
+               "  --no-overlap       halo exchange on the compute stream (A/B switch)\n"
+               "  --no-graph         eager launches instead of one captured hipGraph\n"
+               "  --timers           per-phase GPU timers\n"
+               "  --repeat R / --warmup W   timed / untimed solves (report min and mean)\n"
+               "  --tile-rows T      leapfrog tile rows (4, 8, 16)\n"
+               "  --json PATH        machine-readable summary (rank 0)\n"
+               "  --dump PREFIX      write u^K: PREFIX[.rankR].bin (fp64, C order, owned nodes) + .json\n"
+               "  --force            run even if the CFL condition is violated\n"
+               "  --quiet            only the summary\n");
+  std::exit(2);
+}
+
+Args parse(int argc, char** argv) {
+  Args a;
+  std::vector<std::string> pos;
+  for (int i = 1; i < argc; ++i) {
+    std::string s = argv[i];
+    auto next = [&]() -> std::string {
+      if (i + 1 >= argc) usage(("missing value for " + s).c_str());
+      return argv[++i];
+    };
+    if (s == "--np") a.np = std::stoi(next());
+    else if (s == "--decomp") a.decomp = next();
+    else if (s == "--check-every") a.check_every = std::stoi(next());
+    else if (s == "--cpu") a.cpu = true;
+    else if (s == "--threads") a.threads = std::stoi(next());
+    else if (s == "--no-overlap") a.overlap = false;
+    else if (s == "--no-graph") a.graph = false;
+    else if (s == "--timers") a.timers = true;
+    else if (s == "--repeat") a.repeat = std::stoi(next());
+    else if (s == "--warmup") a.warmup = std::stoi(next());
+    else if (s == "--tile-rows") a.tile_rows = std::stoi(next());
+    else if (s == "--json") a.json = next();
+    else if (s == "--dump") a.dump = next();
+    else if (s == "--force") a.force = true;
+    else if (s == "--quiet") a.quiet = true;
+    else if (s == "-h" || s == "--help") usage();
+    else if (!s.empty() && s[0] == '-' && s.size() > 1 && !std::isdigit(static_cast<unsigned char>(s[1])) && s[1] != '.')
+      usage(("unknown option " + s).c_str());
+    else pos.push_back(s);
+  }
+  if (pos.size() < 3 || pos.size() > 4) usage("expected positional N tau K [L]");
+  a.prob.N = std::stoll(pos[0]);
+  a.prob.tau = std::stod(pos[1]);
+  a.prob.K = std::stoi(pos[2]);
+  if (pos.size() == 4) {
+    a.prob.L = std::stod(pos[3]);
+    a.have_L = true;
+  }
+  if (a.repeat < 1) a.repeat = 1;
+  return a;
+}
+
+int env_int(const char* const* names, int dflt) {
+  for (const char* const* n = names; *n; ++n) {
+    const char* v = std::getenv(*n);
+    if (v && *v) return std::atoi(v);
+  }
+  return dflt;
+}
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+std::string rdzv_path() {
+  if (const char* p = std::getenv("W3D_RDZV_FILE")) return p;
+  const char* port = std::getenv("MASTER_PORT");
+  const char* run = std::getenv("TORCHELASTIC_RUN_ID");
+  std::ostringstream os;
+  os << "/tmp/wave3d-rdzv-" << (port ? port : "0") << "-" << (run ? run : "x") << "-" << getppid() << ".uid";
+  return os.str();
+}
+
+std::string exchange_unique_id(int rank) {
+  const std::string path = rdzv_path();
+  if (rank == 0) {
+    const std::string id = Comm::make_unique_id();
+    const std::string tmp = path + ".tmp";
+    {
+      std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
+      f.write(id.data(), static_cast<std::streamsize>(id.size()));
+      if (!f) fail("cannot write rendezvous file " + tmp);
+    }
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) fail("cannot publish rendezvous file " + path);
+    return id;
+  }
+  const double t0 = now_s();
+  for (;;) {
+    std::ifstream f(path, std::ios::binary);
+    if (f) {
+      std::string id((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+      if (id.size() == 128) return id;
+    }
+    if (now_s() - t0 > 120.0) fail("timed out waiting for rendezvous file " + path);
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  }
+}
+
+void print_errors(const std::vector<int>& steps, const std::vector<double>& mx, const std::vector<double>& rms,
+                  double tau) {
+  for (size_t i = 0; i < steps.size(); ++i)
+    std::printf("Step %d, t = %f, Max Error = %e, L2 Error = %e\n", steps[i], steps[i] * tau, mx[i], rms[i]);
+}
+
+void write_dump(const std::string& prefix, const Problem& p, const Layout& l, const std::vector<double>& u, int rank,
+                int world, const Dims& d) {
+  const std::string base = world > 1 ? prefix + ".rank" + std::to_string(rank) : prefix;
+  std::ofstream f(base + ".bin", std::ios::binary | std::ios::trunc);
+  std::vector<double> row(static_cast<size_t>(l.nz));
+  for (i64 ix = 0; ix < l.nx; ++ix)
+    for (i64 iy = 0; iy < l.ny; ++iy) {
+      const double* src = u.data() + l.off(ix, iy, 0);
+      std::memcpy(row.data(), src, row.size() * sizeof(double));
+      f.write(reinterpret_cast<const char*>(row.data()), static_cast<std::streamsize>(row.size() * sizeof(double)));
+    }
+  std::ofstream j(base + ".json", std::ios::trunc);
+  j << "{\"format\": \"wave3d-dump-v1\", \"dtype\": \"float64\", \"order\": \"C\", \"N\": " << p.N
+    << ", \"L\": " << p.L << ", \"tau\": " << p.tau << ", \"step\": " << p.K << ", \"t\": " << p.K * p.tau
+    << ", \"shape\": [" << l.nx << ", " << l.ny << ", " << l.nz << "], \"offset\": [" << l.gx0 << ", " << l.gy0
+    << ", " << l.gz0 << "], \"global_shape\": [" << p.N + 1 << ", " << p.N + 1 << ", " << p.N + 1
+    << "], \"rank\": " << rank << ", \"world\": " << world << ", \"dims\": [" << d.px << ", " << d.py << ", " << d.pz
+    << "]}\n";
+}
+
+int spawn(int np, char** argv) {
+  // Fork the ranks before anything touches the GPU; each child continues in main() with its rank in the env.
+  std::ostringstream rf;
+  rf << "/tmp/wave3d-rdzv-spawn-" << getpid() << "-" << static_cast<long long>(now_s() * 1e6) << ".uid";
+  const std::string rdzv = rf.str();
+  std::vector<pid_t> kids;
+  for (int r = 0; r < np; ++r) {
+    const pid_t pid = fork();
+    if (pid < 0) fail("fork failed");
+    if (pid == 0) {
+      setenv("RANK", std::to_string(r).c_str(), 1);
+      setenv("LOCAL_RANK", std::to_string(r).c_str(), 1);
+      setenv("WORLD_SIZE", std::to_string(np).c_str(), 1);
+      setenv("W3D_RDZV_FILE", rdzv.c_str(), 1);
+      setenv("W3D_SPAWNED", "1", 1);
+      return -1;  // child: continue
+    }
+    kids.push_back(pid);
+  }
+  (void)argv;
+  int rc = 0;
+  for (pid_t k : kids) {
+    int st = 0;
+    waitpid(k, &st, 0);
+    const int c = WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNALED(st) ? WTERMSIG(st) : 0);
+    if (c != 0 && rc == 0) rc = c;
+  }
+  std::remove(rdzv.c_str());
+  return rc;
+}
+
+int run_cpu(const Args& a) {
+  CpuSolver s(a.prob, a.check_every, a.threads);
+  CpuResult r;
+  double best = 1e30, sum = 0;
+  for (int i = 0; i < a.warmup + a.repeat; ++i) {
+    r = s.run();
+    if (i >= a.warmup) {
+      best = std::min(best, r.solve_s);
+      sum += r.solve_s;
+    }
+  }
+  if (!a.quiet) print_errors(r.steps, r.max_err, r.rms_err, a.prob.tau);
+  const double gcell = a.prob.cell_updates() / best / 1e9;
+  std::printf("Total time: %.6f s (init %.6f s, compute %.6f s), threads %d, %.3f GCell/s\n", best, r.init_s,
+              r.compute_s, cpu_max_threads(), gcell);
+  if (!a.json.empty()) {
+    std::ofstream j(a.json);
+    j << "{\"backend\": \"cpu\", \"N\": " << a.prob.N << ", \"tau\": " << a.prob.tau << ", \"K\": " << a.prob.K
+      << ", \"L\": " << a.prob.L << ", \"threads\": " << cpu_max_threads() << ", \"solve_s\": " << best
+      << ", \"mean_s\": " << sum / a.repeat << ", \"gcell_per_s\": " << gcell
+      << ", \"final_max_err\": " << (r.max_err.empty() ? 0.0 : r.max_err.back())
+      << ", \"final_rms_err\": " << (r.rms_err.empty() ? 0.0 : r.rms_err.back()) << "}\n";
+  }
+  if (!a.dump.empty()) write_dump(a.dump, a.prob, s.layout(), s.field(0), 0, 1, Dims{1, 1, 1});
+  return r.finite ? 0 : 3;
+}
+
+int run_gpu(const Args& a) {
+  static const char* const kRank[] = {"RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID", nullptr};
+  static const char* const kSize[] = {"WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "SLURM_NTASKS", nullptr};
+  static const char* const kLocal[] = {"LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", nullptr};
+  const int rank = env_int(kRank, 0), world = env_int(kSize, 1);
+  const double t_proc0 = now_s();
+  int ndev = 0;
+  W3D_HIP(hipGetDeviceCount(&ndev));
+  W3D_REQUIRE(ndev > 0, "no GPU visible (use --cpu for the CPU path)");
+  const int local = env_int(kLocal, rank);
+  const int dev = local % ndev;
+  W3D_HIP(hipSetDevice(dev));
+  hipDeviceProp_t prop;
+  W3D_HIP(hipGetDeviceProperties(&prop, dev));
+
+  std::shared_ptr<Comm> comm;
+  const double t_comm0 = now_s();
+  if (world > 1) {
+    const std::string id = exchange_unique_id(rank);
+    comm = std::make_shared<Comm>(rank, world, id);
+    if (rank == 0) std::remove(rdzv_path().c_str());
+  }
+  const double t_comm = now_s() - t_comm0;
+
+  SolverOptions o;
+  o.decomp = a.decomp;
+  o.check_every = a.check_every;
+  o.overlap = a.overlap;
+  o.graph = a.graph;
+  o.timers = a.timers;
+  o.tiling.ty = a.tile_rows;
+  GpuSolver s(a.prob, o, rank, world, comm);
+  size_t free_b = 0, total_b = 0;
+  W3D_HIP(hipMemGetInfo(&free_b, &total_b));
+
+  RunResult r;
+  double best = 1e30, sum = 0, first = 0;
+  for (int i = 0; i < a.warmup + a.repeat; ++i) {
+    if (comm) comm_barrier(*comm);
+    r = s.run();
+    double t = r.solve_s;
+    if (comm) t = comm_allreduce(*comm, t, true);  // max over ranks
+    if (i == 0) first = t;
+    if (i >= a.warmup) {
+      best = std::min(best, t);
+      sum += t;
+    }
+  }
+  const double mean = sum / a.repeat;
+  const double t_proc = now_s() - t_proc0;
+  const Dims d = s.dims();
+  if (rank == 0) {
+    if (!a.quiet) {
+      std::printf("wave3d: N=%lld tau=%g K=%d L=%g ranks=%d decomp=%dx%dx%d device=%s courant=%.3f\n",
+                  static_cast<long long>(a.prob.N), a.prob.tau, a.prob.K, a.prob.L, world, d.px, d.py, d.pz,
+                  prop.gcnArchName, a.prob.courant());
+      print_errors(r.steps, r.max_err, r.rms_err, a.prob.tau);
+    }
+    const double gcell = a.prob.cell_updates() / best / 1e9;
+    std::printf("Total time: %.6f s (solve region, max over %d rank%s; best of %d, mean %.6f s, first %.6f s)\n", best,
+                world, world > 1 ? "s" : "", a.repeat, mean, first);
+    std::printf("Throughput: %.2f GCell/s; process wall-clock %.3f s (RCCL init %.3f s); graph %s, overlap %s\n",
+                gcell, t_proc, t_comm, s.options().graph ? "on" : "off", a.overlap ? "on" : "off");
+    if (a.timers)
+      std::printf("Phases (rank 0, last run): init+first step %.3f ms, steps %.3f ms\n", r.phases.init_ms,
+                  r.phases.interior_ms);
+    if (!a.json.empty()) {
+      std::ofstream j(a.json);
+      j.precision(10);
+      j << "{\"backend\": \"hip\", \"N\": " << a.prob.N << ", \"tau\": " << a.prob.tau << ", \"K\": " << a.prob.K
+        << ", \"L\": " << a.prob.L << ", \"ranks\": " << world << ", \"dims\": [" << d.px << ", " << d.py << ", "
+        << d.pz << "], \"solve_s\": " << best << ", \"mean_s\": " << mean << ", \"first_s\": " << first
+        << ", \"process_s\": " << t_proc << ", \"rccl_init_s\": " << t_comm << ", \"gcell_per_s\": " << gcell
+        << ", \"graph\": " << (s.options().graph ? "true" : "false") << ", \"overlap\": "
+        << (a.overlap ? "true" : "false") << ", \"device\": \"" << prop.gcnArchName << "\", \"steps\": [";
+      for (size_t i = 0; i < r.steps.size(); ++i)
+        j << (i ? ", " : "") << "[" << r.steps[i] << ", " << r.max_err[i] << ", " << r.rms_err[i] << "]";
+      j << "]}\n";
+    }
+  }
+  if (!a.dump.empty()) write_dump(a.dump, a.prob, s.layout(), s.download(0), rank, world, d);
+  (void)free_b;
+  (void)total_b;
+  return r.finite ? 0 : 3;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  try {
+    Args a = parse(argc, argv);
+    a.prob.validate();
+    if (!a.prob.cfl_ok()) {
+      std::fprintf(stderr,
+                   "wave3d: CFL violated: courant = tau*sqrt(3)/h = %.4f > 1 (tau_max = %.3e for N=%lld, L=%g); the "
+                   "leapfrog scheme is unstable.%s\n",
+                   a.prob.courant(), a.prob.tau_max(), static_cast<long long>(a.prob.N), a.prob.L,
+                   a.force ? " Continuing (--force)." : " Use a smaller tau, or --force.");
+      if (!a.force) return 2;
+    }
+    if (a.np > 1 && !std::getenv("W3D_SPAWNED")) {
+      const int rc = spawn(a.np, argv);
+      if (rc >= 0) return rc;  // parent
+    }
+    const int rc = a.cpu ? run_cpu(a) : run_gpu(a);
+    if (rc == 3) std::fprintf(stderr, "wave3d: solution blew up (non-finite error)\n");
+    return rc;
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "%s\n", e.what());
+    return 1;
+  }
+}

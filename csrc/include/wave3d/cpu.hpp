@@ -1,0 +1,81 @@
+// CPU path: sequential / OpenMP solver kernels on the same local layout as the GPU path.
+//
+// Covers the reference's sequential (wave.cpp) and OpenMP (openmpwave.cpp) programs (readme.md:33-36, report.pdf
+// p.20-21 §5.1-5.2) and is the bit-exact baseline the HIP kernels are tested against.
+#pragma once
+
+#include "wave3d/decomp.hpp"
+#include "wave3d/problem.hpp"
+
+namespace wave3d {
+
+// Local compute sub-box (local node indices, half-open).
+struct LBox {
+  i64 x0 = 0, x1 = 0, y0 = 0, y1 = 0, z0 = 0, z1 = 0;
+  bool empty() const { return x1 <= x0 || y1 <= y0 || z1 <= z0; }
+  i64 count() const { return empty() ? 0 : (x1 - x0) * (y1 - y0) * (z1 - z0); }
+};
+
+inline LBox compute_box(const Layout& l) { return LBox{l.cx0, l.cx1, l.cy0, l.cy1, l.cz0, l.cz1}; }
+
+// Error accumulator: L∞ and Σe² over the updated (interior) nodes.
+struct ErrAcc {
+  double max = 0.0;
+  double sum = 0.0;
+};
+
+// Set the OpenMP thread count (<=0 keeps the runtime default). Returns the effective count.
+int cpu_set_threads(int n);
+int cpu_max_threads();
+
+// u0 = φ and u1 = u0 + τ²/2 Δ_h u0 over the whole local allocation, ghosts included (they are analytic, so no halo
+// exchange is needed before the first leapfrog step). `s` = &sin_table_ext[1].
+void cpu_init_first(const Layout& l, const Coeffs& c, const double* s, double* u0, double* u1);
+
+// u^{n+1} = 2u^n − u^{n−1} + τ²Δ_h u^n on `box`, written in place over u^{n−1} (`old_out`).
+// If acc != nullptr also accumulates the error vs the analytic solution φ·ct over the box.
+void cpu_leapfrog(const Layout& l, const Coeffs& c, const double* cur, double* old_out, const LBox& box,
+                  const double* s, double ct, ErrAcc* acc);
+
+// Error of a stored field vs φ·ct over `box` (used for step 1 and for the standalone error check).
+void cpu_error(const Layout& l, const double* u, const LBox& box, const double* s, double ct, ErrAcc* acc);
+
+// Pack / unpack one y or z face between the field and a contiguous buffer (x faces are contiguous already).
+void cpu_pack_face(const Layout& l, const Face& f, const double* u, double* buf);
+void cpu_unpack_face(const Layout& l, const Face& f, const double* buf, double* u);
+
+}  // namespace wave3d
+
+// ------------------------------------------------------------------------------------------------------------------
+// Whole-domain CPU solver (the reference's sequential `wave` / OpenMP `wave3dOMP` programs).
+// ------------------------------------------------------------------------------------------------------------------
+#include <vector>
+
+namespace wave3d {
+
+struct CpuResult {
+  std::vector<int> steps;
+  std::vector<double> max_err, rms_err;
+  double solve_s = 0.0, init_s = 0.0, compute_s = 0.0, check_s = 0.0;
+  bool finite = true;
+};
+
+class CpuSolver {
+ public:
+  CpuSolver(const Problem& p, int check_every = 2, int threads = 0);
+  CpuResult run();
+  // u^K (which = 0) or u^{K-1} (which = 1), padded local layout (single rank = whole domain).
+  const std::vector<double>& field(int which) const { return which == 0 ? u_[final_] : u_[1 - final_]; }
+  const Layout& layout() const { return lay_; }
+  std::vector<int> check_steps() const;
+
+ private:
+  Problem prob_;
+  int check_every_;
+  Layout lay_;
+  std::vector<double> u_[2];
+  std::vector<double> s_;
+  int final_ = 1;
+};
+
+}  // namespace wave3d

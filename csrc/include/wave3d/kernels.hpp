@@ -1,0 +1,55 @@
+// Hand-written CDNA4 (gfx950) HIP kernels: launch interface.
+//
+//   k_init_first  : u⁰ = φ and u¹ = u⁰ + τ²/2·Δ_h u⁰ in one write-only pass (16 B/node), ghosts included
+//                   (reference kernels K1 + K2).
+//   k_leapfrog    : the hot loop — 2.5-D tiled 7-point leapfrog, x-marching register queue, LDS-staged (y,z) tile,
+//                   16-byte node pairs, in place over u^{n−1}, Dirichlet BC by construction, optional fused error
+//                   epilogue (reference kernels K3 + K4 + K5).
+//   k_reduce      : fixed-order reduction of per-block error partials (deterministic).
+//   k_pack/unpack : strided y/z halo faces ↔ contiguous RCCL staging buffers (reference kernel K6).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "wave3d/cpu.hpp"
+#include "wave3d/decomp.hpp"
+#include "wave3d/problem.hpp"
+
+namespace wave3d {
+
+// Error partial: x = L∞ candidate, y = Σe².
+using Partial = double2;
+
+// Tiling knobs of the leapfrog kernel (runtime-selectable so the tuner/bench can sweep them).
+struct LeapfrogTiling {
+  int ty = 8;             // tile rows (y) per workgroup; block = 64 × ty threads; one 16-byte pair per lane
+  int target_blocks = 0;  // x-chunking aims for at least this many workgroups (0 = 8 per CU)
+  bool xcd_remap = true;  // give each XCD a contiguous range of tiles (L2 reuse of tile halos)
+  bool nt_store = false;  // non-temporal stores of u^{n+1}
+};
+
+// Number of workgroups (= error partials) a leapfrog launch over `boxes` will use.
+int leapfrog_blocks(const Layout& l, const LBox* boxes, int nbox, const LeapfrogTiling& t);
+
+void launch_init_first(const Layout& l, const Coeffs& c, const double* d_s, double* u0, double* u1,
+                       hipStream_t stream);
+
+// Runs one leapfrog step over up to 6 boxes in a single launch. If `partials` is non-null the error vs φ·ct is reduced
+// per workgroup into partials[0 .. leapfrog_blocks()).
+void launch_leapfrog(const Layout& l, const Coeffs& c, const double* cur, double* old_out, const LBox* boxes, int nbox,
+                     const double* d_s, double ct, Partial* partials, const LeapfrogTiling& t, hipStream_t stream);
+
+// Error of a stored field vs φ·ct over `box` (step 1 / standalone check). Writes leapfrog-compatible partials and
+// returns how many.
+int error_blocks(const Layout& l, const LBox& box);
+void launch_error(const Layout& l, const double* u, const LBox& box, const double* d_s, double ct, Partial* partials,
+                  hipStream_t stream);
+
+// out[0] = (max_i partials[i].x, Σ_i partials[i].y), in a fixed order.
+void launch_reduce(const Partial* partials, int n, Partial* out, hipStream_t stream);
+
+// Pack all strided faces of `plan` from `u` into `buf`, or unpack `buf` into the ghost layers of `u`.
+void launch_pack(const Layout& l, const HaloPlan& plan, const double* u, double* buf, hipStream_t stream);
+void launch_unpack(const Layout& l, const HaloPlan& plan, const double* buf, double* u, hipStream_t stream);
+
+}  // namespace wave3d

@@ -1,0 +1,137 @@
+// GPU solver runtime: one process (rank) per MI355X, RCCL point-to-point halo exchange over xGMI.
+//
+// Reference call stack being replaced (report.pdf p.15-16 §4.2.4-4.4): MPI_Init → cudaSetDevice →
+// host init + H2D → per step {D2H faces → MPI_Sendrecv → H2D; step kernel; BC kernel; error kernel + MPI_Reduce}.
+// Here:
+//   * fields are initialised on the device (no H2D), both in-place leapfrog levels live in HBM;
+//   * per step the boundary SHELL of the local box is updated first, then its faces go to the neighbours with
+//     ncclSend/ncclRecv on a side stream while the INTERIOR update runs on the compute stream;
+//   * error partials stay on the device; the whole error log crosses to the host once, with one all-gather;
+//   * the full K-step solve can be captured into one hipGraph and replayed.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "wave3d/decomp.hpp"
+#include "wave3d/kernels.hpp"
+#include "wave3d/problem.hpp"
+
+namespace wave3d {
+
+#define W3D_HIP(expr)                                                                                \
+  do {                                                                                               \
+    hipError_t _e = (expr);                                                                          \
+    if (_e != hipSuccess) ::wave3d::fail(std::string(#expr) + ": " + hipGetErrorString(_e));          \
+  } while (0)
+
+struct SolverOptions {
+  std::string decomp = "slab";  // slab | block | PxQxR
+  int check_every = 2;          // error check cadence (reference prints every 2nd step); 0 = only the last step
+  bool overlap = true;          // shell/interior split with the halo exchange on a side stream
+  bool graph = true;            // capture the whole solve into a hipGraph, replay it on every run()
+  bool timers = false;          // per-phase hipEvent timers (adds events to the stream; disables the graph)
+  LeapfrogTiling tiling;
+};
+
+struct PhaseTimes {
+  double init_ms = 0, shell_ms = 0, interior_ms = 0, comm_ms = 0, check_ms = 0, gather_ms = 0;
+};
+
+struct RunResult {
+  std::vector<int> steps;         // checked steps
+  std::vector<double> max_err;    // L∞ (global)
+  std::vector<double> rms_err;    // sqrt(Σe² / (N−1)³) (global)
+  double solve_s = 0.0;           // host wall time of run(): field init → last error gathered
+  PhaseTimes phases;              // only with SolverOptions::timers
+  bool finite = true;
+};
+
+// Thin owner of an RCCL communicator.
+class Comm {
+ public:
+  // 128-byte ncclUniqueId as raw bytes (call on rank 0, ship to the others).
+  static std::string make_unique_id();
+  Comm(int rank, int world, const std::string& unique_id);
+  ~Comm();
+  Comm(const Comm&) = delete;
+  Comm& operator=(const Comm&) = delete;
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  void* raw() const { return comm_; }  // ncclComm_t
+  // Raise if RCCL reported an asynchronous error.
+  void check_async() const;
+
+ private:
+  int rank_ = 0, world_ = 1;
+  void* comm_ = nullptr;
+};
+
+class GpuSolver {
+ public:
+  GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, int world, std::shared_ptr<Comm> comm);
+  ~GpuSolver();
+  GpuSolver(const GpuSolver&) = delete;
+  GpuSolver& operator=(const GpuSolver&) = delete;
+
+  // One full solve: u⁰, u¹ → K−1 leapfrog steps with error checks → global error log on the host.
+  RunResult run();
+
+  // Host copy of the local array holding u^K (which = 0) or u^{K−1} (which = 1), full padded layout.
+  std::vector<double> download(int which) const;
+
+  const Layout& layout() const { return lay_; }
+  const Dims& dims() const { return dims_; }
+  const HaloPlan& halo() const { return plan_; }
+  const Problem& problem() const { return prob_; }
+  const SolverOptions& options() const { return opt_; }
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  std::vector<LBox> shell_boxes() const { return shell_; }
+  LBox interior_box() const { return interior_; }
+  std::vector<int> check_steps() const;
+  size_t device_bytes() const;
+
+ private:
+  void enqueue_solve();  // all device work of one solve on s0/s1 (graph-capturable)
+  void exchange(double* field, hipStream_t st);
+  void gather_errors(RunResult& r);
+
+  Problem prob_;
+  SolverOptions opt_;
+  Coeffs coef_;
+  int rank_, world_;
+  std::shared_ptr<Comm> comm_;
+  Dims dims_;
+  Layout lay_;
+  HaloPlan plan_;
+  std::vector<LBox> shell_;
+  LBox interior_;
+  LBox full_;
+
+  double* u_[2] = {nullptr, nullptr};
+  double* d_s_ = nullptr;        // extended sin table (+1 applied when passed to kernels)
+  double* send_buf_ = nullptr;   // packed y/z faces
+  double* recv_buf_ = nullptr;
+  Partial* partials_ = nullptr;
+  int n_partials_ = 0;
+  Partial* errlog_ = nullptr;    // [K+1]
+  Partial* errall_ = nullptr;    // [world][K+1]
+  std::vector<double> ct_;       // cos(a_t n τ)
+  hipStream_t s0_ = nullptr, s1_ = nullptr;
+  hipEvent_t ev_shell_ = nullptr, ev_halo_ = nullptr;
+  hipGraphExec_t graph_exec_ = nullptr;
+  int final_buf_ = 0;            // buffer index holding u^K after a solve
+  std::vector<hipEvent_t> tev_;  // timer events
+};
+
+}  // namespace wave3d
+
+namespace wave3d {
+// Host-scalar collectives over the RCCL communicator (timer max-reduction, barriers). Blocking.
+double comm_allreduce(const Comm& c, double v, bool max_op);
+void comm_barrier(const Comm& c);
+}  // namespace wave3d

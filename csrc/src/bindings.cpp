@@ -1,0 +1,347 @@
+// Python bindings of the native runtime (pybind11). Module: mpi_cuda_amd._C
+//
+// The GPU path is fully native (GpuSolver: HIP kernels + RCCL, C++ step loop, hipGraph). The raw kernel launchers take
+// device pointers as integers (torch.Tensor.data_ptr()) and a stream handle (torch.cuda.current_stream().cuda_stream)
+// so the tests can drive each kernel against a PyTorch fp64 reference. The CPU kernels take numpy float64 arrays.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "wave3d/cpu.hpp"
+#include "wave3d/decomp.hpp"
+#include "wave3d/kernels.hpp"
+#include "wave3d/problem.hpp"
+#include "wave3d/solver.hpp"
+
+namespace py = pybind11;
+using namespace wave3d;
+
+namespace {
+
+using darr = py::array_t<double, py::array::c_style | py::array::forcecast>;
+
+double* mut_ptr(darr& a, i64 need, const char* what) {
+  W3D_REQUIRE(a.size() >= need, std::string(what) + ": array too small");
+  return a.mutable_data();
+}
+const double* ro_ptr(const darr& a, i64 need, const char* what) {
+  W3D_REQUIRE(a.size() >= need, std::string(what) + ": array too small");
+  return a.data();
+}
+
+template <class T>
+T* dptr(std::uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+hipStream_t sptr(std::uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+py::dict result_dict(const RunResult& r) {
+  py::dict d;
+  d["steps"] = r.steps;
+  d["max_err"] = r.max_err;
+  d["rms_err"] = r.rms_err;
+  d["solve_s"] = r.solve_s;
+  d["finite"] = r.finite;
+  py::dict ph;
+  ph["init_ms"] = r.phases.init_ms;
+  ph["steps_ms"] = r.phases.interior_ms;
+  d["phases"] = ph;
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "wave3d native runtime: CDNA4 HIP kernels, RCCL halo exchange, CPU/OpenMP path";
+
+  py::class_<Problem>(m, "Problem")
+      .def(py::init([](i64 N, double tau, int K, double L) {
+             Problem p;
+             p.N = N;
+             p.tau = tau;
+             p.K = K;
+             p.L = L;
+             p.validate();
+             return p;
+           }),
+           py::arg("N") = 512, py::arg("tau") = 1e-3, py::arg("K") = 20, py::arg("L") = 1.0)
+      .def_readwrite("N", &Problem::N)
+      .def_readwrite("tau", &Problem::tau)
+      .def_readwrite("K", &Problem::K)
+      .def_readwrite("L", &Problem::L)
+      .def_property_readonly("h", &Problem::h)
+      .def_property_readonly("a_t", &Problem::a_t)
+      .def_property_readonly("courant", &Problem::courant)
+      .def_property_readonly("cfl_ok", &Problem::cfl_ok)
+      .def_property_readonly("tau_max", &Problem::tau_max)
+      .def_property_readonly("cell_updates", &Problem::cell_updates)
+      .def("__repr__", [](const Problem& p) {
+        return "Problem(N=" + std::to_string(p.N) + ", tau=" + std::to_string(p.tau) + ", K=" + std::to_string(p.K) +
+               ", L=" + std::to_string(p.L) + ")";
+      });
+
+  py::class_<Coeffs>(m, "Coeffs")
+      .def_static("from_problem", &Coeffs::from)
+      .def_readonly("ihx2", &Coeffs::ihx2)
+      .def_readonly("ihy2", &Coeffs::ihy2)
+      .def_readonly("ihz2", &Coeffs::ihz2)
+      .def_readonly("tau2", &Coeffs::tau2)
+      .def_readonly("half_tau2", &Coeffs::half_tau2);
+
+  m.def("sin_table_ext", [](const Problem& p) {
+    auto v = sin_table_ext(p);
+    return darr(static_cast<py::ssize_t>(v.size()), v.data());
+  });
+  m.def("time_factor", &time_factor);
+
+  py::class_<Dims>(m, "Dims")
+      .def(py::init([](int px, int py_, int pz) { return Dims{px, py_, pz}; }))
+      .def_readwrite("px", &Dims::px)
+      .def_readwrite("py", &Dims::py)
+      .def_readwrite("pz", &Dims::pz)
+      .def("size", &Dims::size)
+      .def("as_tuple", [](const Dims& d) { return py::make_tuple(d.px, d.py, d.pz); });
+  m.def("parse_dims", &parse_dims);
+  m.def("block_dims", &block_dims);
+  m.def("split_axis", [](i64 N, int p, int c) {
+    i64 b, e;
+    split_axis(N, p, c, &b, &e);
+    return py::make_tuple(b, e);
+  });
+
+  py::class_<Box>(m, "Box")
+      .def_readonly("x0", &Box::x0)
+      .def_readonly("x1", &Box::x1)
+      .def_readonly("y0", &Box::y0)
+      .def_readonly("y1", &Box::y1)
+      .def_readonly("z0", &Box::z0)
+      .def_readonly("z1", &Box::z1)
+      .def("count", &Box::count);
+  m.def("rank_box", &rank_box);
+  m.def("neighbor_rank", &neighbor_rank);
+  m.def("rank_coords", &rank_coords);
+
+  py::class_<Layout>(m, "Layout")
+      .def_readonly("N", &Layout::N)
+      .def_readonly("nx", &Layout::nx)
+      .def_readonly("ny", &Layout::ny)
+      .def_readonly("nz", &Layout::nz)
+      .def_readonly("gx0", &Layout::gx0)
+      .def_readonly("gy0", &Layout::gy0)
+      .def_readonly("gz0", &Layout::gz0)
+      .def_readonly("zs", &Layout::zs)
+      .def_readonly("pitch", &Layout::pitch)
+      .def_readonly("plane", &Layout::plane)
+      .def_readonly("total", &Layout::total)
+      .def_readonly("cx0", &Layout::cx0)
+      .def_readonly("cx1", &Layout::cx1)
+      .def_readonly("cy0", &Layout::cy0)
+      .def_readonly("cy1", &Layout::cy1)
+      .def_readonly("cz0", &Layout::cz0)
+      .def_readonly("cz1", &Layout::cz1)
+      .def("off", [](const Layout& l, i64 x, i64 y, i64 z) { return l.off(x, y, z); });
+  m.def("make_layout", &make_layout, py::arg("problem"), py::arg("box"), py::arg("pitch_align") = 16);
+
+  py::class_<Face>(m, "Face")
+      .def_readonly("axis", &Face::axis)
+      .def_readonly("side", &Face::side)
+      .def_readonly("peer", &Face::peer)
+      .def_readonly("count", &Face::count)
+      .def_readonly("contiguous", &Face::contiguous)
+      .def_readonly("send_off", &Face::send_off)
+      .def_readonly("recv_off", &Face::recv_off)
+      .def_readonly("send_layer", &Face::send_layer)
+      .def_readonly("recv_layer", &Face::recv_layer)
+      .def_readonly("pack_off", &Face::pack_off);
+  py::class_<HaloPlan>(m, "HaloPlan")
+      .def_readonly("faces", &HaloPlan::faces)
+      .def_readonly("packed_doubles", &HaloPlan::packed_doubles);
+  m.def("make_halo_plan", &make_halo_plan);
+
+  py::class_<LBox>(m, "LBox")
+      .def(py::init([](i64 x0, i64 x1, i64 y0, i64 y1, i64 z0, i64 z1) { return LBox{x0, x1, y0, y1, z0, z1}; }))
+      .def_readwrite("x0", &LBox::x0)
+      .def_readwrite("x1", &LBox::x1)
+      .def_readwrite("y0", &LBox::y0)
+      .def_readwrite("y1", &LBox::y1)
+      .def_readwrite("z0", &LBox::z0)
+      .def_readwrite("z1", &LBox::z1)
+      .def("empty", &LBox::empty)
+      .def("count", &LBox::count);
+  m.def("compute_box", &compute_box);
+
+  // ---------------- CPU kernels ----------------
+  m.def("cpu_set_threads", &cpu_set_threads);
+  m.def("cpu_max_threads", &cpu_max_threads);
+  m.def("cpu_init_first", [](const Layout& l, const Coeffs& c, const darr& s, darr u0, darr u1) {
+    const double* sp = ro_ptr(s, l.N + 3, "s") + 1;
+    double* a = mut_ptr(u0, l.total, "u0");
+    double* b = mut_ptr(u1, l.total, "u1");
+    py::gil_scoped_release nogil;
+    cpu_init_first(l, c, sp, a, b);
+  });
+  m.def(
+      "cpu_leapfrog",
+      [](const Layout& l, const Coeffs& c, const darr& cur, darr old, const LBox& box, const darr& s, double ct,
+         bool check) -> py::object {
+        const double* cp = ro_ptr(cur, l.total, "cur");
+        double* op = mut_ptr(old, l.total, "old");
+        const double* sp = ro_ptr(s, l.N + 3, "s") + 1;
+        ErrAcc acc;
+        {
+          py::gil_scoped_release nogil;
+          cpu_leapfrog(l, c, cp, op, box, sp, ct, check ? &acc : nullptr);
+        }
+        if (!check) return py::none();
+        return py::make_tuple(acc.max, acc.sum);
+      },
+      py::arg("layout"), py::arg("coeffs"), py::arg("cur"), py::arg("old"), py::arg("box"), py::arg("s"),
+      py::arg("ct") = 0.0, py::arg("check") = false);
+  m.def("cpu_error", [](const Layout& l, const darr& u, const LBox& box, const darr& s, double ct) {
+    ErrAcc acc;
+    cpu_error(l, ro_ptr(u, l.total, "u"), box, ro_ptr(s, l.N + 3, "s") + 1, ct, &acc);
+    return py::make_tuple(acc.max, acc.sum);
+  });
+  m.def("cpu_pack_face", [](const Layout& l, const Face& f, const darr& u, darr buf) {
+    cpu_pack_face(l, f, ro_ptr(u, l.total, "u"), mut_ptr(buf, f.count, "buf"));
+  });
+  m.def("cpu_unpack_face", [](const Layout& l, const Face& f, const darr& buf, darr u) {
+    cpu_unpack_face(l, f, ro_ptr(buf, f.count, "buf"), mut_ptr(u, l.total, "u"));
+  });
+
+  py::class_<CpuSolver>(m, "CpuSolver")
+      .def(py::init<const Problem&, int, int>(), py::arg("problem"), py::arg("check_every") = 2,
+           py::arg("threads") = 0)
+      .def("run",
+           [](CpuSolver& s) {
+             CpuResult r;
+             {
+               py::gil_scoped_release nogil;
+               r = s.run();
+             }
+             py::dict d;
+             d["steps"] = r.steps;
+             d["max_err"] = r.max_err;
+             d["rms_err"] = r.rms_err;
+             d["solve_s"] = r.solve_s;
+             d["init_s"] = r.init_s;
+             d["compute_s"] = r.compute_s;
+             d["finite"] = r.finite;
+             return d;
+           })
+      .def("field",
+           [](const CpuSolver& s, int which) {
+             const auto& v = s.field(which);
+             return darr(static_cast<py::ssize_t>(v.size()), v.data());
+           })
+      .def_property_readonly("layout", &CpuSolver::layout)
+      .def("check_steps", &CpuSolver::check_steps);
+
+  // ---------------- GPU ----------------
+  m.def("gpu_device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;
+    }
+    return n;
+  });
+  m.def("gpu_set_device", [](int d) { W3D_HIP(hipSetDevice(d)); });
+  m.def("gpu_synchronize", []() { W3D_HIP(hipDeviceSynchronize()); });
+  m.def("gpu_arch", []() {
+    int d = 0;
+    W3D_HIP(hipGetDevice(&d));
+    hipDeviceProp_t p;
+    W3D_HIP(hipGetDeviceProperties(&p, d));
+    return std::string(p.gcnArchName);
+  });
+
+  py::class_<LeapfrogTiling>(m, "LeapfrogTiling")
+      .def(py::init<>())
+      .def_readwrite("ty", &LeapfrogTiling::ty)
+      .def_readwrite("target_blocks", &LeapfrogTiling::target_blocks)
+      .def_readwrite("xcd_remap", &LeapfrogTiling::xcd_remap)
+      .def_readwrite("nt_store", &LeapfrogTiling::nt_store);
+
+  m.def("gpu_init_first", [](const Layout& l, const Coeffs& c, std::uintptr_t s, std::uintptr_t u0, std::uintptr_t u1,
+                             std::uintptr_t stream) {
+    launch_init_first(l, c, dptr<const double>(s) + 1, dptr<double>(u0), dptr<double>(u1), sptr(stream));
+  });
+  m.def("gpu_leapfrog_blocks", [](const Layout& l, const std::vector<LBox>& boxes, const LeapfrogTiling& t) {
+    return leapfrog_blocks(l, boxes.data(), static_cast<int>(boxes.size()), t);
+  });
+  m.def("gpu_leapfrog",
+        [](const Layout& l, const Coeffs& c, std::uintptr_t cur, std::uintptr_t old, const std::vector<LBox>& boxes,
+           std::uintptr_t s, double ct, std::uintptr_t partials, const LeapfrogTiling& t, std::uintptr_t stream) {
+          launch_leapfrog(l, c, dptr<const double>(cur), dptr<double>(old), boxes.data(),
+                          static_cast<int>(boxes.size()), dptr<const double>(s) + 1, ct, dptr<Partial>(partials), t,
+                          sptr(stream));
+        });
+  m.def("gpu_error_blocks", &error_blocks);
+  m.def("gpu_error", [](const Layout& l, std::uintptr_t u, const LBox& b, std::uintptr_t s, double ct,
+                        std::uintptr_t partials, std::uintptr_t stream) {
+    launch_error(l, dptr<const double>(u), b, dptr<const double>(s) + 1, ct, dptr<Partial>(partials), sptr(stream));
+  });
+  m.def("gpu_reduce", [](std::uintptr_t partials, int n, std::uintptr_t out, std::uintptr_t stream) {
+    launch_reduce(dptr<const Partial>(partials), n, dptr<Partial>(out), sptr(stream));
+  });
+  m.def("gpu_pack", [](const Layout& l, const HaloPlan& p, std::uintptr_t u, std::uintptr_t buf, std::uintptr_t st) {
+    launch_pack(l, p, dptr<const double>(u), dptr<double>(buf), sptr(st));
+  });
+  m.def("gpu_unpack", [](const Layout& l, const HaloPlan& p, std::uintptr_t buf, std::uintptr_t u, std::uintptr_t st) {
+    launch_unpack(l, p, dptr<const double>(buf), dptr<double>(u), sptr(st));
+  });
+
+  py::class_<SolverOptions>(m, "SolverOptions")
+      .def(py::init<>())
+      .def_readwrite("decomp", &SolverOptions::decomp)
+      .def_readwrite("check_every", &SolverOptions::check_every)
+      .def_readwrite("overlap", &SolverOptions::overlap)
+      .def_readwrite("graph", &SolverOptions::graph)
+      .def_readwrite("timers", &SolverOptions::timers)
+      .def_readwrite("tiling", &SolverOptions::tiling);
+
+  py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
+      .def(py::init([](int rank, int world, py::bytes uid) {
+             std::string s = uid;
+             py::gil_scoped_release nogil;
+             return std::make_shared<Comm>(rank, world, s);
+           }),
+           py::arg("rank"), py::arg("world"), py::arg("unique_id"))
+      .def_static("make_unique_id", []() { return py::bytes(Comm::make_unique_id()); })
+      .def_property_readonly("rank", &Comm::rank)
+      .def_property_readonly("world", &Comm::world)
+      .def("check_async", &Comm::check_async);
+
+  py::class_<GpuSolver>(m, "GpuSolver")
+      .def(py::init([](const Problem& p, const SolverOptions& o, int rank, int world, std::shared_ptr<Comm> c) {
+             return std::make_unique<GpuSolver>(p, o, rank, world, std::move(c));
+           }),
+           py::arg("problem"), py::arg("options"), py::arg("rank") = 0, py::arg("world") = 1,
+           py::arg("comm") = nullptr)
+      .def("run",
+           [](GpuSolver& s) {
+             RunResult r;
+             {
+               py::gil_scoped_release nogil;
+               r = s.run();
+             }
+             return result_dict(r);
+           })
+      .def("download",
+           [](const GpuSolver& s, int which) {
+             auto v = s.download(which);
+             return darr(static_cast<py::ssize_t>(v.size()), v.data());
+           },
+           py::arg("which") = 0)
+      .def_property_readonly("layout", &GpuSolver::layout)
+      .def_property_readonly("dims", &GpuSolver::dims)
+      .def_property_readonly("halo", &GpuSolver::halo)
+      .def_property_readonly("rank", &GpuSolver::rank)
+      .def_property_readonly("world", &GpuSolver::world)
+      .def("shell_boxes", &GpuSolver::shell_boxes)
+      .def("interior_box", &GpuSolver::interior_box)
+      .def("check_steps", &GpuSolver::check_steps)
+      .def("device_bytes", &GpuSolver::device_bytes)
+      .def_property_readonly("graph_enabled", [](const GpuSolver& s) { return s.options().graph; });
+}

@@ -1,0 +1,333 @@
+// GPU solver runtime. See wave3d/solver.hpp.
+#include "wave3d/solver.hpp"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <thread>
+
+namespace wave3d {
+
+#define W3D_NCCL(expr)                                                                               \
+  do {                                                                                               \
+    ncclResult_t _r = (expr);                                                                        \
+    if (_r != ncclSuccess) ::wave3d::fail(std::string(#expr) + ": " + ncclGetErrorString(_r));        \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------------------------------
+// Comm
+// ------------------------------------------------------------------------------------------------------------------
+std::string Comm::make_unique_id() {
+  ncclUniqueId id;
+  W3D_NCCL(ncclGetUniqueId(&id));
+  return std::string(id.internal, sizeof(id.internal));
+}
+
+Comm::Comm(int rank, int world, const std::string& unique_id) : rank_(rank), world_(world) {
+  ncclUniqueId id;
+  W3D_REQUIRE(unique_id.size() == sizeof(id.internal), "bad RCCL unique id size");
+  std::memcpy(id.internal, unique_id.data(), sizeof(id.internal));
+  ncclComm_t c = nullptr;
+  W3D_NCCL(ncclCommInitRank(&c, world, id, rank));
+  comm_ = c;
+}
+
+Comm::~Comm() {
+  if (comm_) ncclCommDestroy(static_cast<ncclComm_t>(comm_));
+}
+
+void Comm::check_async() const {
+  ncclResult_t st = ncclSuccess;
+  W3D_NCCL(ncclCommGetAsyncError(static_cast<ncclComm_t>(comm_), &st));
+  if (st != ncclSuccess && st != ncclInProgress) fail(std::string("RCCL async error: ") + ncclGetErrorString(st));
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// GpuSolver
+// ------------------------------------------------------------------------------------------------------------------
+namespace {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Wait for a stream while polling RCCL for asynchronous failures (a dead peer must not hang the job forever).
+void wait_stream(hipStream_t s, const Comm* comm, double timeout_s) {
+  const double t0 = now_s();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) fail(std::string("stream failed: ") + hipGetErrorString(e));
+    if (comm) comm->check_async();
+    if (now_s() - t0 > timeout_s) fail("timed out waiting for the GPU (halo exchange stuck?)");
+    std::this_thread::yield();
+  }
+}
+
+}  // namespace
+
+GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, int world, std::shared_ptr<Comm> comm)
+    : prob_(prob), opt_(opt), coef_(Coeffs::from(prob)), rank_(rank), world_(world), comm_(std::move(comm)) {
+  prob_.validate();
+  W3D_REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
+  W3D_REQUIRE(world == 1 || comm_, "world > 1 needs an RCCL communicator");
+  dims_ = parse_dims(opt_.decomp, world, prob_.N);
+  const Box box = rank_box(prob_, dims_, rank);
+  W3D_REQUIRE(box.nx() >= 1 && box.ny() >= 1 && box.nz() >= 1,
+              "decomposition leaves a rank without nodes; use fewer ranks or a larger N");
+  lay_ = make_layout(prob_, box);
+  plan_ = make_halo_plan(lay_, dims_, rank);
+  full_ = compute_box(lay_);
+
+  // interior = compute box minus one layer on every side that has a neighbour; shell = the rest, in ≤6 disjoint boxes
+  bool nb[3][2];
+  for (int a = 0; a < 3; ++a)
+    for (int s = 0; s < 2; ++s) nb[a][s] = neighbor_rank(dims_, rank, a, s) >= 0;
+  interior_ = full_;
+  if (nb[0][0]) interior_.x0 += 1;
+  if (nb[0][1]) interior_.x1 -= 1;
+  if (nb[1][0]) interior_.y0 += 1;
+  if (nb[1][1]) interior_.y1 -= 1;
+  if (nb[2][0]) interior_.z0 += 1;
+  if (nb[2][1]) interior_.z1 -= 1;
+  auto push = [&](LBox b) {
+    if (!b.empty()) shell_.push_back(b);
+  };
+  if (!full_.empty()) {
+    const i64 ix0 = imin(imax(interior_.x0, full_.x0), full_.x1), ix1 = imax(interior_.x1, ix0);
+    const i64 iy0 = imin(imax(interior_.y0, full_.y0), full_.y1), iy1 = imax(interior_.y1, iy0);
+    if (nb[0][0]) push(LBox{full_.x0, full_.x0 + 1, full_.y0, full_.y1, full_.z0, full_.z1});
+    if (nb[0][1]) push(LBox{imax(full_.x1 - 1, full_.x0 + (nb[0][0] ? 1 : 0)), full_.x1, full_.y0, full_.y1, full_.z0, full_.z1});
+    if (nb[1][0]) push(LBox{ix0, ix1, full_.y0, full_.y0 + 1, full_.z0, full_.z1});
+    if (nb[1][1]) push(LBox{ix0, ix1, imax(full_.y1 - 1, full_.y0 + (nb[1][0] ? 1 : 0)), full_.y1, full_.z0, full_.z1});
+    if (nb[2][0]) push(LBox{ix0, ix1, iy0, iy1, full_.z0, full_.z0 + 1});
+    if (nb[2][1]) push(LBox{ix0, ix1, iy0, iy1, imax(full_.z1 - 1, full_.z0 + (nb[2][0] ? 1 : 0)), full_.z1});
+  }
+  if (interior_.x1 < interior_.x0 || interior_.y1 < interior_.y0 || interior_.z1 < interior_.z0) interior_ = LBox{};
+
+  // device memory
+  W3D_HIP(hipStreamCreateWithFlags(&s0_, hipStreamNonBlocking));
+  W3D_HIP(hipStreamCreateWithFlags(&s1_, hipStreamNonBlocking));
+  W3D_HIP(hipEventCreateWithFlags(&ev_shell_, hipEventDisableTiming));
+  W3D_HIP(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
+  for (int b = 0; b < 2; ++b) {
+    W3D_HIP(hipMalloc(&u_[b], static_cast<size_t>(lay_.bytes())));
+    W3D_HIP(hipMemset(u_[b], 0, static_cast<size_t>(lay_.bytes())));
+  }
+  const std::vector<double> s = sin_table_ext(prob_);
+  W3D_HIP(hipMalloc(&d_s_, s.size() * sizeof(double)));
+  W3D_HIP(hipMemcpy(d_s_, s.data(), s.size() * sizeof(double), hipMemcpyHostToDevice));
+  if (plan_.packed_doubles > 0) {
+    W3D_HIP(hipMalloc(&send_buf_, static_cast<size_t>(plan_.packed_doubles) * sizeof(double)));
+    W3D_HIP(hipMalloc(&recv_buf_, static_cast<size_t>(plan_.packed_doubles) * sizeof(double)));
+  }
+  const int n_full = leapfrog_blocks(lay_, &full_, 1, opt_.tiling);
+  const int n_split = leapfrog_blocks(lay_, shell_.data(), static_cast<int>(shell_.size()), opt_.tiling) +
+                      leapfrog_blocks(lay_, &interior_, 1, opt_.tiling);
+  n_partials_ = std::max({n_full, n_split, error_blocks(lay_, full_), 1});
+  W3D_HIP(hipMalloc(&partials_, static_cast<size_t>(n_partials_) * sizeof(Partial)));
+  W3D_HIP(hipMalloc(&errlog_, static_cast<size_t>(prob_.K + 1) * sizeof(Partial)));
+  W3D_HIP(hipMalloc(&errall_, static_cast<size_t>(world_) * (prob_.K + 1) * sizeof(Partial)));
+  ct_.resize(static_cast<size_t>(prob_.K + 1));
+  for (int n = 0; n <= prob_.K; ++n) ct_[static_cast<size_t>(n)] = time_factor(prob_, n);
+  if (opt_.timers) opt_.graph = false;
+}
+
+GpuSolver::~GpuSolver() {
+  if (graph_exec_) hipGraphExecDestroy(graph_exec_);
+  for (double* p : {u_[0], u_[1], d_s_, send_buf_, recv_buf_})
+    if (p) hipFree(p);
+  if (partials_) hipFree(partials_);
+  if (errlog_) hipFree(errlog_);
+  if (errall_) hipFree(errall_);
+  for (hipEvent_t e : tev_) hipEventDestroy(e);
+  if (ev_shell_) hipEventDestroy(ev_shell_);
+  if (ev_halo_) hipEventDestroy(ev_halo_);
+  if (s0_) hipStreamDestroy(s0_);
+  if (s1_) hipStreamDestroy(s1_);
+}
+
+size_t GpuSolver::device_bytes() const {
+  return 2 * static_cast<size_t>(lay_.bytes()) + 2 * static_cast<size_t>(plan_.packed_doubles) * sizeof(double) +
+         static_cast<size_t>(n_partials_) * sizeof(Partial) + static_cast<size_t>(prob_.N + 3) * sizeof(double);
+}
+
+std::vector<int> GpuSolver::check_steps() const {
+  std::vector<int> v;
+  const int ce = opt_.check_every;
+  for (int n = 1; n <= prob_.K; ++n)
+    if ((ce > 0 && n % ce == 0) || n == prob_.K) v.push_back(n);
+  return v;
+}
+
+void GpuSolver::exchange(double* field, hipStream_t st) {
+  if (!plan_.any()) return;
+  if (plan_.packed_doubles > 0) launch_pack(lay_, plan_, field, send_buf_, st);
+  ncclComm_t c = static_cast<ncclComm_t>(comm_->raw());
+  W3D_NCCL(ncclGroupStart());
+  for (const Face& f : plan_.faces) {
+    const double* sp = f.contiguous ? field + f.send_off : send_buf_ + f.pack_off;
+    double* rp = f.contiguous ? field + f.recv_off : recv_buf_ + f.pack_off;
+    W3D_NCCL(ncclSend(sp, static_cast<size_t>(f.count), ncclFloat64, f.peer, c, st));
+    W3D_NCCL(ncclRecv(rp, static_cast<size_t>(f.count), ncclFloat64, f.peer, c, st));
+  }
+  W3D_NCCL(ncclGroupEnd());
+  if (plan_.packed_doubles > 0) launch_unpack(lay_, plan_, recv_buf_, field, st);
+}
+
+void GpuSolver::enqueue_solve() {
+  const int K = prob_.K;
+  const double* s = d_s_ + 1;
+  const auto checks = check_steps();
+  std::vector<char> is_check(static_cast<size_t>(K + 1), 0);
+  for (int n : checks) is_check[static_cast<size_t>(n)] = 1;
+  auto tev = [&](int i, hipStream_t st) {
+    if (opt_.timers) W3D_HIP(hipEventRecord(tev_[static_cast<size_t>(i)], st));
+  };
+
+  tev(0, s0_);
+  W3D_HIP(hipMemsetAsync(errlog_, 0, static_cast<size_t>(K + 1) * sizeof(Partial), s0_));
+  launch_init_first(lay_, coef_, s, u_[0], u_[1], s0_);
+  if (is_check[1]) {
+    launch_error(lay_, u_[1], full_, s, ct_[1], partials_, s0_);
+    launch_reduce(partials_, error_blocks(lay_, full_), errlog_ + 1, s0_);
+  }
+  tev(1, s0_);
+  const bool split = opt_.overlap && plan_.any();
+  const int n_shell = leapfrog_blocks(lay_, shell_.data(), static_cast<int>(shell_.size()), opt_.tiling);
+  const int n_int = leapfrog_blocks(lay_, &interior_, 1, opt_.tiling);
+  const int n_full = leapfrog_blocks(lay_, &full_, 1, opt_.tiling);
+  int cur = 1, old = 0;
+  for (int n = 1; n <= K - 1; ++n) {
+    const bool chk = is_check[static_cast<size_t>(n + 1)] != 0;
+    Partial* pp = chk ? partials_ : nullptr;
+    const double ct = ct_[static_cast<size_t>(n + 1)];
+    const bool last = n == K - 1;
+    if (split) {
+      launch_leapfrog(lay_, coef_, u_[cur], u_[old], shell_.data(), static_cast<int>(shell_.size()), s, ct, pp,
+                      opt_.tiling, s0_);
+      if (!last) {
+        W3D_HIP(hipEventRecord(ev_shell_, s0_));
+        W3D_HIP(hipStreamWaitEvent(s1_, ev_shell_, 0));
+        exchange(u_[old], s1_);
+        W3D_HIP(hipEventRecord(ev_halo_, s1_));
+      }
+      launch_leapfrog(lay_, coef_, u_[cur], u_[old], &interior_, 1, s, ct, pp ? pp + n_shell : nullptr, opt_.tiling,
+                      s0_);
+      if (!last) W3D_HIP(hipStreamWaitEvent(s0_, ev_halo_, 0));
+      if (chk) launch_reduce(partials_, n_shell + n_int, errlog_ + n + 1, s0_);
+    } else {
+      if (n >= 2) exchange(u_[cur], s0_);
+      launch_leapfrog(lay_, coef_, u_[cur], u_[old], &full_, 1, s, ct, pp, opt_.tiling, s0_);
+      if (chk) launch_reduce(partials_, n_full, errlog_ + n + 1, s0_);
+    }
+    std::swap(cur, old);
+  }
+  final_buf_ = cur;
+  tev(2, s0_);
+}
+
+void GpuSolver::gather_errors(RunResult& r) {
+  const int K = prob_.K;
+  const size_t per = static_cast<size_t>(K + 1);
+  std::vector<Partial> host(per * static_cast<size_t>(world_));
+  if (world_ > 1) {
+    W3D_NCCL(ncclAllGather(errlog_, errall_, 2 * per, ncclFloat64, static_cast<ncclComm_t>(comm_->raw()), s0_));
+    W3D_HIP(hipMemcpyAsync(host.data(), errall_, host.size() * sizeof(Partial), hipMemcpyDeviceToHost, s0_));
+  } else {
+    W3D_HIP(hipMemcpyAsync(host.data(), errlog_, per * sizeof(Partial), hipMemcpyDeviceToHost, s0_));
+  }
+  wait_stream(s0_, comm_.get(), 600.0);
+  const double n_int = static_cast<double>(prob_.N - 1);
+  const double denom = n_int * n_int * n_int;
+  for (int n : check_steps()) {
+    double m = 0.0, sum = 0.0;
+    for (int q = 0; q < world_; ++q) {  // fixed rank order
+      const Partial& v = host[static_cast<size_t>(q) * per + static_cast<size_t>(n)];
+      m = v.x > m || std::isnan(v.x) ? v.x : m;
+      sum += v.y;
+    }
+    r.steps.push_back(n);
+    r.max_err.push_back(m);
+    r.rms_err.push_back(std::sqrt(sum / denom));
+    if (!std::isfinite(m) || !std::isfinite(sum)) r.finite = false;
+  }
+}
+
+RunResult GpuSolver::run() {
+  RunResult r;
+  if (opt_.timers && tev_.empty()) {
+    tev_.resize(3);
+    for (auto& e : tev_) W3D_HIP(hipEventCreate(&e));
+  }
+  if (opt_.graph && !graph_exec_) {
+    // capture once (outside the timed region of later runs); fall back to eager launches if capture is refused
+    hipGraph_t g = nullptr;
+    bool ok = hipStreamBeginCapture(s0_, hipStreamCaptureModeThreadLocal) == hipSuccess;
+    if (ok) {
+      try {
+        enqueue_solve();
+      } catch (...) {
+        ok = false;
+      }
+      const hipError_t e = hipStreamEndCapture(s0_, &g);
+      ok = ok && e == hipSuccess && g != nullptr;
+    }
+    if (ok) ok = hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0) == hipSuccess;
+    if (g) hipGraphDestroy(g);
+    (void)hipGetLastError();
+    if (!ok) {
+      graph_exec_ = nullptr;
+      opt_.graph = false;
+    }
+  }
+  const double t0 = now_s();
+  if (graph_exec_)
+    W3D_HIP(hipGraphLaunch(graph_exec_, s0_));
+  else
+    enqueue_solve();
+  gather_errors(r);
+  r.solve_s = now_s() - t0;
+  if (opt_.timers) {
+    float a = 0, b = 0;
+    W3D_HIP(hipEventElapsedTime(&a, tev_[0], tev_[1]));
+    W3D_HIP(hipEventElapsedTime(&b, tev_[1], tev_[2]));
+    r.phases.init_ms = a;
+    r.phases.interior_ms = b;
+  }
+  return r;
+}
+
+std::vector<double> GpuSolver::download(int which) const {
+  std::vector<double> h(static_cast<size_t>(lay_.total));
+  const double* src = u_[which == 0 ? final_buf_ : 1 - final_buf_];
+  W3D_HIP(hipDeviceSynchronize());
+  W3D_HIP(hipMemcpy(h.data(), src, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+  return h;
+}
+
+}  // namespace wave3d
+
+namespace wave3d {
+
+double comm_allreduce(const Comm& c, double v, bool max_op) {
+  static thread_local hipStream_t st = nullptr;
+  static thread_local double* buf = nullptr;
+  if (!st) {
+    W3D_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    W3D_HIP(hipMalloc(&buf, sizeof(double)));
+  }
+  W3D_HIP(hipMemcpyAsync(buf, &v, sizeof(double), hipMemcpyHostToDevice, st));
+  W3D_NCCL(ncclAllReduce(buf, buf, 1, ncclFloat64, max_op ? ncclMax : ncclSum, static_cast<ncclComm_t>(c.raw()), st));
+  double out = 0.0;
+  W3D_HIP(hipMemcpyAsync(&out, buf, sizeof(double), hipMemcpyDeviceToHost, st));
+  wait_stream(st, &c, 600.0);
+  return out;
+}
+
+void comm_barrier(const Comm& c) { (void)comm_allreduce(c, 0.0, false); }
+
+}  // namespace wave3d

@@ -1,0 +1,162 @@
+"""High-level entry point: ``Solver`` (persistent, for repeated timed solves) and ``solve()`` (one shot).
+
+Backends / transports:
+
+=========  ==========  =============================================================================================
+backend    transport   what runs
+=========  ==========  =============================================================================================
+hip        rccl        native C++ GpuSolver: HIP kernels, C++ step loop, RCCL P2P halos on a side stream overlapped
+                       with the interior update, whole solve captured in one hipGraph (production path, any world)
+hip        torch       Python step loop, HIP kernels, halos over torch.distributed (RCCL, or gloo staged via host)
+cpu        native      C++ CpuSolver, OpenMP (the reference's sequential / OpenMP programs), world == 1
+cpu        torch       Python step loop, native OpenMP kernels, halos over torch.distributed gloo (MPI analogue)
+torch      -           plain PyTorch fp64 reference solver (oracle), world == 1
+=========  ==========  =============================================================================================
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+from ._native import load
+from .models.wave3d import ProblemSpec, torch_reference_solve
+
+
+@dataclass
+class SolveResult:
+    spec: ProblemSpec
+    backend: str
+    transport: str
+    world: int
+    dims: tuple
+    steps: list
+    max_err: list
+    rms_err: list
+    solve_s: float
+    finite: bool = True
+    extra: dict = field(default_factory=dict)
+
+    def lines(self) -> list[str]:
+        from .utils.report import error_line
+
+        return [error_line(n, n * self.spec.tau, m, r) for n, m, r in zip(self.steps, self.max_err, self.rms_err)]
+
+    @property
+    def gcell_per_s(self) -> float:
+        return self.spec.cell_updates / self.solve_s / 1e9 if self.solve_s > 0 else float("nan")
+
+
+def _resolve(backend: str, transport: str, world: int) -> tuple[str, str]:
+    if backend == "auto":
+        backend = "hip" if torch.cuda.is_available() else "cpu"
+    if transport == "auto":
+        transport = {"hip": "rccl", "cpu": "native" if world == 1 else "torch", "torch": "none"}[backend]
+    ok = {("hip", "rccl"), ("hip", "torch"), ("cpu", "native"), ("cpu", "torch"), ("torch", "none")}
+    if (backend, transport) not in ok:
+        raise ValueError(f"unsupported backend/transport combination {backend}/{transport}")
+    if backend == "cpu" and transport == "native" and world > 1:
+        raise ValueError("the native CPU solver is single-rank; use transport='torch' for world > 1")
+    if backend == "torch" and world > 1:
+        raise ValueError("the torch reference solver is single-rank")
+    return backend, transport
+
+
+class Solver:
+    """Construct once (allocation, communicator, graph capture on the first run), then ``run()`` repeatedly."""
+
+    def __init__(self, spec: ProblemSpec, backend: str = "auto", transport: str = "auto", decomp: str = "slab",
+                 rank: int | None = None, world: int | None = None, device: int | None = None,
+                 overlap: bool = True, graph: bool = True, threads: int = 0, tiling: dict | None = None,
+                 comm=None, group=None, stage_via_host: bool = False, force: bool = False):
+        import torch.distributed as dist
+
+        if not spec.cfl_ok and not force:
+            raise ValueError(f"CFL violated: courant = {spec.courant:.4f} > 1 (tau_max = {spec.tau_max:.3e}); "
+                             "pass force=True to run anyway")
+        if rank is None or world is None:
+            if dist.is_initialized():
+                rank, world = dist.get_rank(), dist.get_world_size()
+            else:
+                rank, world = 0, 1
+        self.spec, self.rank, self.world = spec, rank, world
+        self.backend, self.transport = _resolve(backend, transport, world)
+        self.decomp = decomp
+        self._impl = None
+        C = load()
+        if self.backend == "hip":
+            if not torch.cuda.is_available():
+                raise RuntimeError("backend 'hip' needs a GPU")
+            dev = device if device is not None else (rank % torch.cuda.device_count())
+            torch.cuda.set_device(dev)
+            C.gpu_set_device(dev)
+            self.device = torch.device("cuda", dev)
+        else:
+            self.device = torch.device("cpu")
+        if self.backend == "hip" and self.transport == "rccl":
+            from .parallel.rccl import make_comm
+
+            opts = C.SolverOptions()
+            opts.decomp = decomp
+            opts.check_every = spec.check_every
+            opts.overlap = overlap
+            opts.graph = graph
+            if tiling:
+                for k, v in tiling.items():
+                    setattr(opts.tiling, k, v)
+            if comm is None and world > 1:
+                comm = make_comm(rank, world, group)
+            self.comm = comm
+            self._impl = C.GpuSolver(spec.native(), opts, rank, world, comm)
+            self.dims = self._impl.dims.as_tuple()
+        elif self.transport in ("torch",):
+            from .parallel.dist_solver import TorchDistSolver
+
+            self._impl = TorchDistSolver(spec, rank, world, decomp, self.device, group, stage_via_host, threads)
+            self.dims = self._impl.plan.dims
+        elif self.backend == "cpu":
+            self._impl = C.CpuSolver(spec.native(), spec.check_every, threads)
+            self.dims = (1, 1, 1)
+        else:
+            self.dims = (1, 1, 1)
+
+    def run(self) -> SolveResult:
+        if self.backend == "torch":
+            import time
+
+            t0 = time.perf_counter()
+            errs = torch_reference_solve(self.spec)
+            dt = time.perf_counter() - t0
+            steps = sorted(errs)
+            return SolveResult(self.spec, "torch", "none", 1, (1, 1, 1), steps, [errs[n][0] for n in steps],
+                               [errs[n][1] for n in steps], dt,
+                               all(math.isfinite(v) for n in steps for v in errs[n]))
+        r = self._impl.run()
+        return SolveResult(self.spec, self.backend, self.transport, self.world, tuple(self.dims), list(r["steps"]),
+                           list(r["max_err"]), list(r["rms_err"]), float(r["solve_s"]), bool(r["finite"]),
+                           {k: v for k, v in r.items() if k not in ("steps", "max_err", "rms_err", "solve_s",
+                                                                    "finite")})
+
+    @property
+    def native(self):
+        return self._impl
+
+    def owned_field(self, which: int = 0) -> torch.Tensor:
+        """This rank's owned nodes of u^K (which=0) or u^{K-1} (which=1) as a CPU (nx, ny, nz) float64 tensor."""
+        from .ops.stencil import grid_view
+
+        if self.transport == "torch":
+            return self._impl.owned_field(which)
+        if self.backend == "hip":
+            flat = torch.from_numpy(self._impl.download(which))
+            lay = self._impl.layout
+        else:
+            flat = torch.from_numpy(self._impl.field(which).copy())
+            lay = self._impl.layout
+        g = grid_view(lay, flat)
+        return g[1:1 + int(lay.nx), 1:1 + int(lay.ny), 1:1 + int(lay.nz)].clone()
+
+
+def solve(spec: ProblemSpec, **kw) -> SolveResult:
+    return Solver(spec, **kw).run()

@@ -1,0 +1,124 @@
+"""HIP kernel numerics vs the native CPU path (bit-exact, same op order, -ffp-contract=off) and vs a plain PyTorch
+fp64 reference of the same op."""
+import math
+
+import pytest
+import torch
+
+from mpi_cuda_amd.ops import stencil as ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(C, N, world=1, rank=0, decomp="slab", tau=1e-3):
+    prob = C.Problem(N, tau, 20, 1.0)
+    dims = C.parse_dims(decomp, world, N)
+    lay = C.make_layout(prob, C.rank_box(prob, dims, rank))
+    return prob, C.Coeffs.from_problem(prob), lay, dims
+
+
+@pytest.mark.parametrize("N,world,rank,decomp", [(32, 1, 0, "slab"), (47, 1, 0, "slab"), (64, 2, 1, "slab"),
+                                                 (50, 8, 5, "block"), (33, 4, 0, "1x2x2"), (129, 3, 2, "slab")])
+def test_init_first_bitexact(gpu, N, world, rank, decomp):
+    C = gpu
+    prob, co, lay, _ = _setup(C, N, world, rank, decomp)
+    s_cpu = ops.sin_table_ext(prob)
+    a0, a1 = ops.alloc_field(lay), ops.alloc_field(lay)
+    ops.init_first(lay, co, s_cpu, a0, a1)
+    s_gpu = s_cpu.cuda()
+    g0, g1 = ops.alloc_field(lay, "cuda"), ops.alloc_field(lay, "cuda")
+    ops.init_first(lay, co, s_gpu, g0, g1)
+    torch.cuda.synchronize()
+    assert torch.equal(ops.to_grid(lay, g0).cpu(), ops.to_grid(lay, a0))
+    assert torch.equal(ops.to_grid(lay, g1).cpu(), ops.to_grid(lay, a1))
+
+
+TILINGS = [dict(ty=8), dict(ty=4), dict(ty=16), dict(ty=8, xcd_remap=False), dict(ty=8, nt_store=True),
+           dict(ty=4, target_blocks=64)]
+
+
+@pytest.mark.parametrize("tiling", TILINGS)
+@pytest.mark.parametrize("N,world,rank,decomp", [(40, 1, 0, "slab"), (61, 2, 0, "slab"), (70, 8, 3, "block"),
+                                                 (130, 1, 0, "slab")])
+def test_leapfrog_bitexact_and_vs_torch(gpu, tiling, N, world, rank, decomp):
+    C = gpu
+    prob, co, lay, _ = _setup(C, N, world, rank, decomp)
+    torch.manual_seed(N + rank)
+    # random fields (ghosts included) so every neighbour access is exercised
+    cur = torch.randn(int(lay.total), dtype=torch.float64)
+    old = torch.randn(int(lay.total), dtype=torch.float64)
+    box = C.compute_box(lay)
+    s = ops.sin_table_ext(prob)
+    ct = math.cos(prob.a_t * 5 * prob.tau)
+    old_cpu = old.clone()
+    e_cpu = ops.leapfrog(lay, co, cur, old_cpu, [box], s, ct, check=True)
+    t = C.LeapfrogTiling()
+    for k, v in tiling.items():
+        setattr(t, k, v)
+    cur_g, old_g = cur.cuda(), old.cuda()
+    e_gpu = ops.leapfrog(lay, co, cur_g, old_g, [box], s.cuda(), ct, check=True, tiling=t)
+    torch.cuda.synchronize()
+    # whole padded array must match: updated nodes bit-exact, everything else untouched
+    assert torch.equal(old_g.cpu(), old_cpu)
+    assert e_gpu[0] == e_cpu[0]
+    assert math.isclose(e_gpu[1], e_cpu[1], rel_tol=1e-12)
+    # PyTorch fp64 reference of the same op
+    ref = ops.ref_leapfrog_grid(ops.to_grid(lay, cur), ops.to_grid(lay, old), co.ihx2, co.ihy2, co.ihz2, co.tau2, box)
+    torch.testing.assert_close(ops.to_grid(lay, old_g.cpu()), ref, rtol=0, atol=1e-9)
+
+
+def test_leapfrog_subboxes(gpu):
+    """Several disjoint boxes in one launch (the shell of a block-decomposed rank) == one launch per box == CPU."""
+    C = gpu
+    prob, co, lay, _ = _setup(C, 90, 8, 6, "2x2x2")
+    torch.manual_seed(1)
+    cur = torch.randn(int(lay.total), dtype=torch.float64)
+    old = torch.randn(int(lay.total), dtype=torch.float64)
+    s = ops.sin_table_ext(prob)
+    full = C.compute_box(lay)
+    boxes = [C.LBox(full.x0, full.x0 + 1, full.y0, full.y1, full.z0, full.z1),
+             C.LBox(full.x0 + 1, full.x1, full.y0, full.y0 + 1, full.z0, full.z1),
+             C.LBox(full.x0 + 1, full.x1, full.y0 + 1, full.y1, full.z1 - 1, full.z1),
+             C.LBox(full.x0 + 3, full.x0 + 7, full.y0 + 5, full.y0 + 6, full.z0 + 3, full.z0 + 4)]
+    o_cpu = old.clone()
+    e_cpu = ops.leapfrog(lay, co, cur, o_cpu, boxes, s, 0.7, check=True)
+    o_gpu = old.cuda()
+    e_gpu = ops.leapfrog(lay, co, cur.cuda(), o_gpu, boxes, s.cuda(), 0.7, check=True)
+    torch.cuda.synchronize()
+    assert torch.equal(o_gpu.cpu(), o_cpu)
+    assert e_gpu[0] == e_cpu[0] and math.isclose(e_gpu[1], e_cpu[1], rel_tol=1e-12)
+
+
+def test_error_kernel(gpu):
+    C = gpu
+    prob, co, lay, _ = _setup(C, 77, 2, 1, "slab")
+    torch.manual_seed(3)
+    u = torch.randn(int(lay.total), dtype=torch.float64)
+    s = ops.sin_table_ext(prob)
+    box = C.compute_box(lay)
+    a = ops.error(lay, u, box, s, 0.3)
+    b = ops.error(lay, u.cuda(), box, s.cuda(), 0.3)
+    assert a[0] == b[0] and math.isclose(a[1], b[1], rel_tol=1e-12)
+
+
+@pytest.mark.parametrize("decomp,world,rank", [("2x2x2", 8, 3), ("1x2x3", 6, 4), ("block", 16, 9)])
+def test_pack_unpack(gpu, decomp, world, rank):
+    C = gpu
+    prob, co, lay, dims = _setup(C, 45, world, rank, decomp)
+    plan = C.make_halo_plan(lay, dims, rank)
+    torch.manual_seed(rank)
+    u = torch.randn(int(lay.total), dtype=torch.float64)
+    n = max(int(plan.packed_doubles), 1)
+    b_cpu = torch.zeros(n, dtype=torch.float64)
+    ops.pack(lay, plan, u, b_cpu)
+    b_gpu = torch.zeros(n, dtype=torch.float64, device="cuda")
+    ops.pack(lay, plan, u.cuda(), b_gpu)
+    torch.cuda.synchronize()
+    assert torch.equal(b_gpu.cpu(), b_cpu)
+    src = torch.randn(n, dtype=torch.float64)
+    v_cpu = u.clone()
+    ops.unpack(lay, plan, src, v_cpu)
+    v_gpu = u.cuda()
+    ops.unpack(lay, plan, src.cuda(), v_gpu)
+    torch.cuda.synchronize()
+    assert torch.equal(v_gpu.cpu(), v_cpu)

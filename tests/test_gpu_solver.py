@@ -1,0 +1,67 @@
+"""End-to-end native GPU solver: golden log, oracle, bit-exact vs CPU, graph == eager, native code actually loaded."""
+import math
+
+import pytest
+import torch
+
+from mpi_cuda_amd import ProblemSpec
+from mpi_cuda_amd.models.wave3d import REFERENCE_LOG_512, oracle_errors
+from mpi_cuda_amd.solver import Solver
+
+pytestmark = pytest.mark.gpu
+
+
+def test_native_extension_is_the_gpu_path(gpu):
+    assert gpu.__file__.endswith(".so")
+    assert gpu.gpu_arch().startswith("gfx950"), gpu.gpu_arch()
+
+
+@pytest.mark.parametrize("N,K", [(48, 10), (65, 7), (128, 20)])
+def test_gpu_matches_cpu_bitexact(gpu, N, K):
+    spec = ProblemSpec(N=N, tau=1e-3, K=K, check_every=1)
+    g = Solver(spec, backend="hip", device=0)
+    rg = g.run()
+    c = Solver(spec, backend="cpu")
+    rc = c.run()
+    assert rg.steps == rc.steps
+    assert rg.max_err == rc.max_err
+    for a, b in zip(rg.rms_err, rc.rms_err):
+        assert math.isclose(a, b, rel_tol=1e-12)
+    assert torch.equal(g.owned_field(0), c.owned_field(0))
+    assert torch.equal(g.owned_field(1), c.owned_field(1))
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_graph_and_eager_identical_and_repeatable(gpu, graph):
+    spec = ProblemSpec(N=96, tau=1e-3, K=12)
+    s = Solver(spec, backend="hip", device=0, graph=graph)
+    r1 = s.run()
+    f1 = s.owned_field(0)
+    r2 = s.run()
+    assert r1.max_err == r2.max_err and r1.rms_err == r2.rms_err
+    assert torch.equal(f1, s.owned_field(0))
+    ref = oracle_errors(spec)
+    for n, m, e in zip(r1.steps, r1.max_err, r1.rms_err):
+        assert math.isclose(m, ref[n][0], rel_tol=1e-6) and math.isclose(e, ref[n][1], rel_tol=1e-6)
+
+
+def test_golden_log_512(gpu):
+    """The reference's printed 512³ log (report.pdf p.15-16) to its 7 printed digits (±1 in the last place)."""
+    spec = ProblemSpec(N=512, tau=1e-3, K=20)
+    r = Solver(spec, backend="hip", device=0).run()
+    assert r.steps == [n for n, _, _ in REFERENCE_LOG_512]
+    for (n, m, e), gm, ge in zip(REFERENCE_LOG_512, r.max_err, r.rms_err):
+        assert abs(gm - m) <= 1.5e-6 * m + 2e-17, (n, gm, m)
+        assert abs(ge - e) <= 1.5e-6 * e + 2e-17, (n, ge, e)
+    lines = r.lines()
+    assert lines[-1] == "Step 20, t = 0.020000, Max Error = 3.960129e-09, L2 Error = 1.404229e-09"
+
+
+@pytest.mark.parametrize("tiling", [dict(ty=4), dict(ty=16, xcd_remap=False), dict(ty=8, nt_store=True)])
+def test_tilings_agree(gpu, tiling):
+    spec = ProblemSpec(N=100, tau=1e-3, K=8)
+    a = Solver(spec, backend="hip", device=0)
+    b = Solver(spec, backend="hip", device=0, tiling=tiling)
+    ra, rb = a.run(), b.run()
+    assert ra.max_err == rb.max_err
+    assert torch.equal(a.owned_field(0), b.owned_field(0))

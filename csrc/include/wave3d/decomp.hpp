@@ -54,14 +54,11 @@ inline Dims block_dims(int P, i64 N) {
       if ((P / px) % py) continue;
       const int pz = P / px / py;
       const double ax = n / px, ay = n / py, az = n / pz;
-      // faces actually exchanged: 2 per split axis
-      double cost = 0.0;
-      if (px > 1) cost += 2.0 * ay * az;
-      if (py > 1) cost += 2.0 * ax * az;
-      if (pz > 1) cost += 2.0 * ax * ay;
+      // faces of the busiest rank: one per axis split in two, two per axis split further
+      const double fx = px > 2 ? 2.0 : px - 1.0, fy = py > 2 ? 2.0 : py - 1.0, fz = pz > 2 ? 2.0 : pz - 1.0;
+      double cost = fx * ay * az + fy * ax * az + fz * ax * ay;
       // strided (y/z) faces cost more than contiguous x faces: packing + non-contiguous access
-      if (py > 1) cost += 0.25 * ax * az;
-      if (pz > 1) cost += 0.5 * ax * ay;
+      cost += 0.125 * fy * ax * az + 0.25 * fz * ax * ay;
       const bool better = best_cost < 0.0 || cost < best_cost - 1e-9 ||
                           (std::abs(cost - best_cost) <= 1e-9 && (px > best.px || (px == best.px && py > best.py)));
       if (better) {

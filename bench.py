@@ -32,6 +32,13 @@ REF_GCELL = {1: 512**3 * 20 / 0.752 / 1e9, 2: 512**3 * 20 / 0.505 / 1e9}
 REF_FINAL_LINF = 3.960129e-09  # report.pdf p.16 §4.3.1, step 20
 
 
+def _tiling(a) -> dict:
+    t = {"variant": a.variant}
+    if a.tile_rows:
+        t["rows" if a.variant == 1 else "ty"] = a.tile_rows
+    return t
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -45,7 +52,8 @@ def main() -> int:
     ap.add_argument("--transport", default="rccl", choices=["rccl", "torch"])
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--tile-rows", type=int, default=8)
+    ap.add_argument("--variant", type=int, default=1, help="leapfrog kernel (1 = register-queue, 0 = LDS tile)")
+    ap.add_argument("--tile-rows", type=int, default=0, help="rows per wave (v1) / per workgroup (v0); 0 = default")
     ap.add_argument("--cpu", action="store_true", help="CPU backend (contract test without a GPU)")
     ap.add_argument("--out", default="", help="also append the JSON line to this file")
     a = ap.parse_args()
@@ -67,7 +75,7 @@ def main() -> int:
     transport = ("torch" if world > 1 else "native") if a.cpu else a.transport
     solver = Solver(spec, backend=backend, transport=transport, decomp=a.decomp, rank=rank, world=world,
                     device=None if a.cpu else local, overlap=not a.no_overlap, graph=not a.no_graph,
-                    tiling={"ty": a.tile_rows})
+                    tiling=_tiling(a))
 
     def barrier_sync():
         if not a.cpu:

@@ -44,7 +44,10 @@ struct Args {
   int repeat = 1;
   int warmup = 0;
   int np = 0;
-  int tile_rows = 8;
+  int tile_rows = -1;
+  int variant = -1;
+  int target_blocks = 0;
+  int nt_store = -1;
   std::string json, dump;
   bool quiet = false;
 };
@@ -64,7 +67,10 @@ struct Args {
                "  --no-graph         eager launches instead of one captured hipGraph\n"
                "  --timers           per-phase GPU timers\n"
                "  --repeat R / --warmup W   timed / untimed solves (report min and mean)\n"
-               "  --tile-rows T      leapfrog tile rows (4, 8, 16)\n"
+               "  --variant V        leapfrog kernel: 1 = register-queue waves (default), 0 = LDS-staged tile\n"
+               "  --tile-rows T      rows per wave (v1: 1,2,4,8) or per workgroup (v0: 4,8,16)\n"
+               "  --target-blocks B  x-chunking target (waves for v1, workgroups for v0)\n"
+               "  --nt-store 0/1     non-temporal stores of u^{n+1} (default 1)\n"
                "  --json PATH        machine-readable summary (rank 0)\n"
                "  --dump PREFIX      write u^K: PREFIX[.rankR].bin (fp64, C order, owned nodes) + .json\n"
                "  --force            run even if the CFL condition is violated\n"
@@ -92,6 +98,9 @@ Args parse(int argc, char** argv) {
     else if (s == "--repeat") a.repeat = std::stoi(next());
     else if (s == "--warmup") a.warmup = std::stoi(next());
     else if (s == "--tile-rows") a.tile_rows = std::stoi(next());
+    else if (s == "--variant") a.variant = std::stoi(next());
+    else if (s == "--target-blocks") a.target_blocks = std::stoi(next());
+    else if (s == "--nt-store") a.nt_store = std::stoi(next());
     else if (s == "--json") a.json = next();
     else if (s == "--dump") a.dump = next();
     else if (s == "--force") a.force = true;
@@ -273,7 +282,10 @@ int run_gpu(const Args& a) {
   o.overlap = a.overlap;
   o.graph = a.graph;
   o.timers = a.timers;
-  o.tiling.ty = a.tile_rows;
+  if (a.variant >= 0) o.tiling.variant = a.variant;
+  if (a.tile_rows > 0) (o.tiling.variant == 1 ? o.tiling.rows : o.tiling.ty) = a.tile_rows;
+  o.tiling.target_blocks = a.target_blocks;
+  if (a.nt_store >= 0) o.tiling.nt_store = a.nt_store != 0;
   GpuSolver s(a.prob, o, rank, world, comm);
   size_t free_b = 0, total_b = 0;
   W3D_HIP(hipMemGetInfo(&free_b, &total_b));

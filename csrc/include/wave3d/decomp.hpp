@@ -111,9 +111,10 @@ inline int neighbor_rank(const Dims& d, int rank, int axis, int side) {
 
 // Local storage of one rank's box with a ghost layer of width 1 on every side.
 //   offset(ix,iy,iz) = (ix+1)·plane + (iy+1)·pitch + (iz+1+zs),  ix ∈ [-1,nx], iy ∈ [-1,ny], iz ∈ [-1,nz]
-// zs ∈ {0,1} shifts the row so that the first updated z node sits at an even offset: kernels then move nodes in
-// 16-byte pairs (dwordx4) that are naturally aligned. pitch is a multiple of 16 doubles (128 B) and keeps at least one
-// spare pair after the ghost node so the pair holding a row's right neighbour never straddles into the next row.
+// zs ∈ [0,15] shifts the row so that the first updated z node sits on a 128-byte line boundary: kernels move nodes
+// in 16-byte pairs (dwordx4) and a wave's 64 pairs then cover exactly eight whole 128-B lines. pitch is a multiple of
+// 16 doubles (128 B, so every row starts on a line) and keeps at least one spare pair after the ghost node so the pair
+// holding a row's right neighbour never straddles into the next row.
 struct Layout {
   i64 N = 0;
   i64 nx = 0, ny = 0, nz = 0;     // owned nodes
@@ -144,7 +145,7 @@ inline Layout make_layout(const Problem& p, const Box& b, i64 pitch_align = 16) 
   l.cy1 = imax(l.cy0, hi(b.y0, l.ny));
   l.cz0 = lo(b.z0);
   l.cz1 = imax(l.cz0, hi(b.z0, l.nz));
-  l.zs = (l.cz0 + 1) & 1;
+  l.zs = (16 - (l.cz0 + 1) % 16) % 16;
   l.pitch = round_up(l.nz + 2 + l.zs + 2, pitch_align);
   l.plane = (l.ny + 2) * l.pitch;
   l.total = (l.nx + 2) * l.plane;

@@ -22,13 +22,15 @@ using Partial = double2;
 
 // Tiling knobs of the leapfrog kernel (runtime-selectable so the tuner/bench can sweep them).
 struct LeapfrogTiling {
-  int ty = 8;             // tile rows (y) per workgroup; block = 64 × ty threads; one 16-byte pair per lane
-  int target_blocks = 0;  // x-chunking aims for at least this many workgroups (0 = 8 per CU)
+  int variant = 1;        // 0 = LDS-staged workgroup tile (k_leapfrog_lds), 1 = register-queue waves (k_leapfrog_rq)
+  int rows = 2;           // variant 1: rows (y) per wave held in registers (1, 2, 4 or 8)
+  int ty = 8;             // variant 0: tile rows (y) per workgroup; block = 64 × ty threads
+  int target_blocks = 0;  // x-chunking aims for at least this many work items (v0: workgroups, v1: waves; 0 = auto)
   bool xcd_remap = true;  // give each XCD a contiguous range of tiles (L2 reuse of tile halos)
-  bool nt_store = false;  // non-temporal stores of u^{n+1}
+  bool nt_store = true;   // non-temporal stores of u^{n+1} (measured faster on MI355X, profiles/)
 };
 
-// Number of workgroups (= error partials) a leapfrog launch over `boxes` will use.
+// Number of error partials (v0: workgroups, v1: waves) a leapfrog launch over `boxes` writes.
 int leapfrog_blocks(const Layout& l, const LBox* boxes, int nbox, const LeapfrogTiling& t);
 
 void launch_init_first(const Layout& l, const Coeffs& c, const double* d_s, double* u0, double* u1,

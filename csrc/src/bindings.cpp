@@ -258,6 +258,8 @@ PYBIND11_MODULE(_C, m) {
 
   py::class_<LeapfrogTiling>(m, "LeapfrogTiling")
       .def(py::init<>())
+      .def_readwrite("variant", &LeapfrogTiling::variant)
+      .def_readwrite("rows", &LeapfrogTiling::rows)
       .def_readwrite("ty", &LeapfrogTiling::ty)
       .def_readwrite("target_blocks", &LeapfrogTiling::target_blocks)
       .def_readwrite("xcd_remap", &LeapfrogTiling::xcd_remap)

@@ -130,7 +130,7 @@ struct LfParams {
 };
 
 template <int TY, bool CHECK, bool NT>
-__global__ __launch_bounds__(kLanes* TY) void k_leapfrog(const LfParams p) {
+__global__ __launch_bounds__(kLanes* TY) void k_leapfrog_lds(const LfParams p) {
   static_assert(TY >= 4, "halo slots need at least 128 + 2*TY threads");
   __shared__ v2d lds[2][TY + 2][kLanes + 2];
   __shared__ double red_m[TY], red_s[TY];
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(kLanes* TY) void k_leapfrog(const LfParams p) {
 
   const double ihx2 = p.ihx2, ihy2 = p.ihy2, ihz2 = p.ihz2, tau2 = p.tau2;
   double emax = 0.0, esum = 0.0;
-  double sxy = 0.0, sz0 = 0.0, sz1 = 0.0;
+  double sxy = 0.0, sz0 = 0.0, sz1 = 0.0, sxp = CHECK ? p.s[p.gx0 + xs] : 0.0;
   if (CHECK && active) {
     sxy = p.s[p.gy0 + y];
     sz0 = p.s[p.gz0 + o0 - 1 - p.zs];
@@ -217,6 +217,7 @@ __global__ __launch_bounds__(kLanes* TY) void k_leapfrog(const LfParams p) {
     const int buf = static_cast<int>((x - xs) & 1);
     const bool more = x + 1 < xe;
     v2d nxt = zero2, uo_n = zero2, hv_n = zero2;
+    const double nsxp = CHECK && more ? p.s[p.gx0 + x + 1] : 0.0;  // one plane ahead (in-order vmcnt)
     if (more) {
       if (active) {
         nxt = ld2(cur + px + 2 * plane + my);
@@ -245,7 +246,7 @@ __global__ __launch_bounds__(kLanes* TY) void k_leapfrog(const LfParams p) {
       else if (ok1)
         dst[1] = r.y;
       if (CHECK) {
-        const double sx = p.s[p.gx0 + x] * sxy;
+        const double sx = sxp * sxy;
         if (ok0) {
           const double e = fabs(r.x - (sx * sz0) * p.ct);
           emax = e > emax ? e : emax;
@@ -263,6 +264,7 @@ __global__ __launch_bounds__(kLanes* TY) void k_leapfrog(const LfParams p) {
     up = nxt;
     uo = uo_n;
     hv = hv_n;
+    sxp = nsxp;
   }
 
   if (CHECK) {
@@ -283,15 +285,203 @@ __global__ __launch_bounds__(kLanes* TY) void k_leapfrog(const LfParams p) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// leapfrog, variant 1: register-queue waves (no LDS, no barriers)
+// ---------------------------------------------------------------------------------------------------------------
+// Each WAVE independently owns R rows × 64 pairs (128 z nodes) of the (y,z) plane and marches along x. All of u^n it
+// needs lives in registers: for each row the x−1 / x / x+1 queue (+ x+2 in flight), the rows above/below the tile
+// (two extra row loads per plane, L2-served: they are the neighbouring waves' own rows), and per row one 8-byte z-halo
+// node that lanes 0 and npe−1 fetch. z-neighbours inside the row come from the adjacent lanes (__shfl_up/_down), y-
+// neighbours from the adjacent rows' registers. Nothing is staged through LDS and waves never wait for each other, so
+// many independent HBM streams stay in flight (R rows × 2 fields × 1 KiB per wave per plane).
+constexpr int kWavesRq = 4;  // waves per workgroup (scheduling only; they do not cooperate)
+
+template <int R, bool CHECK, bool NT>
+__global__ __launch_bounds__(64 * kWavesRq) void k_leapfrog_rq(const LfParams p) {
+  const int lane = static_cast<int>(threadIdx.x) & 63;
+  const int wv = static_cast<int>(threadIdx.x) >> 6;
+  int blk = static_cast<int>(blockIdx.x);
+  if (p.xcd_remap) {
+    const int per = p.nblocks >> 3;
+    blk = (static_cast<int>(blockIdx.x) & 7) * per + (static_cast<int>(blockIdx.x) >> 3);
+  }
+  const int tile = blk * kWavesRq + wv;
+  const int pidx = static_cast<int>(blockIdx.x) * kWavesRq + wv;
+  if (tile >= p.ntiles) {
+    if (CHECK && lane == 0) p.partials[pidx] = make_double2(0.0, 0.0);
+    return;
+  }
+  TileBox B = p.box[0];
+#pragma unroll
+  for (int k = 1; k < kMaxBoxes; ++k)
+    if (k < p.nbox && tile >= p.box[k].tile_begin) B = p.box[k];
+  int t = tile - B.tile_begin;
+  const int tz = t % B.ntz;
+  t /= B.ntz;
+  const int ty = t % B.nty;
+  const int tx = t / B.nty;
+
+  const i64 pzt = B.pz0 + static_cast<i64>(tz) * kLanes;
+  const int npe = static_cast<int>(imin(kLanes, B.pz_end - pzt));
+  const i64 yt = B.y0 + static_cast<i64>(ty) * R;
+  const int nre = static_cast<int>(imin(R, B.y1 - yt));
+  const i64 xs = B.x0 + static_cast<i64>(tx) * B.xchunk;
+  const i64 xe = imin(xs + B.xchunk, B.x1);
+
+  const bool act = lane < npe;
+  const i64 o0 = 2 * (pzt + lane);
+  const bool ok0 = act && o0 >= B.zo0 && o0 < B.zo1;
+  const bool ok1 = act && o0 + 1 >= B.zo0 && o0 + 1 < B.zo1;
+  const i64 pitch = p.pitch, plane = p.plane;
+  const i64 base = (yt + 1) * pitch + o0;   // row yt (r = 0), element 0 of my pair
+  const i64 top = base - pitch;              // row yt − 1
+  const i64 bot = base + nre * pitch;        // row yt + nre
+  // z halo: lane 0 fetches node 2·pzt − 1 (left of the tile); the right neighbour 2·(pzt+npe) is fetched by lane
+  // npe − 1, or by lane 1 when the tile is a single pair (lane 0 then reads it with a shuffle)
+  const int rlane = npe == 1 ? 1 : npe - 1;
+  const bool hzl = lane == 0, hzr = lane == rlane;
+  const i64 hzoff = (yt + 1) * pitch + (hzl ? 2 * pzt - 1 : 2 * (pzt + npe));
+
+  const double* __restrict__ cur = p.cur;
+  double* __restrict__ out = p.out;
+  const v2d z2 = {0.0, 0.0};
+  v2d m[R], c[R], q[R], o[R];
+  double hz[R];
+  v2d ht = z2, hb = z2;
+  i64 px = (xs + 1) * plane;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    m[r] = z2;
+    c[r] = z2;
+    q[r] = z2;
+    o[r] = z2;
+    hz[r] = 0.0;
+    if (r < nre) {
+      if (act) {
+        m[r] = ld2(cur + px - plane + base + r * pitch);
+        c[r] = ld2(cur + px + base + r * pitch);
+        q[r] = ld2(cur + px + plane + base + r * pitch);
+        o[r] = ld2(out + px + base + r * pitch);
+      }
+      if (hzl || hzr) hz[r] = cur[px + hzoff + r * pitch];
+    }
+  }
+  if (act) {
+    ht = ld2(cur + px + top);
+    hb = ld2(cur + px + bot);
+  }
+  const double ihx2 = p.ihx2, ihy2 = p.ihy2, ihz2 = p.ihz2, tau2 = p.tau2;
+  double emax = 0.0, esum = 0.0;
+  // error-epilogue factors of φ are loaded up front / one plane ahead, like every other load: vector-memory
+  // completion is in order, so a load consumed in the same iteration would drain the whole prefetch queue
+  double sz0 = 0.0, sz1 = 0.0, sx = 0.0;
+  double sy[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) sy[r] = CHECK && r < nre ? p.s[p.gy0 + yt + r] : 0.0;
+  if (CHECK) {
+    if (act) {
+      sz0 = p.s[p.gz0 + o0 - 1 - p.zs];
+      sz1 = p.s[p.gz0 + o0 - p.zs];
+    }
+    sx = p.s[p.gx0 + xs];
+  }
+
+  for (i64 x = xs; x < xe; ++x, px += plane) {
+    const bool more = x + 1 < xe;
+    v2d nq[R], no[R];
+    double nhz[R];
+    v2d nht = z2, nhb = z2;
+    const double nsx = CHECK && more ? p.s[p.gx0 + x + 1] : 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      nq[r] = z2;
+      no[r] = z2;
+      nhz[r] = 0.0;
+      if (more && r < nre) {
+        if (act) {
+          nq[r] = ld2(cur + px + 2 * plane + base + r * pitch);
+          no[r] = ld2(out + px + plane + base + r * pitch);
+        }
+        if (hzl || hzr) nhz[r] = cur[px + plane + hzoff + r * pitch];
+      }
+    }
+    if (more && act) {
+      nht = ld2(cur + px + plane + top);
+      nhb = ld2(cur + px + plane + bot);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r < nre) {
+        const v2d ym = r == 0 ? ht : c[r - 1];
+        const v2d yp = (r + 1 < nre && r + 1 < R) ? c[r + 1 < R ? r + 1 : r] : hb;
+        const double up_y = __shfl_up(c[r].y, 1, 64);
+        const double dn_x = __shfl_down(c[r].x, 1, 64);
+        const double hzs = npe == 1 ? __shfl_down(hz[r], 1, 64) : hz[r];
+        const double zm = lane == 0 ? hz[r] : up_y;
+        const double zp = lane == npe - 1 ? hzs : dn_x;
+        const double l0 = lap7(c[r].x, m[r].x, q[r].x, ym.x, yp.x, zm, c[r].y, ihx2, ihy2, ihz2);
+        const double l1 = lap7(c[r].y, m[r].y, q[r].y, ym.y, yp.y, c[r].x, zp, ihx2, ihy2, ihz2);
+        v2d v;
+        v.x = leapfrog(c[r].x, o[r].x, l0, tau2);
+        v.y = leapfrog(c[r].y, o[r].y, l1, tau2);
+        double* dst = out + px + base + r * pitch;
+        if (ok0 && ok1)
+          st2<NT>(dst, v);
+        else if (ok0)
+          dst[0] = v.x;
+        else if (ok1)
+          dst[1] = v.y;
+        if (CHECK) {
+          const double sxy = sx * sy[r];
+          if (ok0) {
+            const double e = fabs(v.x - (sxy * sz0) * p.ct);
+            emax = e > emax ? e : emax;
+            esum += e * e;
+          }
+          if (ok1) {
+            const double e = fabs(v.y - (sxy * sz1) * p.ct);
+            emax = e > emax ? e : emax;
+            esum += e * e;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      m[r] = c[r];
+      c[r] = q[r];
+      q[r] = nq[r];
+      o[r] = no[r];
+      hz[r] = nhz[r];
+    }
+    ht = nht;
+    hb = nhb;
+    sx = nsx;
+  }
+  if (CHECK) {
+    wave_reduce(emax, esum);
+    if (lane == 0) p.partials[pidx] = make_double2(emax, esum);
+  }
+}
+
+template <int R>
+void launch_rq(const LfParams& p, int nblocks, bool check, bool nt, hipStream_t st);
+
 // Host-side tiling plan shared by leapfrog_blocks() and launch_leapfrog().
 struct Plan {
   LfParams prm;
-  int nblocks;
+  int nblocks;    // workgroups launched
+  int npartials;  // error partials written (v0: per workgroup, v1: per wave)
 };
 
 Plan make_plan(const Layout& l, const LBox* boxes, int nbox, const LeapfrogTiling& t) {
   W3D_REQUIRE(nbox >= 0 && nbox <= kMaxBoxes, "too many boxes in one leapfrog launch");
-  W3D_REQUIRE(t.ty == 4 || t.ty == 8 || t.ty == 16, "leapfrog tile rows must be 4, 8 or 16");
+  const bool rq = t.variant == 1;
+  W3D_REQUIRE(t.variant == 0 || t.variant == 1, "leapfrog variant must be 0 (lds) or 1 (rq)");
+  W3D_REQUIRE(rq || t.ty == 4 || t.ty == 8 || t.ty == 16, "leapfrog tile rows must be 4, 8 or 16");
+  W3D_REQUIRE(!rq || t.rows == 1 || t.rows == 2 || t.rows == 4 || t.rows == 8, "rows per wave must be 1, 2, 4 or 8");
+  const int trows = rq ? t.rows : t.ty;
   Plan pl{};
   LfParams& p = pl.prm;
   p.plane = l.plane;
@@ -300,14 +490,15 @@ Plan make_plan(const Layout& l, const LBox* boxes, int nbox, const LeapfrogTilin
   p.gy0 = l.gy0;
   p.gz0 = l.gz0;
   p.zs = l.zs;
-  const int target = t.target_blocks > 0 ? t.target_blocks : 256 * 8;
+  // v0: one tile per workgroup, aim for 8 workgroups per CU; v1: one tile per wave, aim for 16 waves per CU
+  const int target = t.target_blocks > 0 ? t.target_blocks : (rq ? 256 * 16 : 256 * 8);
   // tiles before x-chunking, to spread the x-chunk count over boxes
   i64 base_total = 0;
   for (int b = 0; b < nbox; ++b) {
     const LBox& x = boxes[b];
     if (x.empty()) continue;
     const i64 zo0 = x.z0 + 1 + l.zs, zo1 = x.z1 + 1 + l.zs;
-    base_total += ceil_div((zo1 + 1) / 2 - zo0 / 2, kLanes) * ceil_div(x.y1 - x.y0, t.ty);
+    base_total += ceil_div((zo1 + 1) / 2 - zo0 / 2, kLanes) * ceil_div(x.y1 - x.y0, trows);
   }
   const i64 want = base_total > 0 ? imax(1, ceil_div(target, base_total)) : 1;
   int nb = 0, tiles = 0;
@@ -327,7 +518,7 @@ Plan make_plan(const Layout& l, const LBox* boxes, int nbox, const LeapfrogTilin
     tb.pz_end = (tb.zo1 + 1) / 2;
     W3D_REQUIRE(2 * tb.pz_end + 2 <= l.pitch, "row pitch too small for the pair tiling");
     tb.ntz = static_cast<int>(ceil_div(tb.pz_end - tb.pz0, kLanes));
-    tb.nty = static_cast<int>(ceil_div(x.y1 - x.y0, t.ty));
+    tb.nty = static_cast<int>(ceil_div(x.y1 - x.y0, trows));
     const i64 nxb = x.x1 - x.x0;
     const i64 min_chunk = 16;
     i64 chunk = imax(min_chunk, ceil_div(nxb, want));
@@ -343,8 +534,10 @@ Plan make_plan(const Layout& l, const LBox* boxes, int nbox, const LeapfrogTilin
   p.nbox = nb;
   p.ntiles = tiles;
   p.xcd_remap = t.xcd_remap ? 1 : 0;
-  pl.nblocks = t.xcd_remap ? static_cast<int>(round_up(tiles, 8)) : tiles;
+  const int units = rq ? static_cast<int>(ceil_div(tiles, kWavesRq)) : tiles;  // workgroups
+  pl.nblocks = t.xcd_remap ? static_cast<int>(round_up(units, 8)) : units;
   p.nblocks = pl.nblocks;
+  pl.npartials = rq ? pl.nblocks * kWavesRq : pl.nblocks;
   return pl;
 }
 
@@ -353,14 +546,30 @@ void launch_lf_ty(const LfParams& p, int nblocks, bool check, bool nt, hipStream
   const dim3 block(kLanes, TY), grid(nblocks);
   if (check) {
     if (nt)
-      hipLaunchKernelGGL((k_leapfrog<TY, true, true>), grid, block, 0, st, p);
+      hipLaunchKernelGGL((k_leapfrog_lds<TY, true, true>), grid, block, 0, st, p);
     else
-      hipLaunchKernelGGL((k_leapfrog<TY, true, false>), grid, block, 0, st, p);
+      hipLaunchKernelGGL((k_leapfrog_lds<TY, true, false>), grid, block, 0, st, p);
   } else {
     if (nt)
-      hipLaunchKernelGGL((k_leapfrog<TY, false, true>), grid, block, 0, st, p);
+      hipLaunchKernelGGL((k_leapfrog_lds<TY, false, true>), grid, block, 0, st, p);
     else
-      hipLaunchKernelGGL((k_leapfrog<TY, false, false>), grid, block, 0, st, p);
+      hipLaunchKernelGGL((k_leapfrog_lds<TY, false, false>), grid, block, 0, st, p);
+  }
+}
+
+template <int R>
+void launch_rq(const LfParams& p, int nblocks, bool check, bool nt, hipStream_t st) {
+  const dim3 block(64 * kWavesRq), grid(nblocks);
+  if (check) {
+    if (nt)
+      hipLaunchKernelGGL((k_leapfrog_rq<R, true, true>), grid, block, 0, st, p);
+    else
+      hipLaunchKernelGGL((k_leapfrog_rq<R, true, false>), grid, block, 0, st, p);
+  } else {
+    if (nt)
+      hipLaunchKernelGGL((k_leapfrog_rq<R, false, true>), grid, block, 0, st, p);
+    else
+      hipLaunchKernelGGL((k_leapfrog_rq<R, false, false>), grid, block, 0, st, p);
   }
 }
 
@@ -467,7 +676,7 @@ void launch_init_first(const Layout& l, const Coeffs& c, const double* d_s, doub
 }
 
 int leapfrog_blocks(const Layout& l, const LBox* boxes, int nbox, const LeapfrogTiling& t) {
-  return make_plan(l, boxes, nbox, t).nblocks;
+  return make_plan(l, boxes, nbox, t).npartials;
 }
 
 void launch_leapfrog(const Layout& l, const Coeffs& c, const double* cur, double* old_out, const LBox* boxes, int nbox,
@@ -485,10 +694,19 @@ void launch_leapfrog(const Layout& l, const Coeffs& c, const double* cur, double
   p.tau2 = c.tau2;
   p.ct = ct;
   const bool check = partials != nullptr;
-  switch (t.ty) {
-    case 4: launch_lf_ty<4>(p, pl.nblocks, check, t.nt_store, stream); break;
-    case 8: launch_lf_ty<8>(p, pl.nblocks, check, t.nt_store, stream); break;
-    default: launch_lf_ty<16>(p, pl.nblocks, check, t.nt_store, stream); break;
+  if (t.variant == 1) {
+    switch (t.rows) {
+      case 1: launch_rq<1>(p, pl.nblocks, check, t.nt_store, stream); break;
+      case 2: launch_rq<2>(p, pl.nblocks, check, t.nt_store, stream); break;
+      case 4: launch_rq<4>(p, pl.nblocks, check, t.nt_store, stream); break;
+      default: launch_rq<8>(p, pl.nblocks, check, t.nt_store, stream); break;
+    }
+  } else {
+    switch (t.ty) {
+      case 4: launch_lf_ty<4>(p, pl.nblocks, check, t.nt_store, stream); break;
+      case 8: launch_lf_ty<8>(p, pl.nblocks, check, t.nt_store, stream); break;
+      default: launch_lf_ty<16>(p, pl.nblocks, check, t.nt_store, stream); break;
+    }
   }
   W3D_HIP_CHECK(hipGetLastError());
 }

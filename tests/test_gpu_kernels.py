@@ -33,8 +33,10 @@ def test_init_first_bitexact(gpu, N, world, rank, decomp):
     assert torch.equal(ops.to_grid(lay, g1).cpu(), ops.to_grid(lay, a1))
 
 
-TILINGS = [dict(ty=8), dict(ty=4), dict(ty=16), dict(ty=8, xcd_remap=False), dict(ty=8, nt_store=True),
-           dict(ty=4, target_blocks=64)]
+TILINGS = [dict(variant=0, ty=8), dict(variant=0, ty=4), dict(variant=0, ty=16), dict(variant=0, ty=8, xcd_remap=False),
+           dict(variant=0, ty=8, nt_store=True), dict(variant=0, ty=4, target_blocks=64),
+           dict(variant=1, rows=1), dict(variant=1, rows=2), dict(variant=1, rows=4), dict(variant=1, rows=8),
+           dict(variant=1, rows=4, xcd_remap=False, nt_store=True), dict(variant=1, rows=2, target_blocks=100)]
 
 
 @pytest.mark.parametrize("tiling", TILINGS)

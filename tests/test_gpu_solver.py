@@ -57,10 +57,12 @@ def test_golden_log_512(gpu):
     assert lines[-1] == "Step 20, t = 0.020000, Max Error = 3.960129e-09, L2 Error = 1.404229e-09"
 
 
-@pytest.mark.parametrize("tiling", [dict(ty=4), dict(ty=16, xcd_remap=False), dict(ty=8, nt_store=True)])
+@pytest.mark.parametrize("tiling", [dict(variant=0, ty=4), dict(variant=0, ty=16, xcd_remap=False),
+                                    dict(variant=0, ty=8, nt_store=True), dict(variant=1, rows=1),
+                                    dict(variant=1, rows=8, nt_store=True)])
 def test_tilings_agree(gpu, tiling):
     spec = ProblemSpec(N=100, tau=1e-3, K=8)
-    a = Solver(spec, backend="hip", device=0)
+    a = Solver(spec, backend="hip", device=0, tiling=dict(variant=1, rows=4))
     b = Solver(spec, backend="hip", device=0, tiling=tiling)
     ra, rb = a.run(), b.run()
     assert ra.max_err == rb.max_err

@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Kernel-level tuning sweep for the leapfrog kernel on one GPU (HIP events, no profiler needed).
+
+Times one leapfrog launch over the 512³ compute box for every tiling in the sweep, plus streaming baselines
+measured in the same process (torch copy = 1 read + 1 write stream, torch add = 2 reads + 1 write — the stencil's
+compulsory pattern) so achieved TB/s can be read against what this HBM actually delivers.
+
+    python tools/tune_leapfrog.py [--N 512] [--iters 20] [--json out.json]
+"""
+from __future__ import annotations
+
+import argparse
+import itertools
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, iters: int, warm: int = 3) -> float:
+    import torch
+
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ts = []
+    for _ in range(iters):
+        s.record()
+        fn()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e))
+    ts.sort()
+    return ts[len(ts) // 2] * 1e3  # median µs
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--N", type=int, default=512)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--json", default="")
+    ap.add_argument("--quick", action="store_true")
+    a = ap.parse_args()
+    import torch
+
+    from mpi_cuda_amd._native import load
+    from mpi_cuda_amd.ops import stencil as ops
+
+    C = load()
+    torch.cuda.set_device(0)
+    prob = C.Problem(a.N, 1e-3, 20, 1.0)
+    co = C.Coeffs.from_problem(prob)
+    lay = C.make_layout(prob, C.rank_box(prob, C.Dims(1, 1, 1), 0))
+    box = C.compute_box(lay)
+    nodes = box.count()
+    s = ops.sin_table_ext(prob, "cuda")
+    u0, u1 = ops.alloc_field(lay, "cuda"), ops.alloc_field(lay, "cuda")
+    ops.init_first(lay, co, s, u0, u1)
+    torch.cuda.synchronize()
+    out = []
+
+    nbytes = int(lay.total) * 8
+    x = torch.empty(int(lay.total), dtype=torch.float64, device="cuda")
+    y = torch.empty_like(x)
+    z = torch.empty_like(x)
+    t = timeit(lambda: y.copy_(x), a.iters)
+    out.append({"kernel": "torch copy (1R+1W)", "us": t, "TBps": 2 * nbytes / t / 1e6})
+    t = timeit(lambda: torch.add(x, y, out=z), a.iters)
+    out.append({"kernel": "torch add (2R+1W)", "us": t, "TBps": 3 * nbytes / t / 1e6})
+    t = timeit(lambda: ops.init_first(lay, co, s, u0, u1), a.iters)
+    out.append({"kernel": "k_init_first (2W)", "us": t, "TBps": 2 * nbytes / t / 1e6})
+    del x, y, z
+
+    configs = []
+    for ty, tb, nt in itertools.product([8, 16], [0, 1024], [False, True]):
+        configs.append(dict(variant=0, ty=ty, target_blocks=tb, xcd_remap=True, nt_store=nt))
+    for rows, tb, rm, nt in itertools.product([1, 2, 4, 8], [0, 2048, 8192], [True, False], [False, True]):
+        configs.append(dict(variant=1, rows=rows, target_blocks=tb, xcd_remap=rm, nt_store=nt))
+    if a.quick:
+        configs = [c for c in configs if c["target_blocks"] == 0 and c["xcd_remap"]]
+    for cfg, chk in itertools.product(configs, [False, True] if not a.quick else [False]):
+        tl = C.LeapfrogTiling()
+        for k, v in cfg.items():
+            setattr(tl, k, v)
+        nb = C.gpu_leapfrog_blocks(lay, [box], tl)
+        part = torch.empty((nb, 2), dtype=torch.float64, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+
+        def step():
+            C.gpu_leapfrog(lay, co, u1.data_ptr(), u0.data_ptr(), [box], s.data_ptr(), 0.5,
+                           part.data_ptr() if chk else 0, tl, st)
+
+        t = timeit(step, a.iters)
+        out.append({"kernel": "k_leapfrog", **cfg, "partials": nb, "check": chk, "us": t,
+                    "TBps": 24 * nodes / t / 1e6})
+    for r in out:
+        print(json.dumps(r), flush=True)
+    best = min((r for r in out if r["kernel"] == "k_leapfrog"), key=lambda r: r["us"])
+    print("BEST", json.dumps(best))
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -72,7 +72,9 @@ class Comm {
 
 class GpuSolver {
  public:
-  GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, int world, std::shared_ptr<Comm> comm);
+  // loopback = true: this rank is driven by a GpuGroup (in-process ranks, device-copy halos; tests)
+  GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, int world, std::shared_ptr<Comm> comm,
+            bool loopback = false);
   ~GpuSolver();
   GpuSolver(const GpuSolver&) = delete;
   GpuSolver& operator=(const GpuSolver&) = delete;
@@ -96,15 +98,29 @@ class GpuSolver {
   size_t device_bytes() const;
 
  private:
+  friend class GpuGroup;
   void enqueue_solve();  // all device work of one solve on s0/s1 (graph-capturable)
   void exchange(double* field, hipStream_t st);
   void gather_errors(RunResult& r);
+  bool split() const;
+  bool needs_exchange(int n) const;
+  double* xfield() const;
+  hipStream_t xstream() const;
+  void phase_init();
+  void phase_shell(int n);
+  void phase_exchange_rccl(int n);
+  void phase_interior(int n);
+  void lb_pack(int n);
+  void lb_pull(int n, const std::vector<GpuSolver*>& ranks);
+  void lb_fence(int n, const std::vector<GpuSolver*>& ranks);
+  RunResult collect_local();
 
   Problem prob_;
   SolverOptions opt_;
   Coeffs coef_;
   int rank_, world_;
   std::shared_ptr<Comm> comm_;
+  bool loopback_ = false;
   Dims dims_;
   Layout lay_;
   HaloPlan plan_;
@@ -122,7 +138,10 @@ class GpuSolver {
   Partial* errall_ = nullptr;    // [world][K+1]
   std::vector<double> ct_;       // cos(a_t n τ)
   hipStream_t s0_ = nullptr, s1_ = nullptr;
-  hipEvent_t ev_shell_ = nullptr, ev_halo_ = nullptr;
+  hipEvent_t ev_shell_ = nullptr, ev_halo_ = nullptr, ev_packed_ = nullptr;
+  int n_full_ = 0, n_shell_ = 0, n_int_ = 0;  // error partials of each launch kind
+  int cur_ = 1, old_ = 0;                     // buffer roles during enqueue
+  std::vector<char> is_check_;
   hipGraphExec_t graph_exec_ = nullptr;
   int final_buf_ = 0;            // buffer index holding u^K after a solve
   std::vector<hipEvent_t> tev_;  // timer events
@@ -131,6 +150,20 @@ class GpuSolver {
 }  // namespace wave3d
 
 namespace wave3d {
+
+// P ranks of one decomposition inside ONE process on the current device, halos moved by device-to-device copies.
+// Same GpuSolver code as production except the transport; used to validate the multi-rank path on one GPU.
+class GpuGroup {
+ public:
+  GpuGroup(const Problem& prob, const SolverOptions& opt, int world);
+  RunResult run();  // global error log (rank-ordered combine), solve_s = wall time of the group solve
+  GpuSolver& rank(int r) { return *ranks_[static_cast<size_t>(r)]; }
+  int world() const { return static_cast<int>(ranks_.size()); }
+
+ private:
+  std::vector<std::unique_ptr<GpuSolver>> ranks_;
+};
+
 // Host-scalar collectives over the RCCL communicator (timer max-reduction, barriers). Blocking.
 double comm_allreduce(const Comm& c, double v, bool max_op);
 void comm_barrier(const Comm& c);

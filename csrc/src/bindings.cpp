@@ -346,4 +346,26 @@ PYBIND11_MODULE(_C, m) {
       .def("check_steps", &GpuSolver::check_steps)
       .def("device_bytes", &GpuSolver::device_bytes)
       .def_property_readonly("graph_enabled", [](const GpuSolver& s) { return s.options().graph; });
+
+  py::class_<GpuGroup>(m, "GpuGroup")
+      .def(py::init<const Problem&, const SolverOptions&, int>(), py::arg("problem"), py::arg("options"),
+           py::arg("world"))
+      .def("run",
+           [](GpuGroup& g) {
+             RunResult r;
+             {
+               py::gil_scoped_release nogil;
+               r = g.run();
+             }
+             return result_dict(r);
+           })
+      .def("download",
+           [](GpuGroup& g, int rank, int which) {
+             auto v = g.rank(rank).download(which);
+             return darr(static_cast<py::ssize_t>(v.size()), v.data());
+           },
+           py::arg("rank"), py::arg("which") = 0)
+      .def("layout", [](GpuGroup& g, int rank) { return g.rank(rank).layout(); })
+      .def("dims", [](GpuGroup& g) { return g.rank(0).dims(); })
+      .def_property_readonly("world", &GpuGroup::world);
 }

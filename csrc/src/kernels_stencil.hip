@@ -298,7 +298,8 @@ __global__ __launch_bounds__(kLanes* TY) void k_leapfrog_lds(const LfParams p) {
 constexpr int kWavesRq = 4;  // waves per workgroup (scheduling only; they do not cooperate)
 
 template <int R, bool CHECK, bool NT>
-__global__ __launch_bounds__(64 * kWavesRq) void k_leapfrog_rq(const LfParams p) {
+__global__ __launch_bounds__(64 * kWavesRq) __attribute__((amdgpu_waves_per_eu(R <= 2 ? 4 : 2))) void k_leapfrog_rq(
+    const LfParams p) {
   const int lane = static_cast<int>(threadIdx.x) & 63;
   const int wv = static_cast<int>(threadIdx.x) >> 6;
   int blk = static_cast<int>(blockIdx.x);

@@ -69,11 +69,13 @@ void wait_stream(hipStream_t s, const Comm* comm, double timeout_s) {
 
 }  // namespace
 
-GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, int world, std::shared_ptr<Comm> comm)
-    : prob_(prob), opt_(opt), coef_(Coeffs::from(prob)), rank_(rank), world_(world), comm_(std::move(comm)) {
+GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, int world, std::shared_ptr<Comm> comm,
+                     bool loopback)
+    : prob_(prob), opt_(opt), coef_(Coeffs::from(prob)), rank_(rank), world_(world), comm_(std::move(comm)),
+      loopback_(loopback) {
   prob_.validate();
   W3D_REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
-  W3D_REQUIRE(world == 1 || comm_, "world > 1 needs an RCCL communicator");
+  W3D_REQUIRE(world == 1 || comm_ || loopback_, "world > 1 needs an RCCL communicator (or the loopback group)");
   dims_ = parse_dims(opt_.decomp, world, prob_.N);
   const Box box = rank_box(prob_, dims_, rank);
   W3D_REQUIRE(box.nx() >= 1 && box.ny() >= 1 && box.nz() >= 1,
@@ -113,6 +115,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   W3D_HIP(hipStreamCreateWithFlags(&s1_, hipStreamNonBlocking));
   W3D_HIP(hipEventCreateWithFlags(&ev_shell_, hipEventDisableTiming));
   W3D_HIP(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
+  W3D_HIP(hipEventCreateWithFlags(&ev_packed_, hipEventDisableTiming));
   for (int b = 0; b < 2; ++b) {
     W3D_HIP(hipMalloc(&u_[b], static_cast<size_t>(lay_.bytes())));
     W3D_HIP(hipMemset(u_[b], 0, static_cast<size_t>(lay_.bytes())));
@@ -124,16 +127,16 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
     W3D_HIP(hipMalloc(&send_buf_, static_cast<size_t>(plan_.packed_doubles) * sizeof(double)));
     W3D_HIP(hipMalloc(&recv_buf_, static_cast<size_t>(plan_.packed_doubles) * sizeof(double)));
   }
-  const int n_full = leapfrog_blocks(lay_, &full_, 1, opt_.tiling);
-  const int n_split = leapfrog_blocks(lay_, shell_.data(), static_cast<int>(shell_.size()), opt_.tiling) +
-                      leapfrog_blocks(lay_, &interior_, 1, opt_.tiling);
-  n_partials_ = std::max({n_full, n_split, error_blocks(lay_, full_), 1});
+  n_full_ = leapfrog_blocks(lay_, &full_, 1, opt_.tiling);
+  n_shell_ = leapfrog_blocks(lay_, shell_.data(), static_cast<int>(shell_.size()), opt_.tiling);
+  n_int_ = leapfrog_blocks(lay_, &interior_, 1, opt_.tiling);
+  n_partials_ = std::max({n_full_, n_shell_ + n_int_, error_blocks(lay_, full_), 1});
   W3D_HIP(hipMalloc(&partials_, static_cast<size_t>(n_partials_) * sizeof(Partial)));
   W3D_HIP(hipMalloc(&errlog_, static_cast<size_t>(prob_.K + 1) * sizeof(Partial)));
   W3D_HIP(hipMalloc(&errall_, static_cast<size_t>(world_) * (prob_.K + 1) * sizeof(Partial)));
   ct_.resize(static_cast<size_t>(prob_.K + 1));
   for (int n = 0; n <= prob_.K; ++n) ct_[static_cast<size_t>(n)] = time_factor(prob_, n);
-  if (opt_.timers) opt_.graph = false;
+  if (opt_.timers || loopback_) opt_.graph = false;
 }
 
 GpuSolver::~GpuSolver() {
@@ -146,6 +149,7 @@ GpuSolver::~GpuSolver() {
   for (hipEvent_t e : tev_) hipEventDestroy(e);
   if (ev_shell_) hipEventDestroy(ev_shell_);
   if (ev_halo_) hipEventDestroy(ev_halo_);
+  if (ev_packed_) hipEventDestroy(ev_packed_);
   if (s0_) hipStreamDestroy(s0_);
   if (s1_) hipStreamDestroy(s1_);
 }
@@ -178,74 +182,151 @@ void GpuSolver::exchange(double* field, hipStream_t st) {
   if (plan_.packed_doubles > 0) launch_unpack(lay_, plan_, recv_buf_, field, st);
 }
 
-void GpuSolver::enqueue_solve() {
+// ------------------------------------------------------------------------------------------------------------------
+// step phases. One step n (u^{n+1} from u^n, u^{n−1}) is: shell → exchange → interior. With overlap the exchange
+// carries the NEW field's shell faces on the side stream s1 while the interior runs on s0; without overlap the
+// exchange carries the CURRENT field's faces on s0 before the whole-box update.
+// ------------------------------------------------------------------------------------------------------------------
+bool GpuSolver::split() const { return opt_.overlap && plan_.any(); }
+
+bool GpuSolver::needs_exchange(int n) const {
+  if (!plan_.any()) return false;
+  return split() ? n < prob_.K - 1 : n >= 2;
+}
+
+double* GpuSolver::xfield() const { return split() ? u_[old_] : u_[cur_]; }
+hipStream_t GpuSolver::xstream() const { return split() ? s1_ : s0_; }
+
+void GpuSolver::phase_init() {
   const int K = prob_.K;
   const double* s = d_s_ + 1;
-  const auto checks = check_steps();
-  std::vector<char> is_check(static_cast<size_t>(K + 1), 0);
-  for (int n : checks) is_check[static_cast<size_t>(n)] = 1;
-  auto tev = [&](int i, hipStream_t st) {
-    if (opt_.timers) W3D_HIP(hipEventRecord(tev_[static_cast<size_t>(i)], st));
-  };
-
-  tev(0, s0_);
+  is_check_.assign(static_cast<size_t>(K + 1), 0);
+  for (int n : check_steps()) is_check_[static_cast<size_t>(n)] = 1;
+  if (opt_.timers) W3D_HIP(hipEventRecord(tev_[0], s0_));
   W3D_HIP(hipMemsetAsync(errlog_, 0, static_cast<size_t>(K + 1) * sizeof(Partial), s0_));
   launch_init_first(lay_, coef_, s, u_[0], u_[1], s0_);
-  if (is_check[1]) {
+  if (is_check_[1]) {
     launch_error(lay_, u_[1], full_, s, ct_[1], partials_, s0_);
     launch_reduce(partials_, error_blocks(lay_, full_), errlog_ + 1, s0_);
   }
-  tev(1, s0_);
-  const bool split = opt_.overlap && plan_.any();
-  const int n_shell = leapfrog_blocks(lay_, shell_.data(), static_cast<int>(shell_.size()), opt_.tiling);
-  const int n_int = leapfrog_blocks(lay_, &interior_, 1, opt_.tiling);
-  const int n_full = leapfrog_blocks(lay_, &full_, 1, opt_.tiling);
-  int cur = 1, old = 0;
-  for (int n = 1; n <= K - 1; ++n) {
-    const bool chk = is_check[static_cast<size_t>(n + 1)] != 0;
-    Partial* pp = chk ? partials_ : nullptr;
-    const double ct = ct_[static_cast<size_t>(n + 1)];
-    const bool last = n == K - 1;
-    if (split) {
-      launch_leapfrog(lay_, coef_, u_[cur], u_[old], shell_.data(), static_cast<int>(shell_.size()), s, ct, pp,
-                      opt_.tiling, s0_);
-      if (!last) {
-        W3D_HIP(hipEventRecord(ev_shell_, s0_));
-        W3D_HIP(hipStreamWaitEvent(s1_, ev_shell_, 0));
-        exchange(u_[old], s1_);
-        W3D_HIP(hipEventRecord(ev_halo_, s1_));
-      }
-      launch_leapfrog(lay_, coef_, u_[cur], u_[old], &interior_, 1, s, ct, pp ? pp + n_shell : nullptr, opt_.tiling,
-                      s0_);
-      if (!last) W3D_HIP(hipStreamWaitEvent(s0_, ev_halo_, 0));
-      if (chk) launch_reduce(partials_, n_shell + n_int, errlog_ + n + 1, s0_);
-    } else {
-      if (n >= 2) exchange(u_[cur], s0_);
-      launch_leapfrog(lay_, coef_, u_[cur], u_[old], &full_, 1, s, ct, pp, opt_.tiling, s0_);
-      if (chk) launch_reduce(partials_, n_full, errlog_ + n + 1, s0_);
-    }
-    std::swap(cur, old);
+  if (opt_.timers) W3D_HIP(hipEventRecord(tev_[1], s0_));
+  cur_ = 1;
+  old_ = 0;
+}
+
+void GpuSolver::phase_shell(int n) {
+  const bool chk = is_check_[static_cast<size_t>(n + 1)] != 0;
+  if (split()) {
+    launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], shell_.data(), static_cast<int>(shell_.size()), d_s_ + 1,
+                    ct_[static_cast<size_t>(n + 1)], chk ? partials_ : nullptr, opt_.tiling, s0_);
   }
-  final_buf_ = cur;
-  tev(2, s0_);
+  if (needs_exchange(n)) W3D_HIP(hipEventRecord(ev_shell_, s0_));
+}
+
+void GpuSolver::phase_exchange_rccl(int n) {
+  if (!needs_exchange(n)) return;
+  hipStream_t xs = xstream();
+  if (xs != s0_) W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
+  exchange(xfield(), xs);
+  if (split()) W3D_HIP(hipEventRecord(ev_halo_, xs));
+}
+
+void GpuSolver::phase_interior(int n) {
+  const bool chk = is_check_[static_cast<size_t>(n + 1)] != 0;
+  const double ct = ct_[static_cast<size_t>(n + 1)];
+  if (split()) {
+    launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &interior_, 1, d_s_ + 1, ct,
+                    chk ? partials_ + n_shell_ : nullptr, opt_.tiling, s0_);
+    if (needs_exchange(n)) W3D_HIP(hipStreamWaitEvent(s0_, ev_halo_, 0));
+    if (chk) launch_reduce(partials_, n_shell_ + n_int_, errlog_ + n + 1, s0_);
+  } else {
+    launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &full_, 1, d_s_ + 1, ct, chk ? partials_ : nullptr,
+                    opt_.tiling, s0_);
+    if (chk) launch_reduce(partials_, n_full_, errlog_ + n + 1, s0_);
+  }
+  std::swap(cur_, old_);
+  if (n == prob_.K - 1) {
+    final_buf_ = cur_;
+    if (opt_.timers) W3D_HIP(hipEventRecord(tev_[2], s0_));
+  }
+}
+
+void GpuSolver::enqueue_solve() {
+  phase_init();
+  for (int n = 1; n <= prob_.K - 1; ++n) {
+    phase_shell(n);
+    phase_exchange_rccl(n);
+    phase_interior(n);
+  }
+  final_buf_ = cur_;
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// loopback transport (GpuGroup): P ranks in one process on one device, halos moved by device copies. Test-only
+// stand-in for RCCL that exercises the identical shell/interior split, halo plans, pack/unpack and stream/event
+// ordering of the production path on a single GPU (RCCL refuses two ranks on one device).
+// ------------------------------------------------------------------------------------------------------------------
+void GpuSolver::lb_pack(int n) {
+  if (!needs_exchange(n)) return;
+  hipStream_t xs = xstream();
+  if (xs != s0_) W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
+  if (plan_.packed_doubles > 0) launch_pack(lay_, plan_, xfield(), send_buf_, xs);
+  W3D_HIP(hipEventRecord(ev_packed_, xs));
+}
+
+void GpuSolver::lb_pull(int n, const std::vector<GpuSolver*>& ranks) {
+  if (!needs_exchange(n)) return;
+  hipStream_t xs = xstream();
+  const int b = split() ? old_ : cur_;
+  for (const Face& f : plan_.faces) {
+    const GpuSolver* q = ranks[static_cast<size_t>(f.peer)];
+    const Face* g = nullptr;
+    for (const Face& h : q->plan_.faces)
+      if (h.peer == rank_) g = &h;
+    W3D_REQUIRE(g && g->count == f.count, "loopback: mismatched faces");
+    W3D_HIP(hipStreamWaitEvent(xs, q->ev_packed_, 0));
+    const double* src = g->contiguous ? q->u_[b] + g->send_off : q->send_buf_ + g->pack_off;
+    double* dst = f.contiguous ? u_[b] + f.recv_off : recv_buf_ + f.pack_off;
+    W3D_HIP(hipMemcpyAsync(dst, src, static_cast<size_t>(f.count) * sizeof(double), hipMemcpyDeviceToDevice, xs));
+  }
+  if (plan_.packed_doubles > 0) launch_unpack(lay_, plan_, recv_buf_, u_[b], xs);
+  W3D_HIP(hipEventRecord(ev_halo_, xs));
+}
+
+void GpuSolver::lb_fence(int n, const std::vector<GpuSolver*>& ranks) {
+  // the peers have read this rank's send regions once their pulls are done: keep both streams behind them
+  if (!needs_exchange(n)) return;
+  for (const Face& f : plan_.faces) {
+    const GpuSolver* q = ranks[static_cast<size_t>(f.peer)];
+    W3D_HIP(hipStreamWaitEvent(s0_, q->ev_halo_, 0));
+    if (s1_ != s0_) W3D_HIP(hipStreamWaitEvent(s1_, q->ev_halo_, 0));
+  }
+}
+
+RunResult GpuSolver::collect_local() {
+  RunResult r;
+  gather_errors(r);
+  return r;
 }
 
 void GpuSolver::gather_errors(RunResult& r) {
   const int K = prob_.K;
   const size_t per = static_cast<size_t>(K + 1);
   std::vector<Partial> host(per * static_cast<size_t>(world_));
-  if (world_ > 1) {
+  if (world_ > 1 && comm_) {
     W3D_NCCL(ncclAllGather(errlog_, errall_, 2 * per, ncclFloat64, static_cast<ncclComm_t>(comm_->raw()), s0_));
     W3D_HIP(hipMemcpyAsync(host.data(), errall_, host.size() * sizeof(Partial), hipMemcpyDeviceToHost, s0_));
   } else {
+    host.resize(per);
     W3D_HIP(hipMemcpyAsync(host.data(), errlog_, per * sizeof(Partial), hipMemcpyDeviceToHost, s0_));
   }
   wait_stream(s0_, comm_.get(), 600.0);
+  const int nsrc = static_cast<int>(host.size() / per);
   const double n_int = static_cast<double>(prob_.N - 1);
   const double denom = n_int * n_int * n_int;
   for (int n : check_steps()) {
     double m = 0.0, sum = 0.0;
-    for (int q = 0; q < world_; ++q) {  // fixed rank order
+    for (int q = 0; q < nsrc; ++q) {  // fixed rank order
       const Partial& v = host[static_cast<size_t>(q) * per + static_cast<size_t>(n)];
       m = v.x > m || std::isnan(v.x) ? v.x : m;
       sum += v.y;
@@ -329,5 +410,54 @@ double comm_allreduce(const Comm& c, double v, bool max_op) {
 }
 
 void comm_barrier(const Comm& c) { (void)comm_allreduce(c, 0.0, false); }
+
+}  // namespace wave3d
+
+namespace wave3d {
+
+GpuGroup::GpuGroup(const Problem& prob, const SolverOptions& opt, int world) {
+  W3D_REQUIRE(world >= 1, "world must be >= 1");
+  for (int r = 0; r < world; ++r) ranks_.push_back(std::make_unique<GpuSolver>(prob, opt, r, world, nullptr, true));
+}
+
+RunResult GpuGroup::run() {
+  std::vector<GpuSolver*> rs;
+  for (auto& p : ranks_) rs.push_back(p.get());
+  const int K = rs[0]->prob_.K;
+  const double t0 = now_s();
+  for (auto* s : rs) s->phase_init();
+  for (int n = 1; n <= K - 1; ++n) {
+    for (auto* s : rs) s->phase_shell(n);
+    for (auto* s : rs) s->lb_pack(n);
+    for (auto* s : rs) s->lb_pull(n, rs);
+    for (auto* s : rs) s->lb_fence(n, rs);
+    for (auto* s : rs) s->phase_interior(n);
+  }
+  // combine the per-rank error logs in rank order (what the RCCL all-gather does across processes)
+  const size_t per = static_cast<size_t>(K + 1);
+  std::vector<Partial> all(per * rs.size());
+  for (size_t q = 0; q < rs.size(); ++q) {
+    rs[q]->final_buf_ = rs[q]->cur_;
+    W3D_HIP(hipMemcpyAsync(all.data() + q * per, rs[q]->errlog_, per * sizeof(Partial), hipMemcpyDeviceToHost,
+                           rs[q]->s0_));
+  }
+  for (auto* s : rs) wait_stream(s->s0_, nullptr, 600.0);
+  RunResult r;
+  const double n_int = static_cast<double>(rs[0]->prob_.N - 1);
+  for (int n : rs[0]->check_steps()) {
+    double m = 0.0, sum = 0.0;
+    for (size_t q = 0; q < rs.size(); ++q) {
+      const Partial& v = all[q * per + static_cast<size_t>(n)];
+      m = v.x > m || std::isnan(v.x) ? v.x : m;
+      sum += v.y;
+    }
+    r.steps.push_back(n);
+    r.max_err.push_back(m);
+    r.rms_err.push_back(std::sqrt(sum / (n_int * n_int * n_int)));
+    if (!std::isfinite(m) || !std::isfinite(sum)) r.finite = false;
+  }
+  r.solve_s = now_s() - t0;
+  return r;
+}
 
 }  // namespace wave3d

@@ -8,6 +8,8 @@ backend    transport   what runs
 hip        rccl        native C++ GpuSolver: HIP kernels, C++ step loop, RCCL P2P halos on a side stream overlapped
                        with the interior update, whole solve captured in one hipGraph (production path, any world)
 hip        torch       Python step loop, HIP kernels, halos over torch.distributed (RCCL, or gloo staged via host)
+hip        loopback    native GpuGroup: all ranks of a decomposition in THIS process on one GPU, device-copy halos
+                       (exercises the production multi-rank C++ path on a single GPU; tests)
 cpu        native      C++ CpuSolver, OpenMP (the reference's sequential / OpenMP programs), world == 1
 cpu        torch       Python step loop, native OpenMP kernels, halos over torch.distributed gloo (MPI analogue)
 torch      -           plain PyTorch fp64 reference solver (oracle), world == 1
@@ -53,7 +55,8 @@ def _resolve(backend: str, transport: str, world: int) -> tuple[str, str]:
         backend = "hip" if torch.cuda.is_available() else "cpu"
     if transport == "auto":
         transport = {"hip": "rccl", "cpu": "native" if world == 1 else "torch", "torch": "none"}[backend]
-    ok = {("hip", "rccl"), ("hip", "torch"), ("cpu", "native"), ("cpu", "torch"), ("torch", "none")}
+    ok = {("hip", "rccl"), ("hip", "torch"), ("hip", "loopback"), ("cpu", "native"), ("cpu", "torch"),
+          ("torch", "none")}
     if (backend, transport) not in ok:
         raise ValueError(f"unsupported backend/transport combination {backend}/{transport}")
     if backend == "cpu" and transport == "native" and world > 1:
@@ -94,17 +97,14 @@ class Solver:
             self.device = torch.device("cuda", dev)
         else:
             self.device = torch.device("cpu")
-        if self.backend == "hip" and self.transport == "rccl":
+        if self.backend == "hip" and self.transport == "loopback":
+            opts = self._options(C, decomp, spec, overlap, False, tiling)
+            self._impl = C.GpuGroup(spec.native(), opts, world)
+            self.dims = self._impl.dims().as_tuple()
+        elif self.backend == "hip" and self.transport == "rccl":
             from .parallel.rccl import make_comm
 
-            opts = C.SolverOptions()
-            opts.decomp = decomp
-            opts.check_every = spec.check_every
-            opts.overlap = overlap
-            opts.graph = graph
-            if tiling:
-                for k, v in tiling.items():
-                    setattr(opts.tiling, k, v)
+            opts = self._options(C, decomp, spec, overlap, graph, tiling)
             if comm is None and world > 1:
                 comm = make_comm(rank, world, group)
             self.comm = comm
@@ -120,6 +120,18 @@ class Solver:
             self.dims = (1, 1, 1)
         else:
             self.dims = (1, 1, 1)
+
+    @staticmethod
+    def _options(C, decomp, spec, overlap, graph, tiling):
+        opts = C.SolverOptions()
+        opts.decomp = decomp
+        opts.check_every = spec.check_every
+        opts.overlap = overlap
+        opts.graph = graph
+        if tiling:
+            for k, v in tiling.items():
+                setattr(opts.tiling, k, v)
+        return opts
 
     def run(self) -> SolveResult:
         if self.backend == "torch":
@@ -141,6 +153,23 @@ class Solver:
     @property
     def native(self):
         return self._impl
+
+    def global_field(self, which: int = 0) -> torch.Tensor:
+        """The whole (N+1)³ field u^K (which=0) / u^{K-1} (which=1) on the CPU (single rank or loopback group)."""
+        from .ops.stencil import grid_view
+
+        if self.transport != "loopback":
+            if self.world != 1:
+                raise RuntimeError("global_field needs world == 1 or the loopback transport")
+            return self.owned_field(which)
+        n = self.spec.N + 1
+        out = torch.empty((n, n, n), dtype=torch.float64)
+        for r in range(self.world):
+            lay = self._impl.layout(r)
+            g = grid_view(lay, torch.from_numpy(self._impl.download(r, which)))
+            out[lay.gx0:lay.gx0 + lay.nx, lay.gy0:lay.gy0 + lay.ny, lay.gz0:lay.gz0 + lay.nz] = \
+                g[1:1 + int(lay.nx), 1:1 + int(lay.ny), 1:1 + int(lay.nz)]
+        return out
 
     def owned_field(self, which: int = 0) -> torch.Tensor:
         """This rank's owned nodes of u^K (which=0) or u^{K-1} (which=1) as a CPU (nx, ny, nz) float64 tensor."""

@@ -1,0 +1,75 @@
+"""Multi-process decomposition on the CPU over torch.distributed gloo (the reference's MPI / MPI+OpenMP programs,
+report.pdf p.9-11): every decomposition and rank count reproduces the single-process field bit-for-bit."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+_WORKER = r"""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["ROOT"])
+from mpi_cuda_amd import ProblemSpec
+from mpi_cuda_amd.solver import Solver
+dist.init_process_group("gloo")
+spec = ProblemSpec(N=int(os.environ["N"]), tau=1e-3, K=int(os.environ["K"]), check_every=1)
+s = Solver(spec, backend="cpu", transport="torch", decomp=os.environ["DECOMP"], threads=1)
+r = s.run()
+torch.save({"max": r.max_err, "rms": r.rms_err, "f": s.owned_field(0), "f1": s.owned_field(1),
+            "dims": tuple(s.dims)}, os.environ["OUT"] + f".{dist.get_rank()}.pt")
+dist.destroy_process_group()
+"""
+
+
+def _run(tmp_path, world, decomp, N, K, port):
+    script = tmp_path / "w.py"
+    script.write_text(_WORKER)
+    env = dict(os.environ, ROOT=ROOT, OUT=str(tmp_path / "res"), DECOMP=decomp, N=str(N), K=str(K),
+               OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", str(world), "--master-addr",
+           "127.0.0.1", "--master-port", str(port), str(script)]
+    subprocess.run(cmd, env=env, check=True, timeout=300, capture_output=True)
+    return [torch.load(str(tmp_path / f"res.{r}.pt"), weights_only=True) for r in range(world)]
+
+
+@pytest.mark.parametrize("world,decomp", [(2, "slab"), (4, "block"), (3, "1x3x1"), (4, "1x1x4")])
+def test_decomposed_cpu_bitexact(tmp_path, world, decomp):
+    from mpi_cuda_amd import ProblemSpec
+    from mpi_cuda_amd.parallel.decomp import plan
+    from mpi_cuda_amd.solver import Solver
+
+    N, K = 30, 6
+    port = 29400 + world * 10 + len(decomp) + (os.getpid() % 50)
+    res = _run(tmp_path, world, decomp, N, K, port)
+    spec = ProblemSpec(N=N, tau=1e-3, K=K, check_every=1)
+    ref = Solver(spec, backend="cpu")
+    rr = ref.run()
+    full0, full1 = ref.owned_field(0), ref.owned_field(1)
+    for rank, d in enumerate(res):
+        assert d["max"] == rr.max_err
+        assert all(abs(a - b) <= 1e-12 * b for a, b in zip(d["rms"], rr.rms_err))
+        x0, x1, y0, y1, z0, z1 = plan(N, world, rank, decomp).box
+        assert torch.equal(d["f"], full0[x0:x1, y0:y1, z0:z1])
+        assert torch.equal(d["f1"], full1[x0:x1, y0:y1, z0:z1])
+
+
+def test_bench_contract_cpu_two_ranks(tmp_path):
+    """bench.py under torch.distributed.run prints exactly one JSON line with the contract keys (CPU backend)."""
+    import json
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(29380 + os.getpid() % 50), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu",
+           "--N", "24", "--steps", "2", "--warmup", "1"]
+    out = subprocess.run(cmd, check=True, timeout=300, capture_output=True, text=True).stdout
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1 and d["correct"]
+    for k in ("model", "global_batch", "seq_len", "parallelism"):
+        assert k in d["config"]

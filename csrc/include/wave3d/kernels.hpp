@@ -36,10 +36,33 @@ int leapfrog_blocks(const Layout& l, const LBox* boxes, int nbox, const Leapfrog
 void launch_init_first(const Layout& l, const Coeffs& c, const double* d_s, double* u0, double* u1,
                        hipStream_t stream);
 
+// u¹ and u² (the first leapfrog step) computed analytically from φ in one write-only pass, ghosts included:
+// bit-identical to launch_init_first followed by one launch_leapfrog over the whole interior. With `partials`
+// the error of u² vs φ·ct2 over the owned interior is reduced per workgroup (init_two_partials() of them).
+int init_two_partials(const Layout& l);
+void launch_init_two(const Layout& l, const Coeffs& c, const double* d_s, double* u1, double* u2, double ct2,
+                     Partial* partials, hipStream_t stream);
+
 // Runs one leapfrog step over up to 6 boxes in a single launch. If `partials` is non-null the error vs φ·ct is reduced
 // per workgroup into partials[0 .. leapfrog_blocks()).
 void launch_leapfrog(const Layout& l, const Coeffs& c, const double* cur, double* old_out, const LBox* boxes, int nbox,
                      const double* d_s, double ct, Partial* partials, const LeapfrogTiling& t, hipStream_t stream);
+
+// Temporal blocking: TWO leapfrog steps in one pass over HBM (u^{n+1}, u^{n+2} from u^{n−1}, u^n), 16 instead of
+// 24 compulsory bytes per node-step. Needs every node of `box` to be updatable without a halo exchange (single rank:
+// box = the whole global interior) and four distinct buffers (the redundant halo rows of step 1 read u^{n−1} that a
+// neighbouring wave may not yet have consumed, so nothing is overwritten in place). If `partials` is non-null the
+// error of u^{n+2} vs φ·ct2 is reduced per wave.
+struct Leapfrog2Tiling {
+  int rows = 2;           // output rows per wave (1, 2 or 4)
+  int target_waves = 0;   // x-chunking target (0 = auto)
+  bool xcd_remap = true;
+  bool nt_store = true;
+};
+int leapfrog2_partials(const Layout& l, const LBox& box, const Leapfrog2Tiling& t);
+void launch_leapfrog2(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
+                      double* out2, const LBox& box, const double* d_s, double ct2, Partial* partials,
+                      const Leapfrog2Tiling& t, hipStream_t stream);
 
 // Error of a stored field vs φ·ct over `box` (step 1 / standalone check). Writes leapfrog-compatible partials and
 // returns how many.

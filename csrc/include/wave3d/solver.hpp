@@ -35,6 +35,12 @@ struct SolverOptions {
   bool graph = true;            // capture the whole solve into a hipGraph, replay it on every run()
   bool timers = false;          // per-phase hipEvent timers (adds events to the stream; disables the graph)
   LeapfrogTiling tiling;
+  // Temporal blocking: 2 = fuse pairs of steps into one HBM pass (k_leapfrog2) wherever no halo exchange and no
+  // intermediate error check intervene (single rank); 1 = one step per pass everywhere.
+  int temporal = 2;
+  Leapfrog2Tiling tiling2;
+  // Start from u¹, u² computed analytically in one write-only pass (k_init_two) instead of u⁰, u¹ + a first step.
+  bool init2 = true;
 };
 
 struct PhaseTimes {
@@ -100,6 +106,8 @@ class GpuSolver {
  private:
   friend class GpuGroup;
   void enqueue_solve();  // all device work of one solve on s0/s1 (graph-capturable)
+  bool fused() const;    // temporal blocking active for this rank
+  void enqueue_solve_fused();
   void exchange(double* field, hipStream_t st);
   void gather_errors(RunResult& r);
   bool split() const;
@@ -128,7 +136,9 @@ class GpuSolver {
   LBox interior_;
   LBox full_;
 
-  double* u_[2] = {nullptr, nullptr};
+  double* u_[4] = {nullptr, nullptr, nullptr, nullptr};  // [2], [3] only with temporal blocking
+  int nbuf_ = 2;
+  int prev_buf_ = 1;             // buffer index holding u^{K−1} after a solve
   double* d_s_ = nullptr;        // extended sin table (+1 applied when passed to kernels)
   double* send_buf_ = nullptr;   // packed y/z faces
   double* recv_buf_ = nullptr;
@@ -139,8 +149,9 @@ class GpuSolver {
   std::vector<double> ct_;       // cos(a_t n τ)
   hipStream_t s0_ = nullptr, s1_ = nullptr;
   hipEvent_t ev_shell_ = nullptr, ev_halo_ = nullptr, ev_packed_ = nullptr;
-  int n_full_ = 0, n_shell_ = 0, n_int_ = 0;  // error partials of each launch kind
+  int n_full_ = 0, n_shell_ = 0, n_int_ = 0, n_fused_ = 0;  // error partials of each launch kind
   int cur_ = 1, old_ = 0;                     // buffer roles during enqueue
+  int start_n_ = 1;                           // first leapfrog step after the init kernel
   std::vector<char> is_check_;
   hipGraphExec_t graph_exec_ = nullptr;
   int final_buf_ = 0;            // buffer index holding u^K after a solve

@@ -269,6 +269,12 @@ PYBIND11_MODULE(_C, m) {
                              std::uintptr_t stream) {
     launch_init_first(l, c, dptr<const double>(s) + 1, dptr<double>(u0), dptr<double>(u1), sptr(stream));
   });
+  m.def("gpu_init_two_partials", &init_two_partials);
+  m.def("gpu_init_two", [](const Layout& l, const Coeffs& c, std::uintptr_t s, std::uintptr_t u1, std::uintptr_t u2,
+                           double ct2, std::uintptr_t partials, std::uintptr_t stream) {
+    launch_init_two(l, c, dptr<const double>(s) + 1, dptr<double>(u1), dptr<double>(u2), ct2,
+                    dptr<Partial>(partials), sptr(stream));
+  });
   m.def("gpu_leapfrog_blocks", [](const Layout& l, const std::vector<LBox>& boxes, const LeapfrogTiling& t) {
     return leapfrog_blocks(l, boxes.data(), static_cast<int>(boxes.size()), t);
   });
@@ -278,6 +284,21 @@ PYBIND11_MODULE(_C, m) {
           launch_leapfrog(l, c, dptr<const double>(cur), dptr<double>(old), boxes.data(),
                           static_cast<int>(boxes.size()), dptr<const double>(s) + 1, ct, dptr<Partial>(partials), t,
                           sptr(stream));
+        });
+  py::class_<Leapfrog2Tiling>(m, "Leapfrog2Tiling")
+      .def(py::init<>())
+      .def_readwrite("rows", &Leapfrog2Tiling::rows)
+      .def_readwrite("target_waves", &Leapfrog2Tiling::target_waves)
+      .def_readwrite("xcd_remap", &Leapfrog2Tiling::xcd_remap)
+      .def_readwrite("nt_store", &Leapfrog2Tiling::nt_store);
+  m.def("gpu_leapfrog2_partials", &leapfrog2_partials);
+  m.def("gpu_leapfrog2",
+        [](const Layout& l, const Coeffs& c, std::uintptr_t prev, std::uintptr_t cur, std::uintptr_t out1,
+           std::uintptr_t out2, const LBox& box, std::uintptr_t s, double ct2, std::uintptr_t partials,
+           const Leapfrog2Tiling& t, std::uintptr_t stream) {
+          launch_leapfrog2(l, c, dptr<const double>(prev), dptr<const double>(cur), dptr<double>(out1),
+                           dptr<double>(out2), box, dptr<const double>(s) + 1, ct2, dptr<Partial>(partials), t,
+                           sptr(stream));
         });
   m.def("gpu_error_blocks", &error_blocks);
   m.def("gpu_error", [](const Layout& l, std::uintptr_t u, const LBox& b, std::uintptr_t s, double ct,
@@ -301,6 +322,9 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("overlap", &SolverOptions::overlap)
       .def_readwrite("graph", &SolverOptions::graph)
       .def_readwrite("timers", &SolverOptions::timers)
+      .def_readwrite("temporal", &SolverOptions::temporal)
+      .def_readwrite("init2", &SolverOptions::init2)
+      .def_readwrite("tiling2", &SolverOptions::tiling2)
       .def_readwrite("tiling", &SolverOptions::tiling);
 
   py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")

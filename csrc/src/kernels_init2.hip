@@ -1,0 +1,260 @@
+// k_init_two: u¹ and u² generated analytically, write-only (16 B/node). See wave3d/kernels.hpp.
+//
+// u² = 2u¹ − u⁰ + τ²Δ_h u¹ needs u¹ on the 7-point neighbourhood; every u¹ value is φ's first-step value
+// u⁰ + τ²/2·Δ_h u⁰ and every φ is a product of three sin-table entries, so no field is ever read. The products keep
+// exactly the association of phi() and u¹ is formed by the same expression as k_init_first, which makes the output
+// bit-identical to init_first followed by one leapfrog step: one 24 B/node pass is replaced by arithmetic.
+//
+// To keep that arithmetic below the store time, a wave marches along x like the leapfrog kernels: u¹ is evaluated
+// once per plane for R+2 rows (the tile plus one row above/below) and reused from a 3-plane register queue as centre,
+// x-neighbour and y-neighbour; z-neighbours come from the adjacent lanes, with the wave's 64 lanes covering pairs
+// [first−1, first+63) so lanes 0 and 63 are halo lanes (62 output pairs per wave).
+// The kernel writes every node of the allocation whose global index is interior (owned nodes AND the ghost layer
+// towards neighbouring ranks), so no halo exchange is needed before the first leapfrog step; boundary nodes are left
+// untouched (they are zero from allocation on and are never written by any kernel).
+#include <hip/hip_runtime.h>
+
+#include "wave3d/kernels.hpp"
+#include "wave3d/stencil.hpp"
+
+namespace wave3d {
+
+namespace {
+
+using v2d = double __attribute__((ext_vector_type(2)));
+constexpr int kWaves = 4;
+constexpr int kOutPairs = 62;
+
+__device__ __forceinline__ void wave_reduce(double& m, double& s) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const double om = __shfl_xor(m, o, 64);
+    const double os = __shfl_xor(s, o, 64);
+    m = om > m ? om : m;
+    s = s + os;
+  }
+}
+
+struct Init2Params {
+  double* u1;
+  double* u2;
+  const double* s;  // sin table, valid for global indices −1..N+1
+  Partial* partials;
+  i64 N, plane, pitch, gx0, gy0, gz0, zs;
+  i64 x0, x1, y0, y1, zo0, zo1;  // written box (local x, y; z as row offsets): allocation ∩ global interior
+  i64 cx0, cx1, cy0, cy1, czo0, czo1;  // owned compute box (error check)
+  i64 pz0, pz_end;
+  double ihx2, ihy2, ihz2, half_tau2, tau2, ct2;
+  int ntz, nty, xchunk, ntiles, nblocks;
+};
+
+template <int R, bool CHECK>
+__global__ __launch_bounds__(64 * kWaves) void k_init_two(const Init2Params p) {
+  constexpr int J = R + 2;  // rows yt−1 .. yt+R
+  const int lane = static_cast<int>(threadIdx.x) & 63;
+  const int wv = static_cast<int>(threadIdx.x) >> 6;
+  const int blk = (static_cast<int>(blockIdx.x) & 7) * (p.nblocks >> 3) + (static_cast<int>(blockIdx.x) >> 3);
+  const int tile = blk * kWaves + wv;
+  const int pidx = static_cast<int>(blockIdx.x) * kWaves + wv;
+  if (tile >= p.ntiles) {
+    if (CHECK && lane == 0) p.partials[pidx] = make_double2(0.0, 0.0);
+    return;
+  }
+  int t = tile;
+  const int tz = t % p.ntz;
+  t /= p.ntz;
+  const int ty = t % p.nty;
+  const int tx = t / p.nty;
+  const i64 pzt = p.pz0 + static_cast<i64>(tz) * kOutPairs;
+  const int npe = static_cast<int>(imin(kOutPairs, p.pz_end - pzt));
+  const i64 yt = p.y0 + static_cast<i64>(ty) * R;
+  const i64 xs = p.x0 + static_cast<i64>(tx) * p.xchunk;
+  const i64 xe = imin(xs + p.xchunk, p.x1);
+  const i64 N = p.N;
+  const double* s = p.s;
+  auto tab = [&](i64 g) { return s[g < -1 ? -1 : (g > N + 1 ? N + 1 : g)]; };
+
+  const bool outl = lane >= 1 && lane <= npe;
+  const i64 o0 = 2 * (pzt - 1 + lane);
+  const bool w0 = outl && o0 >= p.zo0 && o0 < p.zo1;
+  const bool w1 = outl && o0 + 1 >= p.zo0 && o0 + 1 < p.zo1;
+  const bool k0 = outl && o0 >= p.czo0 && o0 < p.czo1;
+  const bool k1 = outl && o0 + 1 >= p.czo0 && o0 + 1 < p.czo1;
+  // z: global index of element 0, table values at z0−1 .. z0+2, interior flags of the two elements
+  const i64 gz = p.gz0 + o0 - 1 - p.zs;
+  double Z[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) Z[k] = tab(gz - 1 + k);
+  const bool zi0 = gz > 0 && gz < N, zi1 = gz + 1 > 0 && gz + 1 < N;
+  // y: rows yt−1 .. yt+R need table values yt−2 .. yt+R+1
+  double Y[J + 2];
+  bool yi[J];
+#pragma unroll
+  for (int k = 0; k < J + 2; ++k) Y[k] = tab(p.gy0 + yt - 2 + k);
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const i64 g = p.gy0 + yt - 1 + j;
+    yi[j] = g > 0 && g < N;
+  }
+  const double ihx2 = p.ihx2, ihy2 = p.ihy2, ihz2 = p.ihz2;
+
+  // u¹ of plane x (global gx) for all J rows, both elements
+  auto u1_plane = [&](i64 lx, v2d* out) {
+    const i64 g = p.gx0 + lx;
+    const double xm = tab(g - 1), xc = tab(g), xp = tab(g + 1);
+    const bool xi = g > 0 && g < N;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const double ym = Y[j], yc = Y[j + 1], yp = Y[j + 2];
+      double r[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const double zc = Z[e + 1];
+        const double v = (xc * yc) * zc;
+        const double lap = lap7(v, (xm * yc) * zc, (xp * yc) * zc, (xc * ym) * zc, (xc * yp) * zc, (xc * yc) * Z[e],
+                                (xc * yc) * Z[e + 2], ihx2, ihy2, ihz2);
+        const bool in = xi && yi[j] && (e == 0 ? zi0 : zi1);
+        r[e] = in ? first_step(v, lap, p.half_tau2) : 0.0;
+      }
+      out[j].x = r[0];
+      out[j].y = r[1];
+    }
+  };
+
+  v2d um[J], uc[J], up[J];
+  u1_plane(xs - 1, um);
+  u1_plane(xs, uc);
+  double emax = 0.0, esum = 0.0;
+  for (i64 x = xs; x < xe; ++x) {
+    u1_plane(x + 1, up);
+    const i64 gxx = p.gx0 + x;
+    const double xc = tab(gxx);
+    const bool xi = gxx > 0 && gxx < N;
+    const bool xown = x >= p.cx0 && x < p.cx1;
+    const i64 pbase = (x + 1) * p.plane;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int j = r + 1;
+      const i64 y = yt + r;
+      if (y >= p.y1) continue;
+      const double zm = __shfl_up(uc[j].y, 1, 64);
+      const double zp = __shfl_down(uc[j].x, 1, 64);
+      v2d u2v;
+      const double l0 = lap7(uc[j].x, um[j].x, up[j].x, uc[j - 1].x, uc[j + 1].x, zm, uc[j].y, ihx2, ihy2, ihz2);
+      const double l1 = lap7(uc[j].y, um[j].y, up[j].y, uc[j - 1].y, uc[j + 1].y, uc[j].x, zp, ihx2, ihy2, ihz2);
+      const double yc = Y[j + 1];
+      const double u00 = (xc * yc) * Z[1], u01 = (xc * yc) * Z[2];  // u⁰ = φ
+      const bool in = xi && yi[j];
+      u2v.x = in && zi0 ? leapfrog(uc[j].x, u00, l0, p.tau2) : 0.0;
+      u2v.y = in && zi1 ? leapfrog(uc[j].y, u01, l1, p.tau2) : 0.0;
+      const i64 off = pbase + (y + 1) * p.pitch + o0;
+      if (w0 && w1) {
+        __builtin_nontemporal_store(uc[j], reinterpret_cast<v2d*>(p.u1 + off));
+        __builtin_nontemporal_store(u2v, reinterpret_cast<v2d*>(p.u2 + off));
+      } else if (w0) {
+        p.u1[off] = uc[j].x;
+        p.u2[off] = u2v.x;
+      } else if (w1) {
+        p.u1[off + 1] = uc[j].y;
+        p.u2[off + 1] = u2v.y;
+      }
+      if (CHECK && xown && y >= p.cy0 && y < p.cy1) {
+        if (k0) {
+          const double er = fabs(u2v.x - u00 * p.ct2);
+          emax = er > emax ? er : emax;
+          esum += er * er;
+        }
+        if (k1) {
+          const double er = fabs(u2v.y - u01 * p.ct2);
+          emax = er > emax ? er : emax;
+          esum += er * er;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      um[j] = uc[j];
+      uc[j] = up[j];
+    }
+  }
+  if (CHECK) {
+    wave_reduce(emax, esum);
+    if (lane == 0) p.partials[pidx] = make_double2(emax, esum);
+  }
+}
+
+constexpr int kRows = 2;
+
+Init2Params make_params(const Layout& l, const Coeffs& c) {
+  Init2Params p{};
+  p.N = l.N;
+  p.plane = l.plane;
+  p.pitch = l.pitch;
+  p.gx0 = l.gx0;
+  p.gy0 = l.gy0;
+  p.gz0 = l.gz0;
+  p.zs = l.zs;
+  // written box: local indices in [−1, n] whose global index is interior
+  auto lo = [&](i64 g0) { return imax(-1, 1 - g0); };
+  auto hi = [&](i64 g0, i64 n) { return imin(n + 1, l.N - g0); };
+  p.x0 = lo(l.gx0);
+  p.x1 = imax(p.x0, hi(l.gx0, l.nx));
+  p.y0 = lo(l.gy0);
+  p.y1 = imax(p.y0, hi(l.gy0, l.ny));
+  const i64 z0 = lo(l.gz0), z1 = imax(z0, hi(l.gz0, l.nz));
+  p.zo0 = z0 + 1 + l.zs;
+  p.zo1 = z1 + 1 + l.zs;
+  p.cx0 = l.cx0;
+  p.cx1 = l.cx1;
+  p.cy0 = l.cy0;
+  p.cy1 = l.cy1;
+  p.czo0 = l.cz0 + 1 + l.zs;
+  p.czo1 = l.cz1 + 1 + l.zs;
+  p.pz0 = p.zo0 / 2;
+  p.pz_end = (p.zo1 + 1) / 2;
+  W3D_REQUIRE(2 * p.pz_end <= l.pitch, "row layout too tight for init_two");
+  p.ihx2 = c.ihx2;
+  p.ihy2 = c.ihy2;
+  p.ihz2 = c.ihz2;
+  p.half_tau2 = c.half_tau2;
+  p.tau2 = c.tau2;
+  const i64 nxb = p.x1 - p.x0, nyb = p.y1 - p.y0;
+  if (nxb <= 0 || nyb <= 0 || p.pz_end <= p.pz0) return p;  // nothing to write
+  p.ntz = static_cast<int>(ceil_div(p.pz_end - p.pz0, kOutPairs));
+  p.nty = static_cast<int>(ceil_div(nyb, kRows));
+  const i64 base = static_cast<i64>(p.ntz) * p.nty;
+  const i64 target = 256 * 16;
+  const i64 chunk = imin(nxb, imax(8, ceil_div(nxb, imax(1, ceil_div(target, base)))));
+  p.xchunk = static_cast<int>(chunk);
+  const i64 tiles = base * ceil_div(nxb, chunk);
+  W3D_REQUIRE(tiles < (1ll << 30), "too many tiles");
+  p.ntiles = static_cast<int>(tiles);
+  p.nblocks = static_cast<int>(round_up(ceil_div(tiles, kWaves), 8));
+  return p;
+}
+
+}  // namespace
+
+int init_two_partials(const Layout& l) {
+  const Init2Params p = make_params(l, Coeffs{1, 1, 1, 1, 0.5});
+  return p.nblocks * kWaves;
+}
+
+void launch_init_two(const Layout& l, const Coeffs& c, const double* d_s, double* u1, double* u2, double ct2,
+                     Partial* partials, hipStream_t stream) {
+  Init2Params p = make_params(l, c);
+  if (p.nblocks == 0) return;
+  p.u1 = u1;
+  p.u2 = u2;
+  p.s = d_s;
+  p.partials = partials;
+  p.ct2 = ct2;
+  if (partials)
+    hipLaunchKernelGGL((k_init_two<kRows, true>), dim3(p.nblocks), dim3(64 * kWaves), 0, stream, p);
+  else
+    hipLaunchKernelGGL((k_init_two<kRows, false>), dim3(p.nblocks), dim3(64 * kWaves), 0, stream, p);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) fail(std::string("init_two launch: ") + hipGetErrorString(e));
+}
+
+}  // namespace wave3d

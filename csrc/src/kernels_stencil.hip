@@ -648,11 +648,11 @@ __global__ __launch_bounds__(1024) void k_reduce(const Partial* __restrict__ in,
 // ---------------------------------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------------------------------
-void launch_init_first(const Layout& l, const Coeffs& c, const double* d_s, double* u0, double* u1,
-                       hipStream_t stream) {
+namespace {
+InitParams init_params(const Layout& l, const Coeffs& c, const double* d_s, double* a, double* b) {
   InitParams p;
-  p.u0 = u0;
-  p.u1 = u1;
+  p.u0 = a;
+  p.u1 = b;
   p.s = d_s;
   p.plane = l.plane;
   p.N = l.N;
@@ -671,6 +671,13 @@ void launch_init_first(const Layout& l, const Coeffs& c, const double* d_s, doub
   p.ihy2 = c.ihy2;
   p.ihz2 = c.ihz2;
   p.half_tau2 = c.half_tau2;
+  return p;
+}
+}  // namespace
+
+void launch_init_first(const Layout& l, const Coeffs& c, const double* d_s, double* u0, double* u1,
+                       hipStream_t stream) {
+  const InitParams p = init_params(l, c, d_s, u0, u1);
   const dim3 grid(static_cast<unsigned>(ceil_div(p.pairs_per_plane, 256)), static_cast<unsigned>(l.nx + 2));
   hipLaunchKernelGGL(k_init_first, grid, dim3(256), 0, stream, p);
   W3D_HIP_CHECK(hipGetLastError());

@@ -116,7 +116,8 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   W3D_HIP(hipEventCreateWithFlags(&ev_shell_, hipEventDisableTiming));
   W3D_HIP(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
   W3D_HIP(hipEventCreateWithFlags(&ev_packed_, hipEventDisableTiming));
-  for (int b = 0; b < 2; ++b) {
+  nbuf_ = (opt_.temporal == 2 && !plan_.any() && world_ == 1) ? 4 : 2;
+  for (int b = 0; b < nbuf_; ++b) {
     W3D_HIP(hipMalloc(&u_[b], static_cast<size_t>(lay_.bytes())));
     W3D_HIP(hipMemset(u_[b], 0, static_cast<size_t>(lay_.bytes())));
   }
@@ -130,7 +131,9 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   n_full_ = leapfrog_blocks(lay_, &full_, 1, opt_.tiling);
   n_shell_ = leapfrog_blocks(lay_, shell_.data(), static_cast<int>(shell_.size()), opt_.tiling);
   n_int_ = leapfrog_blocks(lay_, &interior_, 1, opt_.tiling);
-  n_partials_ = std::max({n_full_, n_shell_ + n_int_, error_blocks(lay_, full_), 1});
+  n_fused_ = (nbuf_ == 4 && !full_.empty()) ? leapfrog2_partials(lay_, full_, opt_.tiling2) : 0;
+  n_partials_ = std::max({n_full_, n_shell_ + n_int_, error_blocks(lay_, full_), n_fused_,
+                          opt_.init2 ? init_two_partials(lay_) : 0, 1});
   W3D_HIP(hipMalloc(&partials_, static_cast<size_t>(n_partials_) * sizeof(Partial)));
   W3D_HIP(hipMalloc(&errlog_, static_cast<size_t>(prob_.K + 1) * sizeof(Partial)));
   W3D_HIP(hipMalloc(&errall_, static_cast<size_t>(world_) * (prob_.K + 1) * sizeof(Partial)));
@@ -141,7 +144,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
 
 GpuSolver::~GpuSolver() {
   if (graph_exec_) hipGraphExecDestroy(graph_exec_);
-  for (double* p : {u_[0], u_[1], d_s_, send_buf_, recv_buf_})
+  for (double* p : {u_[0], u_[1], u_[2], u_[3], d_s_, send_buf_, recv_buf_})
     if (p) hipFree(p);
   if (partials_) hipFree(partials_);
   if (errlog_) hipFree(errlog_);
@@ -155,7 +158,7 @@ GpuSolver::~GpuSolver() {
 }
 
 size_t GpuSolver::device_bytes() const {
-  return 2 * static_cast<size_t>(lay_.bytes()) + 2 * static_cast<size_t>(plan_.packed_doubles) * sizeof(double) +
+  return static_cast<size_t>(nbuf_) * static_cast<size_t>(lay_.bytes()) + 2 * static_cast<size_t>(plan_.packed_doubles) * sizeof(double) +
          static_cast<size_t>(n_partials_) * sizeof(Partial) + static_cast<size_t>(prob_.N + 3) * sizeof(double);
 }
 
@@ -191,7 +194,7 @@ bool GpuSolver::split() const { return opt_.overlap && plan_.any(); }
 
 bool GpuSolver::needs_exchange(int n) const {
   if (!plan_.any()) return false;
-  return split() ? n < prob_.K - 1 : n >= 2;
+  return split() ? n < prob_.K - 1 : n > start_n_;
 }
 
 double* GpuSolver::xfield() const { return split() ? u_[old_] : u_[cur_]; }
@@ -204,10 +207,22 @@ void GpuSolver::phase_init() {
   for (int n : check_steps()) is_check_[static_cast<size_t>(n)] = 1;
   if (opt_.timers) W3D_HIP(hipEventRecord(tev_[0], s0_));
   W3D_HIP(hipMemsetAsync(errlog_, 0, static_cast<size_t>(K + 1) * sizeof(Partial), s0_));
-  launch_init_first(lay_, coef_, s, u_[0], u_[1], s0_);
-  if (is_check_[1]) {
-    launch_error(lay_, u_[1], full_, s, ct_[1], partials_, s0_);
-    launch_reduce(partials_, error_blocks(lay_, full_), errlog_ + 1, s0_);
+  if (opt_.init2 && K >= 2) {
+    // u¹ -> buf 0, u² -> buf 1 analytically (no read pass); the first leapfrog step is n = 2
+    launch_init_two(lay_, coef_, s, u_[0], u_[1], ct_[2], is_check_[2] ? partials_ : nullptr, s0_);
+    if (is_check_[2]) launch_reduce(partials_, init_two_partials(lay_), errlog_ + 2, s0_);
+    if (is_check_[1]) {
+      launch_error(lay_, u_[0], full_, s, ct_[1], partials_, s0_);
+      launch_reduce(partials_, error_blocks(lay_, full_), errlog_ + 1, s0_);
+    }
+    start_n_ = 2;
+  } else {
+    launch_init_first(lay_, coef_, s, u_[0], u_[1], s0_);
+    if (is_check_[1]) {
+      launch_error(lay_, u_[1], full_, s, ct_[1], partials_, s0_);
+      launch_reduce(partials_, error_blocks(lay_, full_), errlog_ + 1, s0_);
+    }
+    start_n_ = 1;
   }
   if (opt_.timers) W3D_HIP(hipEventRecord(tev_[1], s0_));
   cur_ = 1;
@@ -252,13 +267,53 @@ void GpuSolver::phase_interior(int n) {
 }
 
 void GpuSolver::enqueue_solve() {
+  if (fused()) {
+    enqueue_solve_fused();
+    return;
+  }
   phase_init();
-  for (int n = 1; n <= prob_.K - 1; ++n) {
+  for (int n = start_n_; n <= prob_.K - 1; ++n) {
     phase_shell(n);
     phase_exchange_rccl(n);
     phase_interior(n);
   }
   final_buf_ = cur_;
+  prev_buf_ = old_;
+}
+
+bool GpuSolver::fused() const { return opt_.temporal == 2 && !plan_.any() && nbuf_ == 4 && !full_.empty(); }
+
+// Single rank with temporal blocking: steps are taken two at a time (u^{n+1}, u^{n+2} in one HBM pass) whenever the
+// intermediate step n+1 needs no error check; otherwise one in-place step. Four buffers rotate (see kernels.hpp).
+void GpuSolver::enqueue_solve_fused() {
+  phase_init();  // (u0, u1) or (u1, u2) -> bufs (0, 1); cur_ = 1, old_ = 0
+  const int K = prob_.K;
+  const double* s = d_s_ + 1;
+  int n = start_n_;  // u^n is current
+  while (n <= K - 1) {
+    if (n + 2 <= K && !is_check_[static_cast<size_t>(n + 1)]) {
+      int f[2], k = 0;
+      for (int b = 0; b < 4; ++b)
+        if (b != cur_ && b != old_) f[k++] = b;
+      const bool chk = is_check_[static_cast<size_t>(n + 2)] != 0;
+      launch_leapfrog2(lay_, coef_, u_[old_], u_[cur_], u_[f[0]], u_[f[1]], full_, s,
+                       ct_[static_cast<size_t>(n + 2)], chk ? partials_ : nullptr, opt_.tiling2, s0_);
+      if (chk) launch_reduce(partials_, n_fused_, errlog_ + n + 2, s0_);
+      old_ = f[0];
+      cur_ = f[1];
+      n += 2;
+    } else {
+      const bool chk = is_check_[static_cast<size_t>(n + 1)] != 0;
+      launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &full_, 1, s, ct_[static_cast<size_t>(n + 1)],
+                      chk ? partials_ : nullptr, opt_.tiling, s0_);
+      if (chk) launch_reduce(partials_, n_full_, errlog_ + n + 1, s0_);
+      std::swap(cur_, old_);
+      n += 1;
+    }
+  }
+  final_buf_ = cur_;
+  prev_buf_ = old_;
+  if (opt_.timers) W3D_HIP(hipEventRecord(tev_[2], s0_));
 }
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -384,7 +439,7 @@ RunResult GpuSolver::run() {
 
 std::vector<double> GpuSolver::download(int which) const {
   std::vector<double> h(static_cast<size_t>(lay_.total));
-  const double* src = u_[which == 0 ? final_buf_ : 1 - final_buf_];
+  const double* src = u_[which == 0 ? final_buf_ : prev_buf_];
   W3D_HIP(hipDeviceSynchronize());
   W3D_HIP(hipMemcpy(h.data(), src, h.size() * sizeof(double), hipMemcpyDeviceToHost));
   return h;
@@ -426,7 +481,7 @@ RunResult GpuGroup::run() {
   const int K = rs[0]->prob_.K;
   const double t0 = now_s();
   for (auto* s : rs) s->phase_init();
-  for (int n = 1; n <= K - 1; ++n) {
+  for (int n = rs[0]->start_n_; n <= K - 1; ++n) {
     for (auto* s : rs) s->phase_shell(n);
     for (auto* s : rs) s->lb_pack(n);
     for (auto* s : rs) s->lb_pull(n, rs);
@@ -438,6 +493,7 @@ RunResult GpuGroup::run() {
   std::vector<Partial> all(per * rs.size());
   for (size_t q = 0; q < rs.size(); ++q) {
     rs[q]->final_buf_ = rs[q]->cur_;
+    rs[q]->prev_buf_ = rs[q]->old_;
     W3D_HIP(hipMemcpyAsync(all.data() + q * per, rs[q]->errlog_, per * sizeof(Partial), hipMemcpyDeviceToHost,
                            rs[q]->s0_));
   }

@@ -86,6 +86,27 @@ def leapfrog(layout, coeffs, cur: torch.Tensor, old: torch.Tensor, boxes, s_ext:
     return acc
 
 
+def leapfrog2(layout, coeffs, prev: torch.Tensor, cur: torch.Tensor, out1: torch.Tensor, out2: torch.Tensor, box,
+              s_ext: torch.Tensor, ct2: float = 0.0, check: bool = False, tiling=None):
+    """Two fused leapfrog steps (HIP only): out1 = u^{n+1}, out2 = u^{n+2} from prev = u^{n-1}, cur = u^n.
+
+    ``box`` must be the whole single-rank interior. Returns the (L∞, Σe²) error of u^{n+2} if ``check``."""
+    C = _C()
+    if not cur.is_cuda:
+        raise ValueError("leapfrog2 is a GPU kernel; on the CPU take two leapfrog() steps")
+    t = tiling if tiling is not None else C.Leapfrog2Tiling()
+    nb = C.gpu_leapfrog2_partials(layout, box, t)
+    part = torch.empty((max(nb, 1), 2), dtype=torch.float64, device=cur.device) if check else None
+    C.gpu_leapfrog2(layout, coeffs, prev.data_ptr(), cur.data_ptr(), out1.data_ptr(), out2.data_ptr(), box,
+                    s_ext.data_ptr(), ct2, part.data_ptr() if check else 0, t, _stream())
+    if not check:
+        return None
+    out = torch.empty(2, dtype=torch.float64, device=cur.device)
+    C.gpu_reduce(part.data_ptr(), nb, out.data_ptr(), _stream())
+    o = out.cpu()
+    return float(o[0]), float(o[1])
+
+
 def error(layout, u: torch.Tensor, box, s_ext: torch.Tensor, ct: float):
     C = _C()
     if u.is_cuda:

@@ -72,7 +72,8 @@ class Solver:
     def __init__(self, spec: ProblemSpec, backend: str = "auto", transport: str = "auto", decomp: str = "slab",
                  rank: int | None = None, world: int | None = None, device: int | None = None,
                  overlap: bool = True, graph: bool = True, threads: int = 0, tiling: dict | None = None,
-                 comm=None, group=None, stage_via_host: bool = False, force: bool = False):
+                 comm=None, group=None, stage_via_host: bool = False, force: bool = False, temporal: int = 2,
+                 tiling2: dict | None = None, init2: bool = True):
         import torch.distributed as dist
 
         if not spec.cfl_ok and not force:
@@ -98,13 +99,13 @@ class Solver:
         else:
             self.device = torch.device("cpu")
         if self.backend == "hip" and self.transport == "loopback":
-            opts = self._options(C, decomp, spec, overlap, False, tiling)
+            opts = self._options(C, decomp, spec, overlap, False, tiling, temporal, tiling2, init2)
             self._impl = C.GpuGroup(spec.native(), opts, world)
             self.dims = self._impl.dims().as_tuple()
         elif self.backend == "hip" and self.transport == "rccl":
             from .parallel.rccl import make_comm
 
-            opts = self._options(C, decomp, spec, overlap, graph, tiling)
+            opts = self._options(C, decomp, spec, overlap, graph, tiling, temporal, tiling2, init2)
             if comm is None and world > 1:
                 comm = make_comm(rank, world, group)
             self.comm = comm
@@ -122,8 +123,13 @@ class Solver:
             self.dims = (1, 1, 1)
 
     @staticmethod
-    def _options(C, decomp, spec, overlap, graph, tiling):
+    def _options(C, decomp, spec, overlap, graph, tiling, temporal=2, tiling2=None, init2=True):
         opts = C.SolverOptions()
+        opts.temporal = temporal
+        opts.init2 = init2
+        if tiling2:
+            for k, v in tiling2.items():
+                setattr(opts.tiling2, k, v)
         opts.decomp = decomp
         opts.check_every = spec.check_every
         opts.overlap = overlap

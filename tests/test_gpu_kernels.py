@@ -124,3 +124,82 @@ def test_pack_unpack(gpu, decomp, world, rank):
     ops.unpack(lay, plan, src.cuda(), v_gpu)
     torch.cuda.synchronize()
     assert torch.equal(v_gpu.cpu(), v_cpu)
+
+
+@pytest.mark.parametrize("rows", [1, 2, 4])
+@pytest.mark.parametrize("N", [40, 77, 130])
+@pytest.mark.parametrize("target_waves", [0, 50])
+def test_leapfrog2_equals_two_single_steps(gpu, rows, N, target_waves):
+    """Temporal blocking: one fused pass == two CPU steps, bit for bit (random interior, Dirichlet-zero boundary)."""
+    C = gpu
+    prob, co, lay, _ = _setup(C, N)
+    box = C.compute_box(lay)
+    torch.manual_seed(N * 7 + rows)
+
+    def rand_field():
+        g = torch.zeros((int(lay.nx) + 2, int(lay.ny) + 2, int(lay.nz) + 2), dtype=torch.float64)
+        g[2:-2, 2:-2, 2:-2] = torch.randn(int(lay.nx) - 2, int(lay.ny) - 2, int(lay.nz) - 2, dtype=torch.float64)
+        return ops.from_grid(lay, g)
+
+    prev, cur = rand_field(), rand_field()
+    s = ops.sin_table_ext(prob)
+    ct2 = math.cos(prob.a_t * 6 * prob.tau)
+    # CPU: u^{n+1} in place over prev, then u^{n+2} in place over cur
+    a, b = prev.clone(), cur.clone()
+    ops.leapfrog(lay, co, b, a, [box], s)          # a = u^{n+1}
+    e_cpu = ops.leapfrog(lay, co, a, b, [box], s, ct2, check=True)  # b = u^{n+2}
+    t = C.Leapfrog2Tiling()
+    t.rows, t.target_waves = rows, target_waves
+    o1 = torch.zeros(int(lay.total), dtype=torch.float64, device="cuda")
+    o2 = torch.zeros_like(o1)
+    e_gpu = ops.leapfrog2(lay, co, prev.cuda(), cur.cuda(), o1, o2, box, s.cuda(), ct2, check=True, tiling=t)
+    torch.cuda.synchronize()
+    # the fused kernel writes only the interior; boundary/ghost nodes of the outputs stay 0 like the inputs' boundary
+    assert torch.equal(ops.to_grid(lay, o1.cpu()), ops.to_grid(lay, a))
+    assert torch.equal(ops.to_grid(lay, o2.cpu()), ops.to_grid(lay, b))
+    assert e_gpu[0] == e_cpu[0] and math.isclose(e_gpu[1], e_cpu[1], rel_tol=1e-12)
+
+
+@pytest.mark.parametrize("N,world,rank,decomp", [(36, 1, 0, "slab"), (53, 1, 0, "slab"), (40, 2, 1, "slab"),
+                                                 (45, 8, 5, "2x2x2"), (38, 6, 2, "1x2x3")])
+@pytest.mark.parametrize("check", [False, True])
+def test_init_two_equals_init_plus_step(gpu, N, world, rank, decomp, check):
+    """k_init_two (u¹, u² analytically) == init_first + one leapfrog step of the GLOBAL field, ghosts included."""
+    C = gpu
+    prob, co, lay, _ = _setup(C, N, world, rank, decomp)
+    # global reference on the CPU
+    g_prob, g_co, g_lay, _ = _setup(C, N)
+    s = ops.sin_table_ext(prob)
+    u0, u1 = ops.alloc_field(g_lay), ops.alloc_field(g_lay)
+    ops.init_first(g_lay, g_co, s, u0, u1)
+    u2 = u0.clone()
+    ct2 = math.cos(prob.a_t * 2 * prob.tau)
+    ops.leapfrog(g_lay, g_co, u1, u2, [C.compute_box(g_lay)], s)
+    G1, G2 = ops.to_grid(g_lay, u1), ops.to_grid(g_lay, u2)
+    a = ops.alloc_field(lay, "cuda")
+    b = ops.alloc_field(lay, "cuda")
+    nb = C.gpu_init_two_partials(lay)
+    part = torch.zeros((nb, 2), dtype=torch.float64, device="cuda")
+    C.gpu_init_two(lay, co, s.cuda().data_ptr(), a.data_ptr(), b.data_ptr(), ct2, part.data_ptr() if check else 0,
+                   torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    A, B = ops.to_grid(lay, a.cpu()), ops.to_grid(lay, b.cpu())
+    # local grid index i <-> global node gx0 - 1 + i; compare every allocated node inside the global grid
+    n = N + 1
+    xs = slice(max(0, 1 - int(lay.gx0)), min(int(lay.nx) + 2, n + 1 - int(lay.gx0)))
+    ys = slice(max(0, 1 - int(lay.gy0)), min(int(lay.ny) + 2, n + 1 - int(lay.gy0)))
+    zs = slice(max(0, 1 - int(lay.gz0)), min(int(lay.nz) + 2, n + 1 - int(lay.gz0)))
+
+    def gsl(sl, g0):
+        return slice(sl.start + g0, sl.stop + g0)  # +1 (ghost) -1 (local->global) cancel in the padded grids
+
+    ref1 = G1[gsl(xs, int(lay.gx0)), gsl(ys, int(lay.gy0)), gsl(zs, int(lay.gz0))]
+    ref2 = G2[gsl(xs, int(lay.gx0)), gsl(ys, int(lay.gy0)), gsl(zs, int(lay.gz0))]
+    assert torch.equal(A[xs, ys, zs], ref1)
+    assert torch.equal(B[xs, ys, zs], ref2)
+    if check:
+        out = torch.empty(2, dtype=torch.float64, device="cuda")
+        C.gpu_reduce(part.data_ptr(), nb, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        e = ops.error(lay, b.cpu(), C.compute_box(lay), s, ct2)
+        o = out.cpu()
+        assert float(o[0]) == e[0] and math.isclose(float(o[1]), e[1], rel_tol=1e-12)

@@ -67,3 +67,32 @@ def test_tilings_agree(gpu, tiling):
     ra, rb = a.run(), b.run()
     assert ra.max_err == rb.max_err
     assert torch.equal(a.owned_field(0), b.owned_field(0))
+
+
+@pytest.mark.parametrize("N,K,ce", [(64, 20, 2), (65, 9, 3), (50, 7, 0), (48, 6, 1)])
+def test_temporal_blocking_identical(gpu, N, K, ce):
+    spec = ProblemSpec(N=N, tau=1e-3, K=K, check_every=ce)
+    a = Solver(spec, backend="hip", device=0, temporal=1)
+    b = Solver(spec, backend="hip", device=0, temporal=2)
+    ra, rb = a.run(), b.run()
+    assert ra.steps == rb.steps and ra.max_err == rb.max_err
+    for x, y in zip(ra.rms_err, rb.rms_err):
+        assert math.isclose(x, y, rel_tol=1e-12)
+    assert torch.equal(a.owned_field(0), b.owned_field(0))
+    assert torch.equal(a.owned_field(1), b.owned_field(1))
+    rb2 = b.run()
+    assert rb2.max_err == rb.max_err
+
+
+@pytest.mark.parametrize("temporal", [1, 2])
+@pytest.mark.parametrize("N,K,ce", [(60, 12, 2), (45, 2, 1), (50, 5, 1), (33, 1, 2)])
+def test_init2_identical(gpu, temporal, N, K, ce):
+    spec = ProblemSpec(N=N, tau=1e-3, K=K, check_every=ce)
+    a = Solver(spec, backend="hip", device=0, temporal=temporal, init2=False)
+    b = Solver(spec, backend="hip", device=0, temporal=temporal, init2=True)
+    ra, rb = a.run(), b.run()
+    assert ra.steps == rb.steps and ra.max_err == rb.max_err
+    for x, y in zip(ra.rms_err, rb.rms_err):
+        assert math.isclose(x, y, rel_tol=1e-12)
+    assert torch.equal(a.owned_field(0), b.owned_field(0))
+    assert torch.equal(a.owned_field(1), b.owned_field(1))

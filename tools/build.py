@@ -42,6 +42,8 @@ CPU_FLAGS = COMMON + ["-fopenmp", "-march=x86-64-v2"]
 LIB_SOURCES = [
     ("src/kernels_stencil.hip", "hip"),
     ("src/kernels_halo.hip", "hip"),
+    ("src/kernels_leapfrog2.hip", "hip"),
+    ("src/kernels_init2.hip", "hip"),
     ("src/solver_gpu.cpp", "hip"),
     ("src/cpu_kernels.cpp", "cpu"),
     ("src/cpu_solver.cpp", "cpu"),

@@ -42,6 +42,8 @@ def main() -> int:
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--json", default="")
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--minimal", action="store_true", help="only the default single-step and two-step kernels "
+                    "(for counter collection under rocprofv3)")
     a = ap.parse_args()
     import torch
 
@@ -80,7 +82,9 @@ def main() -> int:
         configs.append(dict(variant=1, rows=rows, target_blocks=tb, xcd_remap=rm, nt_store=nt))
     if a.quick:
         configs = [c for c in configs if c["target_blocks"] == 0 and c["xcd_remap"]]
-    for cfg, chk in itertools.product(configs, [False, True] if not a.quick else [False]):
+    if a.minimal:
+        configs = [dict(variant=1, rows=2, target_blocks=0, xcd_remap=True, nt_store=True)]
+    for cfg, chk in itertools.product(configs, [False, True] if not (a.quick or a.minimal) else [False]):
         tl = C.LeapfrogTiling()
         for k, v in cfg.items():
             setattr(tl, k, v)
@@ -95,10 +99,32 @@ def main() -> int:
         t = timeit(step, a.iters)
         out.append({"kernel": "k_leapfrog", **cfg, "partials": nb, "check": chk, "us": t,
                     "TBps": 24 * nodes / t / 1e6})
+    # temporally blocked two-step kernel: 32 B per node per pass = 16 B per node-step
+    bufs = [ops.alloc_field(lay, "cuda") for _ in range(2)]
+    sweep2 = list(itertools.product([1, 2, 4], [0, 4096, 8192, 16384], [True, False],
+                                    [False, True] if not a.quick else [False]))
+    if a.minimal:
+        sweep2 = [(1, 0, True, False), (2, 0, True, False)]
+    for rows, tw, nt, chk in sweep2:
+        t2 = C.Leapfrog2Tiling()
+        t2.rows, t2.target_waves, t2.nt_store = rows, tw, nt
+        nb = C.gpu_leapfrog2_partials(lay, box, t2)
+        part = torch.empty((nb, 2), dtype=torch.float64, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+
+        def pass2():
+            C.gpu_leapfrog2(lay, co, u0.data_ptr(), u1.data_ptr(), bufs[0].data_ptr(), bufs[1].data_ptr(), box,
+                            s.data_ptr(), 0.5, part.data_ptr() if chk else 0, t2, st)
+
+        t = timeit(pass2, a.iters)
+        out.append({"kernel": "k_leapfrog2", "rows": rows, "target_waves": tw, "nt_store": nt, "partials": nb,
+                    "check": chk, "us": t, "us_per_step": t / 2, "TBps": 32 * nodes / t / 1e6})
     for r in out:
         print(json.dumps(r), flush=True)
     best = min((r for r in out if r["kernel"] == "k_leapfrog"), key=lambda r: r["us"])
     print("BEST", json.dumps(best))
+    best2 = min((r for r in out if r["kernel"] == "k_leapfrog2"), key=lambda r: r["us"])
+    print("BEST2", json.dumps(best2))
     if a.json:
         with open(a.json, "w") as f:
             json.dump(out, f, indent=1)

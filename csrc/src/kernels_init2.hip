@@ -52,7 +52,7 @@ template <int R, bool CHECK>
 __global__ __launch_bounds__(64 * kWaves) void k_init_two(const Init2Params p) {
   constexpr int J = R + 2;  // rows yt−1 .. yt+R
   const int lane = static_cast<int>(threadIdx.x) & 63;
-  const int wv = static_cast<int>(threadIdx.x) >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);  // wave-uniform: tile math stays scalar
   const int blk = (static_cast<int>(blockIdx.x) & 7) * (p.nblocks >> 3) + (static_cast<int>(blockIdx.x) >> 3);
   const int tile = blk * kWaves + wv;
   const int pidx = static_cast<int>(blockIdx.x) * kWaves + wv;

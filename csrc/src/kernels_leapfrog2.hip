@@ -67,7 +67,7 @@ template <int R, bool CHECK, bool NT>
 __global__ __launch_bounds__(64 * kWaves) void k_leapfrog2_rq(const Lf2Params p) {
   constexpr int E = R + 4;  // extended rows: e ↔ y = yt − 2 + e
   const int lane = static_cast<int>(threadIdx.x) & 63;
-  const int wv = static_cast<int>(threadIdx.x) >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);  // wave-uniform: tile math stays scalar
   int blk = static_cast<int>(blockIdx.x);
   if (p.xcd_remap) {
     const int per = p.nblocks >> 3;
@@ -99,13 +99,15 @@ __global__ __launch_bounds__(64 * kWaves) void k_leapfrog2_rq(const Lf2Params p)
   const bool ok0 = outl && in0, ok1 = outl && in1;
   const i64 pitch = p.pitch, plane = p.plane;
 
-  // per extended row: offset of my pair, load validity (inside the allocation), interior mask (stage 1)
+  // per extended row: wave-uniform row offset (scalar registers) + one 32-bit lane offset shared by every row, so
+  // each load is a scalar base + vector offset (no 64-bit address per row in VGPRs); load validity; interior mask
+  const int lo = static_cast<int>(o0);
   i64 rb[E];
   bool rl[E], ri[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const i64 y = yt - 2 + e;
-    rb[e] = (y + 1) * pitch + o0;
+    rb[e] = (y + 1) * pitch;
     rl[e] = ld && y >= -1 && y <= p.ny;
     ri[e] = y >= p.y0 && y < p.y1;
   }
@@ -130,11 +132,11 @@ __global__ __launch_bounds__(64 * kWaves) void k_leapfrog2_rq(const Lf2Params p)
     w1[e] = z2;
     w2[e] = z2;
     if (rl[e]) {
-      c[e] = ld2(cur + px + rb[e]);
+      c[e] = ld2(cur + (px + rb[e]) + lo);
       if (e >= 1 && e <= E - 2) {
-        m[e] = ld2(cur + px - plane + rb[e]);
-        q[e] = ld2(cur + px + plane + rb[e]);
-        o[e] = ld2(prev + px + rb[e]);
+        m[e] = ld2(cur + (px - plane + rb[e]) + lo);
+        q[e] = ld2(cur + (px + plane + rb[e]) + lo);
+        o[e] = ld2(prev + (px + rb[e]) + lo);
       }
     }
   }
@@ -160,10 +162,10 @@ __global__ __launch_bounds__(64 * kWaves) void k_leapfrog2_rq(const Lf2Params p)
       no[e] = z2;
       if (more && rl[e]) {
         if (e >= 1 && e <= E - 2) {
-          nq[e] = ld2(cur + px + 2 * plane + rb[e]);
-          no[e] = ld2(prev + px + plane + rb[e]);
+          nq[e] = ld2(cur + (px + 2 * plane + rb[e]) + lo);
+          no[e] = ld2(prev + (px + plane + rb[e]) + lo);
         } else {
-          nc[e] = ld2(cur + px + plane + rb[e]);
+          nc[e] = ld2(cur + (px + plane + rb[e]) + lo);
         }
       }
     }
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_leapfrog2_rq(const Lf2Params p)
       a[e].x = keep && in0 ? leapfrog(c[e].x, o[e].x, l0, tau2) : 0.0;
       a[e].y = keep && in1 ? leapfrog(c[e].y, o[e].y, l1, tau2) : 0.0;
       if (e >= 2 && e <= E - 3 && xout && ro[e - 2]) {
-        double* dst = p.out1 + px + rb[e];
+        double* dst = p.out1 + (px + rb[e]) + lo;
         if (ok0 && ok1)
           st2<NT>(dst, a[e]);
         else if (ok0)
@@ -209,7 +211,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_leapfrog2_rq(const Lf2Params p)
         v.x = leapfrog(ctr.x, m[e].x, l0, tau2);
         v.y = leapfrog(ctr.y, m[e].y, l1, tau2);
         if (ro[r]) {
-          double* dst = p.out2 + px - plane + rb[e];
+          double* dst = p.out2 + (px - plane + rb[e]) + lo;
           if (ok0 && ok1)
             st2<NT>(dst, v);
           else if (ok0)

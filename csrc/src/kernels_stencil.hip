@@ -301,7 +301,7 @@ template <int R, bool CHECK, bool NT>
 __global__ __launch_bounds__(64 * kWavesRq) __attribute__((amdgpu_waves_per_eu(R <= 2 ? 4 : 2))) void k_leapfrog_rq(
     const LfParams p) {
   const int lane = static_cast<int>(threadIdx.x) & 63;
-  const int wv = static_cast<int>(threadIdx.x) >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);  // wave-uniform: tile math stays scalar
   int blk = static_cast<int>(blockIdx.x);
   if (p.xcd_remap) {
     const int per = p.nblocks >> 3;

@@ -54,6 +54,17 @@ double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Upper bound for one blocking wait on the GPU (env W3D_TIMEOUT_S, default 300 s): a lost peer or a stuck halo
+// exchange turns into an error instead of a hang.
+double gpu_timeout_s() {
+  static const double t = [] {
+    const char* v = std::getenv("W3D_TIMEOUT_S");
+    const double x = v ? std::atof(v) : 0.0;
+    return x > 0.0 ? x : 300.0;
+  }();
+  return t;
+}
+
 // Wait for a stream while polling RCCL for asynchronous failures (a dead peer must not hang the job forever).
 void wait_stream(hipStream_t s, const Comm* comm, double timeout_s) {
   const double t0 = now_s();
@@ -375,7 +386,7 @@ void GpuSolver::gather_errors(RunResult& r) {
     host.resize(per);
     W3D_HIP(hipMemcpyAsync(host.data(), errlog_, per * sizeof(Partial), hipMemcpyDeviceToHost, s0_));
   }
-  wait_stream(s0_, comm_.get(), 600.0);
+  wait_stream(s0_, comm_.get(), gpu_timeout_s());
   const int nsrc = static_cast<int>(host.size() / per);
   const double n_int = static_cast<double>(prob_.N - 1);
   const double denom = n_int * n_int * n_int;
@@ -460,7 +471,7 @@ double comm_allreduce(const Comm& c, double v, bool max_op) {
   W3D_NCCL(ncclAllReduce(buf, buf, 1, ncclFloat64, max_op ? ncclMax : ncclSum, static_cast<ncclComm_t>(c.raw()), st));
   double out = 0.0;
   W3D_HIP(hipMemcpyAsync(&out, buf, sizeof(double), hipMemcpyDeviceToHost, st));
-  wait_stream(st, &c, 600.0);
+  wait_stream(st, &c, gpu_timeout_s());
   return out;
 }
 
@@ -497,7 +508,7 @@ RunResult GpuGroup::run() {
     W3D_HIP(hipMemcpyAsync(all.data() + q * per, rs[q]->errlog_, per * sizeof(Partial), hipMemcpyDeviceToHost,
                            rs[q]->s0_));
   }
-  for (auto* s : rs) wait_stream(s->s0_, nullptr, 600.0);
+  for (auto* s : rs) wait_stream(s->s0_, nullptr, gpu_timeout_s());
   RunResult r;
   const double n_int = static_cast<double>(rs[0]->prob_.N - 1);
   for (int n : rs[0]->check_steps()) {

@@ -40,6 +40,10 @@ struct Args {
   bool overlap = true;
   bool graph = true;
   bool timers = false;
+  bool debug_sync = false;
+  bool poison = false;
+  int temporal = 2;
+  bool init2 = true;
   bool force = false;
   int repeat = 1;
   int warmup = 0;
@@ -65,7 +69,11 @@ struct Args {
                "  --cpu [--threads T] sequential/OpenMP CPU path\n"
                "  --no-overlap       halo exchange on the compute stream (A/B switch)\n"
                "  --no-graph         eager launches instead of one captured hipGraph\n"
-               "  --timers           per-phase GPU timers\n"
+               "  --timers           per-phase GPU timers (init / compute / exchange / check)\n"
+               "  --no-temporal      one leapfrog step per HBM pass (disable temporal blocking)\n"
+               "  --no-init2         start from u0,u1 + a first step instead of analytic u1,u2\n"
+               "  --debug-sync       synchronize after every step (race triage)\n"
+               "  --poison-ghosts    NaN-fill ghost layers before every exchange (missed-halo detector)\n"
                "  --repeat R / --warmup W   timed / untimed solves (report min and mean)\n"
                "  --variant V        leapfrog kernel: 1 = register-queue waves (default), 0 = LDS-staged tile\n"
                "  --tile-rows T      rows per wave (v1: 1,2,4,8) or per workgroup (v0: 4,8,16)\n"
@@ -95,6 +103,10 @@ Args parse(int argc, char** argv) {
     else if (s == "--no-overlap") a.overlap = false;
     else if (s == "--no-graph") a.graph = false;
     else if (s == "--timers") a.timers = true;
+    else if (s == "--debug-sync") a.debug_sync = true;
+    else if (s == "--poison-ghosts") a.poison = true;
+    else if (s == "--no-temporal") a.temporal = 1;
+    else if (s == "--no-init2") a.init2 = false;
     else if (s == "--repeat") a.repeat = std::stoi(next());
     else if (s == "--warmup") a.warmup = std::stoi(next());
     else if (s == "--tile-rows") a.tile_rows = std::stoi(next());
@@ -282,6 +294,10 @@ int run_gpu(const Args& a) {
   o.overlap = a.overlap;
   o.graph = a.graph;
   o.timers = a.timers;
+  o.debug_sync = a.debug_sync;
+  o.poison_ghosts = a.poison;
+  o.temporal = a.temporal;
+  o.init2 = a.init2;
   if (a.variant >= 0) o.tiling.variant = a.variant;
   if (a.tile_rows > 0) (o.tiling.variant == 1 ? o.tiling.rows : o.tiling.ty) = a.tile_rows;
   o.tiling.target_blocks = a.target_blocks;
@@ -319,8 +335,11 @@ int run_gpu(const Args& a) {
     std::printf("Throughput: %.2f GCell/s; process wall-clock %.3f s (RCCL init %.3f s); graph %s, overlap %s\n",
                 gcell, t_proc, t_comm, s.options().graph ? "on" : "off", a.overlap ? "on" : "off");
     if (a.timers)
-      std::printf("Phases (rank 0, last run): init+first step %.3f ms, steps %.3f ms\n", r.phases.init_ms,
-                  r.phases.interior_ms);
+      std::printf(
+          "Phases (rank 0, last run, device ms): init %.3f | compute %.3f (shell %.3f) | exchange %.3f | check %.3f"
+          " | gather+sync (host) %.3f\n",
+          r.phases.init_ms, r.phases.interior_ms + r.phases.shell_ms, r.phases.shell_ms, r.phases.comm_ms,
+          r.phases.check_ms, r.phases.gather_ms);
     if (!a.json.empty()) {
       std::ofstream j(a.json);
       j.precision(10);

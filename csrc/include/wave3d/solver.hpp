@@ -34,6 +34,8 @@ struct SolverOptions {
   bool overlap = true;          // shell/interior split with the halo exchange on a side stream
   bool graph = true;            // capture the whole solve into a hipGraph, replay it on every run()
   bool timers = false;          // per-phase hipEvent timers (adds events to the stream; disables the graph)
+  bool debug_sync = false;      // hipDeviceSynchronize after every step (race triage; disables the graph)
+  bool poison_ghosts = false;   // NaN-fill ghost layers before each exchange (a missed halo poisons the errors)
   LeapfrogTiling tiling;
   // Temporal blocking: 2 = fuse pairs of steps into one HBM pass (k_leapfrog2) wherever no halo exchange and no
   // intermediate error check intervene (single rank); 1 = one step per pass everywhere.
@@ -43,6 +45,8 @@ struct SolverOptions {
   bool init2 = true;
 };
 
+// Summed device time per phase of the last run() (SolverOptions::timers). compute = interior / whole-box / fused
+// passes; comm overlaps compute when the exchange runs on the side stream; gather is host wall time.
 struct PhaseTimes {
   double init_ms = 0, shell_ms = 0, interior_ms = 0, comm_ms = 0, check_ms = 0, gather_ms = 0;
 };
@@ -155,7 +159,19 @@ class GpuSolver {
   std::vector<char> is_check_;
   hipGraphExec_t graph_exec_ = nullptr;
   int final_buf_ = 0;            // buffer index holding u^K after a solve
-  std::vector<hipEvent_t> tev_;  // timer events
+  // per-phase timers
+  enum { kPhaseInit = 0, kPhaseShell, kPhaseCompute, kPhaseComm, kPhaseCheck, kNumPhases };
+  struct Mark {
+    int phase;
+    hipEvent_t b, e;
+  };
+  std::vector<hipEvent_t> ev_pool_;
+  size_t ev_next_ = 0;
+  std::vector<Mark> marks_;
+  template <class F>
+  void timed(int phase, hipStream_t st, F&& f);
+  void collect_phases(RunResult& r);
+  void poison(double* field, hipStream_t st);
 };
 
 }  // namespace wave3d

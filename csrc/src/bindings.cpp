@@ -44,7 +44,11 @@ py::dict result_dict(const RunResult& r) {
   d["finite"] = r.finite;
   py::dict ph;
   ph["init_ms"] = r.phases.init_ms;
-  ph["steps_ms"] = r.phases.interior_ms;
+  ph["shell_ms"] = r.phases.shell_ms;
+  ph["compute_ms"] = r.phases.interior_ms;
+  ph["comm_ms"] = r.phases.comm_ms;
+  ph["check_ms"] = r.phases.check_ms;
+  ph["gather_ms"] = r.phases.gather_ms;
   d["phases"] = ph;
   return d;
 }
@@ -322,6 +326,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("overlap", &SolverOptions::overlap)
       .def_readwrite("graph", &SolverOptions::graph)
       .def_readwrite("timers", &SolverOptions::timers)
+      .def_readwrite("debug_sync", &SolverOptions::debug_sync)
+      .def_readwrite("poison_ghosts", &SolverOptions::poison_ghosts)
       .def_readwrite("temporal", &SolverOptions::temporal)
       .def_readwrite("init2", &SolverOptions::init2)
       .def_readwrite("tiling2", &SolverOptions::tiling2)

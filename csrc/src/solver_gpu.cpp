@@ -127,7 +127,17 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   W3D_HIP(hipEventCreateWithFlags(&ev_shell_, hipEventDisableTiming));
   W3D_HIP(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
   W3D_HIP(hipEventCreateWithFlags(&ev_packed_, hipEventDisableTiming));
+  // memory plan: temporal blocking needs four field buffers; fall back to the two-buffer in-place scheme when four
+  // do not fit next to the other allocations (2049³ fp64 is 68.8 GB per buffer)
   nbuf_ = (opt_.temporal == 2 && !plan_.any() && world_ == 1) ? 4 : 2;
+  {
+    size_t free_b = 0, total_b = 0;
+    W3D_HIP(hipMemGetInfo(&free_b, &total_b));
+    const double need2 = 2.0 * static_cast<double>(lay_.bytes()), headroom = 2.0e9;
+    W3D_REQUIRE(need2 + 1.0e8 < static_cast<double>(free_b),
+                "not enough device memory for two field buffers of " + std::to_string(lay_.bytes()) + " bytes");
+    if (nbuf_ == 4 && 2.0 * need2 + headroom > static_cast<double>(free_b)) nbuf_ = 2;
+  }
   for (int b = 0; b < nbuf_; ++b) {
     W3D_HIP(hipMalloc(&u_[b], static_cast<size_t>(lay_.bytes())));
     W3D_HIP(hipMemset(u_[b], 0, static_cast<size_t>(lay_.bytes())));
@@ -150,7 +160,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   W3D_HIP(hipMalloc(&errall_, static_cast<size_t>(world_) * (prob_.K + 1) * sizeof(Partial)));
   ct_.resize(static_cast<size_t>(prob_.K + 1));
   for (int n = 0; n <= prob_.K; ++n) ct_[static_cast<size_t>(n)] = time_factor(prob_, n);
-  if (opt_.timers || loopback_) opt_.graph = false;
+  if (opt_.timers || opt_.debug_sync || loopback_) opt_.graph = false;
 }
 
 GpuSolver::~GpuSolver() {
@@ -160,7 +170,7 @@ GpuSolver::~GpuSolver() {
   if (partials_) hipFree(partials_);
   if (errlog_) hipFree(errlog_);
   if (errall_) hipFree(errall_);
-  for (hipEvent_t e : tev_) hipEventDestroy(e);
+  for (hipEvent_t e : ev_pool_) hipEventDestroy(e);
   if (ev_shell_) hipEventDestroy(ev_shell_);
   if (ev_halo_) hipEventDestroy(ev_halo_);
   if (ev_packed_) hipEventDestroy(ev_packed_);
@@ -211,31 +221,62 @@ bool GpuSolver::needs_exchange(int n) const {
 double* GpuSolver::xfield() const { return split() ? u_[old_] : u_[cur_]; }
 hipStream_t GpuSolver::xstream() const { return split() ? s1_ : s0_; }
 
+// Per-phase device timers (SolverOptions::timers, eager launches only): every timed launch group is bracketed by two
+// events on its stream; after the solve the intervals are summed per phase. The reference reports its GPU time as
+// compute / H2D-D2H copies / MPI exchange (report.pdf p.16 §4.4); here: init, compute (shell + interior / fused),
+// exchange (pack + RCCL + unpack, overlapped with compute on the side stream) and error check (reductions).
+template <class F>
+void GpuSolver::timed(int phase, hipStream_t st, F&& f) {
+  if (!opt_.timers) {
+    f();
+    return;
+  }
+  auto take = [&]() {
+    if (ev_next_ == ev_pool_.size()) {
+      hipEvent_t e;
+      W3D_HIP(hipEventCreate(&e));
+      ev_pool_.push_back(e);
+    }
+    return ev_pool_[ev_next_++];
+  };
+  hipEvent_t a = take(), b = take();
+  W3D_HIP(hipEventRecord(a, st));
+  f();
+  W3D_HIP(hipEventRecord(b, st));
+  marks_.push_back({phase, a, b});
+}
+
 void GpuSolver::phase_init() {
   const int K = prob_.K;
   const double* s = d_s_ + 1;
   is_check_.assign(static_cast<size_t>(K + 1), 0);
   for (int n : check_steps()) is_check_[static_cast<size_t>(n)] = 1;
-  if (opt_.timers) W3D_HIP(hipEventRecord(tev_[0], s0_));
+  ev_next_ = 0;
+  marks_.clear();
   W3D_HIP(hipMemsetAsync(errlog_, 0, static_cast<size_t>(K + 1) * sizeof(Partial), s0_));
   if (opt_.init2 && K >= 2) {
     // u¹ -> buf 0, u² -> buf 1 analytically (no read pass); the first leapfrog step is n = 2
-    launch_init_two(lay_, coef_, s, u_[0], u_[1], ct_[2], is_check_[2] ? partials_ : nullptr, s0_);
-    if (is_check_[2]) launch_reduce(partials_, init_two_partials(lay_), errlog_ + 2, s0_);
-    if (is_check_[1]) {
-      launch_error(lay_, u_[0], full_, s, ct_[1], partials_, s0_);
-      launch_reduce(partials_, error_blocks(lay_, full_), errlog_ + 1, s0_);
-    }
+    timed(kPhaseInit, s0_, [&] {
+      launch_init_two(lay_, coef_, s, u_[0], u_[1], ct_[2], is_check_[2] ? partials_ : nullptr, s0_);
+    });
+    timed(kPhaseCheck, s0_, [&] {
+      if (is_check_[2]) launch_reduce(partials_, init_two_partials(lay_), errlog_ + 2, s0_);
+      if (is_check_[1]) {
+        launch_error(lay_, u_[0], full_, s, ct_[1], partials_, s0_);
+        launch_reduce(partials_, error_blocks(lay_, full_), errlog_ + 1, s0_);
+      }
+    });
     start_n_ = 2;
   } else {
-    launch_init_first(lay_, coef_, s, u_[0], u_[1], s0_);
-    if (is_check_[1]) {
-      launch_error(lay_, u_[1], full_, s, ct_[1], partials_, s0_);
-      launch_reduce(partials_, error_blocks(lay_, full_), errlog_ + 1, s0_);
-    }
+    timed(kPhaseInit, s0_, [&] { launch_init_first(lay_, coef_, s, u_[0], u_[1], s0_); });
+    timed(kPhaseCheck, s0_, [&] {
+      if (is_check_[1]) {
+        launch_error(lay_, u_[1], full_, s, ct_[1], partials_, s0_);
+        launch_reduce(partials_, error_blocks(lay_, full_), errlog_ + 1, s0_);
+      }
+    });
     start_n_ = 1;
   }
-  if (opt_.timers) W3D_HIP(hipEventRecord(tev_[1], s0_));
   cur_ = 1;
   old_ = 0;
 }
@@ -243,8 +284,10 @@ void GpuSolver::phase_init() {
 void GpuSolver::phase_shell(int n) {
   const bool chk = is_check_[static_cast<size_t>(n + 1)] != 0;
   if (split()) {
-    launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], shell_.data(), static_cast<int>(shell_.size()), d_s_ + 1,
-                    ct_[static_cast<size_t>(n + 1)], chk ? partials_ : nullptr, opt_.tiling, s0_);
+    timed(kPhaseShell, s0_, [&] {
+      launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], shell_.data(), static_cast<int>(shell_.size()), d_s_ + 1,
+                      ct_[static_cast<size_t>(n + 1)], chk ? partials_ : nullptr, opt_.tiling, s0_);
+    });
   }
   if (needs_exchange(n)) W3D_HIP(hipEventRecord(ev_shell_, s0_));
 }
@@ -253,7 +296,8 @@ void GpuSolver::phase_exchange_rccl(int n) {
   if (!needs_exchange(n)) return;
   hipStream_t xs = xstream();
   if (xs != s0_) W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
-  exchange(xfield(), xs);
+  if (opt_.poison_ghosts) poison(xfield(), xs);
+  timed(kPhaseComm, xs, [&] { exchange(xfield(), xs); });
   if (split()) W3D_HIP(hipEventRecord(ev_halo_, xs));
 }
 
@@ -261,20 +305,22 @@ void GpuSolver::phase_interior(int n) {
   const bool chk = is_check_[static_cast<size_t>(n + 1)] != 0;
   const double ct = ct_[static_cast<size_t>(n + 1)];
   if (split()) {
-    launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &interior_, 1, d_s_ + 1, ct,
-                    chk ? partials_ + n_shell_ : nullptr, opt_.tiling, s0_);
+    timed(kPhaseCompute, s0_, [&] {
+      launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &interior_, 1, d_s_ + 1, ct,
+                      chk ? partials_ + n_shell_ : nullptr, opt_.tiling, s0_);
+    });
     if (needs_exchange(n)) W3D_HIP(hipStreamWaitEvent(s0_, ev_halo_, 0));
-    if (chk) launch_reduce(partials_, n_shell_ + n_int_, errlog_ + n + 1, s0_);
+    if (chk) timed(kPhaseCheck, s0_, [&] { launch_reduce(partials_, n_shell_ + n_int_, errlog_ + n + 1, s0_); });
   } else {
-    launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &full_, 1, d_s_ + 1, ct, chk ? partials_ : nullptr,
-                    opt_.tiling, s0_);
-    if (chk) launch_reduce(partials_, n_full_, errlog_ + n + 1, s0_);
+    timed(kPhaseCompute, s0_, [&] {
+      launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &full_, 1, d_s_ + 1, ct, chk ? partials_ : nullptr,
+                      opt_.tiling, s0_);
+    });
+    if (chk) timed(kPhaseCheck, s0_, [&] { launch_reduce(partials_, n_full_, errlog_ + n + 1, s0_); });
   }
+  if (opt_.debug_sync) W3D_HIP(hipDeviceSynchronize());
   std::swap(cur_, old_);
-  if (n == prob_.K - 1) {
-    final_buf_ = cur_;
-    if (opt_.timers) W3D_HIP(hipEventRecord(tev_[2], s0_));
-  }
+  if (n == prob_.K - 1) final_buf_ = cur_;
 }
 
 void GpuSolver::enqueue_solve() {
@@ -307,24 +353,55 @@ void GpuSolver::enqueue_solve_fused() {
       for (int b = 0; b < 4; ++b)
         if (b != cur_ && b != old_) f[k++] = b;
       const bool chk = is_check_[static_cast<size_t>(n + 2)] != 0;
-      launch_leapfrog2(lay_, coef_, u_[old_], u_[cur_], u_[f[0]], u_[f[1]], full_, s,
-                       ct_[static_cast<size_t>(n + 2)], chk ? partials_ : nullptr, opt_.tiling2, s0_);
-      if (chk) launch_reduce(partials_, n_fused_, errlog_ + n + 2, s0_);
+      timed(kPhaseCompute, s0_, [&] {
+        launch_leapfrog2(lay_, coef_, u_[old_], u_[cur_], u_[f[0]], u_[f[1]], full_, s,
+                         ct_[static_cast<size_t>(n + 2)], chk ? partials_ : nullptr, opt_.tiling2, s0_);
+      });
+      if (chk) timed(kPhaseCheck, s0_, [&] { launch_reduce(partials_, n_fused_, errlog_ + n + 2, s0_); });
       old_ = f[0];
       cur_ = f[1];
       n += 2;
     } else {
       const bool chk = is_check_[static_cast<size_t>(n + 1)] != 0;
-      launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &full_, 1, s, ct_[static_cast<size_t>(n + 1)],
-                      chk ? partials_ : nullptr, opt_.tiling, s0_);
-      if (chk) launch_reduce(partials_, n_full_, errlog_ + n + 1, s0_);
+      timed(kPhaseCompute, s0_, [&] {
+        launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &full_, 1, s, ct_[static_cast<size_t>(n + 1)],
+                        chk ? partials_ : nullptr, opt_.tiling, s0_);
+      });
+      if (chk) timed(kPhaseCheck, s0_, [&] { launch_reduce(partials_, n_full_, errlog_ + n + 1, s0_); });
       std::swap(cur_, old_);
       n += 1;
     }
+    if (opt_.debug_sync) W3D_HIP(hipDeviceSynchronize());
   }
   final_buf_ = cur_;
   prev_buf_ = old_;
-  if (opt_.timers) W3D_HIP(hipEventRecord(tev_[2], s0_));
+}
+
+// Debug aid: fill the ghost layers that the next exchange must overwrite with NaN, so a halo that
+// is not delivered shows up in the error norms at once instead of silently reusing stale values.
+void GpuSolver::poison(double* field, hipStream_t st) {
+  for (const Face& f : plan_.faces) {
+    if (f.contiguous) {
+      W3D_HIP(hipMemsetAsync(field + f.recv_off, 0xFF, static_cast<size_t>(f.count) * sizeof(double), st));
+    }
+  }
+  if (plan_.packed_doubles > 0)
+    W3D_HIP(hipMemsetAsync(recv_buf_, 0xFF, static_cast<size_t>(plan_.packed_doubles) * sizeof(double), st));
+}
+
+void GpuSolver::collect_phases(RunResult& r) {
+  if (!opt_.timers) return;
+  double acc[kNumPhases] = {0, 0, 0, 0, 0};
+  for (const auto& m : marks_) {
+    float ms = 0.0f;
+    W3D_HIP(hipEventElapsedTime(&ms, m.b, m.e));
+    acc[m.phase] += ms;
+  }
+  r.phases.init_ms = acc[kPhaseInit];
+  r.phases.shell_ms = acc[kPhaseShell];
+  r.phases.interior_ms = acc[kPhaseCompute];
+  r.phases.comm_ms = acc[kPhaseComm];
+  r.phases.check_ms = acc[kPhaseCheck];
 }
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -344,6 +421,7 @@ void GpuSolver::lb_pull(int n, const std::vector<GpuSolver*>& ranks) {
   if (!needs_exchange(n)) return;
   hipStream_t xs = xstream();
   const int b = split() ? old_ : cur_;
+  if (opt_.poison_ghosts) poison(u_[b], xs);
   for (const Face& f : plan_.faces) {
     const GpuSolver* q = ranks[static_cast<size_t>(f.peer)];
     const Face* g = nullptr;
@@ -406,10 +484,6 @@ void GpuSolver::gather_errors(RunResult& r) {
 
 RunResult GpuSolver::run() {
   RunResult r;
-  if (opt_.timers && tev_.empty()) {
-    tev_.resize(3);
-    for (auto& e : tev_) W3D_HIP(hipEventCreate(&e));
-  }
   if (opt_.graph && !graph_exec_) {
     // capture once (outside the timed region of later runs); fall back to eager launches if capture is refused
     hipGraph_t g = nullptr;
@@ -436,15 +510,11 @@ RunResult GpuSolver::run() {
     W3D_HIP(hipGraphLaunch(graph_exec_, s0_));
   else
     enqueue_solve();
+  const double tg = now_s();
   gather_errors(r);
   r.solve_s = now_s() - t0;
-  if (opt_.timers) {
-    float a = 0, b = 0;
-    W3D_HIP(hipEventElapsedTime(&a, tev_[0], tev_[1]));
-    W3D_HIP(hipEventElapsedTime(&b, tev_[1], tev_[2]));
-    r.phases.init_ms = a;
-    r.phases.interior_ms = b;
-  }
+  collect_phases(r);
+  r.phases.gather_ms = (now_s() - tg) * 1e3;  // host: waits for the device, then all-gathers the error log
   return r;
 }
 

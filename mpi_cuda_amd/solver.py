@@ -73,7 +73,8 @@ class Solver:
                  rank: int | None = None, world: int | None = None, device: int | None = None,
                  overlap: bool = True, graph: bool = True, threads: int = 0, tiling: dict | None = None,
                  comm=None, group=None, stage_via_host: bool = False, force: bool = False, temporal: int = 2,
-                 tiling2: dict | None = None, init2: bool = True):
+                 tiling2: dict | None = None, init2: bool = True, timers: bool = False,
+                 debug_sync: bool = False, poison_ghosts: bool = False):
         import torch.distributed as dist
 
         if not spec.cfl_ok and not force:
@@ -100,12 +101,14 @@ class Solver:
             self.device = torch.device("cpu")
         if self.backend == "hip" and self.transport == "loopback":
             opts = self._options(C, decomp, spec, overlap, False, tiling, temporal, tiling2, init2)
+            opts.timers, opts.debug_sync, opts.poison_ghosts = timers, debug_sync, poison_ghosts
             self._impl = C.GpuGroup(spec.native(), opts, world)
             self.dims = self._impl.dims().as_tuple()
         elif self.backend == "hip" and self.transport == "rccl":
             from .parallel.rccl import make_comm
 
             opts = self._options(C, decomp, spec, overlap, graph, tiling, temporal, tiling2, init2)
+            opts.timers, opts.debug_sync, opts.poison_ghosts = timers, debug_sync, poison_ghosts
             if comm is None and world > 1:
                 comm = make_comm(rank, world, group)
             self.comm = comm

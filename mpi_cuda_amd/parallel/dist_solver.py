@@ -45,17 +45,47 @@ class TorchDistSolver:
     def _ct(self, n: int) -> float:
         return math.cos(self.spec.a_t * (n * self.spec.tau))
 
+    def set_state(self, prev: torch.Tensor, cur: torch.Tensor, step: int) -> None:
+        """Resume from global (N+1)³ fields u^{step-1}, u^{step} (a checkpoint, utils/dump.py): the next run() continues
+        from `step` to spec.K instead of starting from the initial condition."""
+        if not 1 <= step < self.spec.K:
+            raise ValueError(f"resume step {step} must be in [1, K={self.spec.K})")
+        self._state = (prev, cur, int(step))
+
+    def _load_state(self) -> int:
+        prev, cur, step = self._state
+        lay = self.layout
+        n = self.spec.N + 1
+        for src, dst in ((prev, self.u[0]), (cur, self.u[1])):
+            g = ops.grid_view(lay, dst)
+            g.zero_()
+            # local grid index i <-> global node g0 - 1 + i (ghosts included), clipped to the domain
+            sl = []
+            gl = []
+            for g0, nn in ((int(lay.gx0), int(lay.nx)), (int(lay.gy0), int(lay.ny)), (int(lay.gz0), int(lay.nz))):
+                lo = max(0, 1 - g0)
+                hi = min(nn + 2, n + 1 - g0)
+                sl.append(slice(lo, hi))
+                gl.append(slice(g0 - 1 + lo, g0 - 1 + hi))
+            g[sl[0], sl[1], sl[2]] = src[gl[0], gl[1], gl[2]].to(dst.device, torch.float64)
+        return step
+
     def run(self) -> dict:
         spec = self.spec
         checks = spec.check_steps()
         local = {}
         t0 = time.perf_counter()
-        ops.init_first(self.layout, self.coeffs, self.s, self.u[0], self.u[1])
-        if 1 in checks:
-            local[1] = ops.error(self.layout, self.u[1], self.full, self.s, self._ct(1))
+        n0 = 1
+        if getattr(self, "_state", None) is not None:
+            n0 = self._load_state()
+            checks = [n for n in checks if n > n0]
+        else:
+            ops.init_first(self.layout, self.coeffs, self.s, self.u[0], self.u[1])
+            if 1 in checks:
+                local[1] = ops.error(self.layout, self.u[1], self.full, self.s, self._ct(1))
         cur, old = 1, 0
-        for n in range(1, spec.K):
-            if n >= 2:
+        for n in range(n0, spec.K):
+            if n > n0:
                 self.halo.exchange(self.u[cur])
             chk = (n + 1) in checks
             r = ops.leapfrog(self.layout, self.coeffs, self.u[cur], self.u[old], [self.full], self.s,

@@ -44,6 +44,8 @@ struct Args {
   bool poison = false;
   int temporal = 2;
   bool init2 = true;
+  int fake_rank = -1, fake_world = 0;
+  int t2_rows = 0, t2_target = -1, deep_min = -1;
   bool force = false;
   int repeat = 1;
   int warmup = 0;
@@ -74,6 +76,8 @@ struct Args {
                "  --no-init2         start from u0,u1 + a first step instead of analytic u1,u2\n"
                "  --debug-sync       synchronize after every step (race triage)\n"
                "  --poison-ghosts    NaN-fill ghost layers before every exchange (missed-halo detector)\n"
+               "  --fake-rank R/P    perf study: time rank R of a P-rank decomposition alone on one GPU, no transport\n"
+               "  --t2-rows R / --t2-target W   fused two-step kernel: rows per wave, x-chunking target (waves)\n"
                "  --repeat R / --warmup W   timed / untimed solves (report min and mean)\n"
                "  --variant V        leapfrog kernel: 1 = register-queue waves (default), 0 = LDS-staged tile\n"
                "  --tile-rows T      rows per wave (v1: 1,2,4,8) or per workgroup (v0: 4,8,16)\n"
@@ -107,6 +111,14 @@ Args parse(int argc, char** argv) {
     else if (s == "--poison-ghosts") a.poison = true;
     else if (s == "--no-temporal") a.temporal = 1;
     else if (s == "--no-init2") a.init2 = false;
+    else if (s == "--t2-rows") a.t2_rows = std::stoi(next());
+    else if (s == "--deep-min-planes") a.deep_min = std::stoi(next());
+    else if (s == "--t2-target") a.t2_target = std::stoi(next());
+    else if (s == "--fake-rank") {
+      const std::string v = next();  // R/P: time rank R of a P-rank decomposition alone, no transport
+      a.fake_rank = std::stoi(v.substr(0, v.find('/')));
+      a.fake_world = std::stoi(v.substr(v.find('/') + 1));
+    }
     else if (s == "--repeat") a.repeat = std::stoi(next());
     else if (s == "--warmup") a.warmup = std::stoi(next());
     else if (s == "--tile-rows") a.tile_rows = std::stoi(next());
@@ -268,7 +280,12 @@ int run_gpu(const Args& a) {
   static const char* const kRank[] = {"RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID", nullptr};
   static const char* const kSize[] = {"WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "SLURM_NTASKS", nullptr};
   static const char* const kLocal[] = {"LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", nullptr};
-  const int rank = env_int(kRank, 0), world = env_int(kSize, 1);
+  int rank = env_int(kRank, 0), world = env_int(kSize, 1);
+  const bool fake = a.fake_rank >= 0;
+  if (fake) {
+    rank = a.fake_rank;
+    world = a.fake_world;
+  }
   const double t_proc0 = now_s();
   int ndev = 0;
   W3D_HIP(hipGetDeviceCount(&ndev));
@@ -281,7 +298,7 @@ int run_gpu(const Args& a) {
 
   std::shared_ptr<Comm> comm;
   const double t_comm0 = now_s();
-  if (world > 1) {
+  if (world > 1 && !fake) {
     const std::string id = exchange_unique_id(rank);
     comm = std::make_shared<Comm>(rank, world, id);
     if (rank == 0) std::remove(rdzv_path().c_str());
@@ -298,6 +315,10 @@ int run_gpu(const Args& a) {
   o.poison_ghosts = a.poison;
   o.temporal = a.temporal;
   o.init2 = a.init2;
+  o.fake_comm = fake;
+  if (a.t2_rows > 0) o.tiling2.rows = a.t2_rows;
+  if (a.deep_min >= 0) o.deep_min_planes = a.deep_min;
+  if (a.t2_target >= 0) o.tiling2.target_waves = a.t2_target;
   if (a.variant >= 0) o.tiling.variant = a.variant;
   if (a.tile_rows > 0) (o.tiling.variant == 1 ? o.tiling.rows : o.tiling.ty) = a.tile_rows;
   o.tiling.target_blocks = a.target_blocks;
@@ -322,7 +343,7 @@ int run_gpu(const Args& a) {
   const double mean = sum / a.repeat;
   const double t_proc = now_s() - t_proc0;
   const Dims d = s.dims();
-  if (rank == 0) {
+  if (rank == 0 || fake) {
     if (!a.quiet) {
       std::printf("wave3d: N=%lld tau=%g K=%d L=%g ranks=%d decomp=%dx%dx%d device=%s courant=%.3f\n",
                   static_cast<long long>(a.prob.N), a.prob.tau, a.prob.K, a.prob.L, world, d.px, d.py, d.pz,
@@ -332,8 +353,9 @@ int run_gpu(const Args& a) {
     const double gcell = a.prob.cell_updates() / best / 1e9;
     std::printf("Total time: %.6f s (solve region, max over %d rank%s; best of %d, mean %.6f s, first %.6f s)\n", best,
                 world, world > 1 ? "s" : "", a.repeat, mean, first);
-    std::printf("Throughput: %.2f GCell/s; process wall-clock %.3f s (RCCL init %.3f s); graph %s, overlap %s\n",
-                gcell, t_proc, t_comm, s.options().graph ? "on" : "off", a.overlap ? "on" : "off");
+    std::printf(
+        "Throughput: %.2f GCell/s; process wall-clock %.3f s (RCCL init %.3f s); schedule %s, graph %s, overlap %s\n",
+        gcell, t_proc, t_comm, s.mode().c_str(), s.options().graph ? "on" : "off", a.overlap ? "on" : "off");
     if (a.timers)
       std::printf(
           "Phases (rank 0, last run, device ms): init %.3f | compute %.3f (shell %.3f) | exchange %.3f | check %.3f"
@@ -348,7 +370,8 @@ int run_gpu(const Args& a) {
         << d.pz << "], \"solve_s\": " << best << ", \"mean_s\": " << mean << ", \"first_s\": " << first
         << ", \"process_s\": " << t_proc << ", \"rccl_init_s\": " << t_comm << ", \"gcell_per_s\": " << gcell
         << ", \"graph\": " << (s.options().graph ? "true" : "false") << ", \"overlap\": "
-        << (a.overlap ? "true" : "false") << ", \"device\": \"" << prop.gcnArchName << "\", \"steps\": [";
+        << (a.overlap ? "true" : "false") << ", \"schedule\": \"" << s.mode() << "\", \"device\": \""
+        << prop.gcnArchName << "\", \"steps\": [";
       for (size_t i = 0; i < r.steps.size(); ++i)
         j << (i ? ", " : "") << "[" << r.steps[i] << ", " << r.max_err[i] << ", " << r.rms_err[i] << "]";
       j << "]}\n";

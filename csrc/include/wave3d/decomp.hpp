@@ -117,20 +117,26 @@ inline int neighbor_rank(const Dims& d, int rank, int axis, int side) {
 // holding a row's right neighbour never straddles into the next row.
 struct Layout {
   i64 N = 0;
+  i64 xg = 1;                     // ghost planes on each x side (2 for the deep-halo temporally blocked slab path)
   i64 nx = 0, ny = 0, nz = 0;     // owned nodes
   i64 gx0 = 0, gy0 = 0, gz0 = 0;  // global index of local node 0
   i64 zs = 0, pitch = 0, plane = 0, total = 0;
   // Local index range of the nodes this rank updates: owned ∩ global interior [1, N-1].
   i64 cx0 = 0, cx1 = 0, cy0 = 0, cy1 = 0, cz0 = 0, cz1 = 0;
 
-  W3D_HD i64 off(i64 ix, i64 iy, i64 iz) const { return (ix + 1) * plane + (iy + 1) * pitch + (iz + 1 + zs); }
+  W3D_HD i64 off(i64 ix, i64 iy, i64 iz) const { return (ix + xg) * plane + (iy + 1) * pitch + (iz + 1 + zs); }
+  // Kernels address plane x at (x+1)·plane from their base pointer; base = field + kbase() accounts for extra ghosts.
+  W3D_HD i64 kbase() const { return (xg - 1) * plane; }
+  // first element of plane ix (its ghost rows and row padding included)
+  W3D_HD i64 plane_off(i64 ix) const { return (ix + xg) * plane; }
   W3D_HD i64 bytes() const { return total * static_cast<i64>(sizeof(double)); }
   W3D_HD bool has_work() const { return cx1 > cx0 && cy1 > cy0 && cz1 > cz0; }
 };
 
-inline Layout make_layout(const Problem& p, const Box& b, i64 pitch_align = 16) {
+inline Layout make_layout(const Problem& p, const Box& b, i64 pitch_align = 16, i64 xg = 1) {
   Layout l;
   l.N = p.N;
+  l.xg = xg;
   l.nx = b.nx();
   l.ny = b.ny();
   l.nz = b.nz();
@@ -148,7 +154,7 @@ inline Layout make_layout(const Problem& p, const Box& b, i64 pitch_align = 16) 
   l.zs = (16 - (l.cz0 + 1) % 16) % 16;
   l.pitch = round_up(l.nz + 2 + l.zs + 2, pitch_align);
   l.plane = (l.ny + 2) * l.pitch;
-  l.total = (l.nx + 2) * l.plane;
+  l.total = (l.nx + 2 * l.xg) * l.plane;
   return l;
 }
 
@@ -188,8 +194,8 @@ inline HaloPlan make_halo_plan(const Layout& l, const Dims& d, int rank) {
       if (axis == 0) {
         f.contiguous = true;
         f.count = l.plane;
-        f.send_off = (f.send_layer + 1) * l.plane;
-        f.recv_off = (f.recv_layer + 1) * l.plane;
+        f.send_off = l.plane_off(f.send_layer);
+        f.recv_off = l.plane_off(f.recv_layer);
       } else {
         f.contiguous = false;
         f.count = axis == 1 ? l.nx * l.nz : l.nx * l.ny;

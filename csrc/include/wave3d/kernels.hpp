@@ -59,10 +59,13 @@ struct Leapfrog2Tiling {
   bool xcd_remap = true;
   bool nt_store = true;
 };
+// [sx0, sx1): local x range where stage-1 (u^{n+1}) values are real; it extends one plane beyond `box` towards a
+// neighbouring rank of a slab decomposition (those ghost planes are recomputed redundantly from 2-deep halos).
+// Default (sx0 > sx1): this rank's updated region.
 int leapfrog2_partials(const Layout& l, const LBox& box, const Leapfrog2Tiling& t);
 void launch_leapfrog2(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
                       double* out2, const LBox& box, const double* d_s, double ct2, Partial* partials,
-                      const Leapfrog2Tiling& t, hipStream_t stream);
+                      const Leapfrog2Tiling& t, hipStream_t stream, i64 sx0 = 1, i64 sx1 = 0);
 
 // Error of a stored field vs φ·ct over `box` (step 1 / standalone check). Writes leapfrog-compatible partials and
 // returns how many.

@@ -36,6 +36,7 @@ struct SolverOptions {
   bool timers = false;          // per-phase hipEvent timers (adds events to the stream; disables the graph)
   bool debug_sync = false;      // hipDeviceSynchronize after every step (race triage; disables the graph)
   bool poison_ghosts = false;   // NaN-fill ghost layers before each exchange (a missed halo poisons the errors)
+  bool fake_comm = false;       // perf study only: run rank `rank` of `world` alone, exchanges replaced by no-ops
   LeapfrogTiling tiling;
   // Temporal blocking: 2 = fuse pairs of steps into one HBM pass (k_leapfrog2) wherever no halo exchange and no
   // intermediate error check intervene (single rank); 1 = one step per pass everywhere.
@@ -43,6 +44,8 @@ struct SolverOptions {
   Leapfrog2Tiling tiling2;
   // Start from u¹, u² computed analytically in one write-only pass (k_init_two) instead of u⁰, u¹ + a first step.
   bool init2 = true;
+  // Slab ranks use the deep-halo fused schedule only from this many owned x-planes up (below, single steps are faster).
+  int deep_min_planes = 96;
 };
 
 // Summed device time per phase of the last run() (SolverOptions::timers). compute = interior / whole-box / fused
@@ -106,26 +109,42 @@ class GpuSolver {
   LBox interior_box() const { return interior_; }
   std::vector<int> check_steps() const;
   size_t device_bytes() const;
+  // "single-step" | "fused-single" (temporal blocking, one rank) | "deep-halo" (temporal blocking, slab ranks)
+  std::string mode() const;
 
  private:
   friend class GpuGroup;
   void enqueue_solve();  // all device work of one solve on s0/s1 (graph-capturable)
-  bool fused() const;    // temporal blocking active for this rank
-  void enqueue_solve_fused();
-  void exchange(double* field, hipStream_t st);
+  void exchange(hipStream_t st);
   void gather_errors(RunResult& r);
+  // Schedule: a solve is phase_init() followed by units; a unit advances one step (in place over u^{n−1}) or two
+  // (a fused pass into the two free buffers). Multi-rank units run shell -> exchange -> interior.
+  enum class Mode { kSingleStep, kFusedSingle, kDeep };
+  struct Unit {
+    int n;       // current level u^n before the unit
+    bool fused;  // two steps (u^{n+1}, u^{n+2}) in one pass
+  };
+  // one point-to-point message of an exchange: `tag` pairs it with the peer's matching message
+  struct Msg {
+    int peer, tag;
+    const double* send;
+    double* recv;
+    i64 count;
+  };
   bool split() const;
-  bool needs_exchange(int n) const;
-  double* xfield() const;
+  bool post_exchange() const;  // the unit's NEW field is exchanged after its shell (else: current field, before)
+  bool needs_exchange(int i) const;
   hipStream_t xstream() const;
+  bool pairable() const;
+  void build_units();
+  void build_msgs(int i);
   void phase_init();
-  void phase_shell(int n);
-  void phase_exchange_rccl(int n);
-  void phase_interior(int n);
-  void lb_pack(int n);
-  void lb_pull(int n, const std::vector<GpuSolver*>& ranks);
-  void lb_fence(int n, const std::vector<GpuSolver*>& ranks);
-  RunResult collect_local();
+  void unit_shell(int i);
+  void unit_exchange_rccl(int i);
+  void unit_interior(int i);
+  void lb_pack(int i);
+  void lb_pull(int i, const std::vector<GpuSolver*>& ranks);
+  void lb_fence(int i, const std::vector<GpuSolver*>& ranks);
 
   Problem prob_;
   SolverOptions opt_;
@@ -142,6 +161,15 @@ class GpuSolver {
 
   double* u_[4] = {nullptr, nullptr, nullptr, nullptr};  // [2], [3] only with temporal blocking
   int nbuf_ = 2;
+  Mode mode_ = Mode::kSingleStep;
+  std::vector<Unit> units_;
+  std::vector<Msg> msgs_;
+  int uf_[2] = {2, 3};            // output buffers of the current fused unit
+  std::vector<LBox> dshell_;      // deep mode: output x-slabs next to neighbours (shell) ...
+  LBox dint_;                     // ... and the rest (interior)
+  i64 sx0_ = 0, sx1_ = 0;         // deep mode: stage-1 x range (one ghost plane beyond each neighbour face)
+  std::vector<int> n_dshell_;     // partials per deep shell launch
+  int n_dint_ = 0;
   int prev_buf_ = 1;             // buffer index holding u^{K−1} after a solve
   double* d_s_ = nullptr;        // extended sin table (+1 applied when passed to kernels)
   double* send_buf_ = nullptr;   // packed y/z faces
@@ -171,7 +199,7 @@ class GpuSolver {
   template <class F>
   void timed(int phase, hipStream_t st, F&& f);
   void collect_phases(RunResult& r);
-  void poison(double* field, hipStream_t st);
+  void poison(hipStream_t st);
 };
 
 }  // namespace wave3d

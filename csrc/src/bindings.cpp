@@ -127,6 +127,7 @@ PYBIND11_MODULE(_C, m) {
 
   py::class_<Layout>(m, "Layout")
       .def_readonly("N", &Layout::N)
+      .def_readonly("xg", &Layout::xg)
       .def_readonly("nx", &Layout::nx)
       .def_readonly("ny", &Layout::ny)
       .def_readonly("nz", &Layout::nz)
@@ -144,7 +145,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("cz0", &Layout::cz0)
       .def_readonly("cz1", &Layout::cz1)
       .def("off", [](const Layout& l, i64 x, i64 y, i64 z) { return l.off(x, y, z); });
-  m.def("make_layout", &make_layout, py::arg("problem"), py::arg("box"), py::arg("pitch_align") = 16);
+  m.def("make_layout", &make_layout, py::arg("problem"), py::arg("box"), py::arg("pitch_align") = 16,
+        py::arg("xg") = 1);
 
   py::class_<Face>(m, "Face")
       .def_readonly("axis", &Face::axis)
@@ -299,11 +301,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("gpu_leapfrog2",
         [](const Layout& l, const Coeffs& c, std::uintptr_t prev, std::uintptr_t cur, std::uintptr_t out1,
            std::uintptr_t out2, const LBox& box, std::uintptr_t s, double ct2, std::uintptr_t partials,
-           const Leapfrog2Tiling& t, std::uintptr_t stream) {
+           const Leapfrog2Tiling& t, std::uintptr_t stream, i64 sx0, i64 sx1) {
           launch_leapfrog2(l, c, dptr<const double>(prev), dptr<const double>(cur), dptr<double>(out1),
                            dptr<double>(out2), box, dptr<const double>(s) + 1, ct2, dptr<Partial>(partials), t,
-                           sptr(stream));
-        });
+                           sptr(stream), sx0, sx1);
+        },
+        py::arg("layout"), py::arg("coeffs"), py::arg("prev"), py::arg("cur"), py::arg("out1"), py::arg("out2"),
+        py::arg("box"), py::arg("s"), py::arg("ct2"), py::arg("partials"), py::arg("tiling"), py::arg("stream"),
+        py::arg("sx0") = 1, py::arg("sx1") = 0);
   m.def("gpu_error_blocks", &error_blocks);
   m.def("gpu_error", [](const Layout& l, std::uintptr_t u, const LBox& b, std::uintptr_t s, double ct,
                         std::uintptr_t partials, std::uintptr_t stream) {
@@ -328,8 +333,10 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("timers", &SolverOptions::timers)
       .def_readwrite("debug_sync", &SolverOptions::debug_sync)
       .def_readwrite("poison_ghosts", &SolverOptions::poison_ghosts)
+      .def_readwrite("fake_comm", &SolverOptions::fake_comm)
       .def_readwrite("temporal", &SolverOptions::temporal)
       .def_readwrite("init2", &SolverOptions::init2)
+      .def_readwrite("deep_min_planes", &SolverOptions::deep_min_planes)
       .def_readwrite("tiling2", &SolverOptions::tiling2)
       .def_readwrite("tiling", &SolverOptions::tiling);
 
@@ -375,6 +382,7 @@ PYBIND11_MODULE(_C, m) {
       .def("interior_box", &GpuSolver::interior_box)
       .def("check_steps", &GpuSolver::check_steps)
       .def("device_bytes", &GpuSolver::device_bytes)
+      .def_property_readonly("mode", &GpuSolver::mode)
       .def_property_readonly("graph_enabled", [](const GpuSolver& s) { return s.options().graph; });
 
   py::class_<GpuGroup>(m, "GpuGroup")
@@ -397,5 +405,6 @@ PYBIND11_MODULE(_C, m) {
            py::arg("rank"), py::arg("which") = 0)
       .def("layout", [](GpuGroup& g, int rank) { return g.rank(rank).layout(); })
       .def("dims", [](GpuGroup& g) { return g.rank(0).dims(); })
+      .def("mode", [](GpuGroup& g) { return g.rank(0).mode(); })
       .def_property_readonly("world", &GpuGroup::world);
 }

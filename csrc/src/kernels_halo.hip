@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void k_pack(const PackParams p) {
 template <bool PACK>
 void launch(const Layout& l, const HaloPlan& plan, double* field, double* buf, hipStream_t st) {
   PackParams p{};
-  p.field = field;
+  p.field = field + l.kbase();
   p.buf = buf;
   p.plane = l.plane;
   p.pitch = l.pitch;

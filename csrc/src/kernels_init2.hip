@@ -195,13 +195,13 @@ Init2Params make_params(const Layout& l, const Coeffs& c) {
   p.gz0 = l.gz0;
   p.zs = l.zs;
   // written box: local indices in [−1, n] whose global index is interior
-  auto lo = [&](i64 g0) { return imax(-1, 1 - g0); };
-  auto hi = [&](i64 g0, i64 n) { return imin(n + 1, l.N - g0); };
-  p.x0 = lo(l.gx0);
-  p.x1 = imax(p.x0, hi(l.gx0, l.nx));
-  p.y0 = lo(l.gy0);
-  p.y1 = imax(p.y0, hi(l.gy0, l.ny));
-  const i64 z0 = lo(l.gz0), z1 = imax(z0, hi(l.gz0, l.nz));
+  auto lo = [&](i64 g0, i64 gw) { return imax(-gw, 1 - g0); };
+  auto hi = [&](i64 g0, i64 n, i64 gw) { return imin(n + gw, l.N - g0); };
+  p.x0 = lo(l.gx0, l.xg);
+  p.x1 = imax(p.x0, hi(l.gx0, l.nx, l.xg));
+  p.y0 = lo(l.gy0, 1);
+  p.y1 = imax(p.y0, hi(l.gy0, l.ny, 1));
+  const i64 z0 = lo(l.gz0, 1), z1 = imax(z0, hi(l.gz0, l.nz, 1));
   p.zo0 = z0 + 1 + l.zs;
   p.zo1 = z1 + 1 + l.zs;
   p.cx0 = l.cx0;
@@ -244,8 +244,8 @@ void launch_init_two(const Layout& l, const Coeffs& c, const double* d_s, double
                      Partial* partials, hipStream_t stream) {
   Init2Params p = make_params(l, c);
   if (p.nblocks == 0) return;
-  p.u1 = u1;
-  p.u2 = u2;
+  p.u1 = u1 + l.kbase();
+  p.u2 = u2 + l.kbase();
   p.s = d_s;
   p.partials = partials;
   p.ct2 = ct2;

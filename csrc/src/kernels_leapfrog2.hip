@@ -57,7 +57,8 @@ struct Lf2Params {
   const double* s;
   Partial* partials;
   i64 plane, pitch, ny, gx0, gy0, gz0, zs;
-  i64 x0, x1, y0, y1, zo0, zo1;  // box (local x, y; z as row offsets)
+  i64 x0, x1, y0, y1, zo0, zo1;  // output box (local x, y; z as row offsets)
+  i64 sx0, sx1;                  // x range where stage-1 values are real (beyond: Dirichlet 0)
   i64 pz0, pz_end;
   double ihx2, ihy2, ihz2, tau2, ct2;
   int ntz, nty, xchunk, ntiles, nblocks, xcd_remap;
@@ -172,7 +173,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_leapfrog2_rq(const Lf2Params p)
     const double nsx = CHECK && more ? p.s[p.gx0 + x] : 0.0;  // φ factor of plane x (stage 2 next iteration)
 
     // ---- stage 1: u^{n+1} at plane x, rows 1..E−2
-    const bool xin = x >= p.x0 && x < p.x1;
+    const bool xin = x >= p.sx0 && x < p.sx1;
     const bool xout = x >= xs && x < xe;
     v2d a[E];
 #pragma unroll
@@ -262,13 +263,20 @@ struct Plan2 {
   int npartials;
 };
 
-Plan2 make_plan2(const Layout& l, const LBox& b, const Leapfrog2Tiling& t) {
+Plan2 make_plan2(const Layout& l, const LBox& b, const Leapfrog2Tiling& t, i64 sx0, i64 sx1) {
   W3D_REQUIRE(t.rows == 1 || t.rows == 2 || t.rows == 4, "leapfrog2 rows per wave must be 1, 2 or 4");
   const LBox full = compute_box(l);
-  W3D_REQUIRE(b.x0 == full.x0 && b.x1 == full.x1 && b.y0 == full.y0 && b.y1 == full.y1 && b.z0 == full.z0 &&
-                  b.z1 == full.z1 && l.gx0 == 0 && l.gy0 == 0 && l.gz0 == 0 && l.nx == l.N + 1 &&
-                  l.ny == l.N + 1 && l.nz == l.N + 1,
-              "leapfrog2 needs the whole single-rank interior (no halo exchange inside a fused pass)");
+  // one x-slab of the whole y,z interior: a single rank, or a rank of a 1-D slab decomposition with 2-deep x halos
+  W3D_REQUIRE(b.y0 == full.y0 && b.y1 == full.y1 && b.z0 == full.z0 && b.z1 == full.z1 && l.gy0 == 0 &&
+                  l.gz0 == 0 && l.ny == l.N + 1 && l.nz == l.N + 1,
+              "leapfrog2 needs whole (y,z) planes (single rank or 1-D slab decomposition)");
+  W3D_REQUIRE(b.x0 >= full.x0 && b.x1 <= full.x1, "leapfrog2 box outside the updated region");
+  // stage 1 runs on planes x0−1 .. x1 and reads u^n on x0−2 .. x1+1; a stage-1 plane outside [sx0, sx1) is taken as 0,
+  // which is only right on the global Dirichlet boundary planes
+  const bool lo_ok = b.x0 - 1 >= sx0 || l.gx0 + b.x0 - 1 == 0;
+  const bool hi_ok = b.x1 < sx1 || l.gx0 + b.x1 == l.N;
+  W3D_REQUIRE(sx0 <= b.x0 && sx1 >= b.x1 && b.x0 - 2 >= -l.xg && b.x1 + 1 <= l.nx + l.xg - 1 && lo_ok && hi_ok,
+              "leapfrog2 stage-1 halo planes not available (needs 2 ghost planes towards neighbours)");
   Plan2 pl{};
   Lf2Params& p = pl.prm;
   p.plane = l.plane;
@@ -284,6 +292,8 @@ Plan2 make_plan2(const Layout& l, const LBox& b, const Leapfrog2Tiling& t) {
   p.y1 = b.y1;
   p.zo0 = b.z0 + 1 + l.zs;
   p.zo1 = b.z1 + 1 + l.zs;
+  p.sx0 = sx0;
+  p.sx1 = sx1;
   p.pz0 = p.zo0 / 2;
   p.pz_end = (p.zo1 + 1) / 2;
   W3D_REQUIRE(p.pz0 >= 1 && 2 * p.pz_end + 2 <= l.pitch, "row layout too tight for the leapfrog2 halo lanes");
@@ -325,21 +335,27 @@ void launch_r(const Lf2Params& p, int nblocks, bool check, bool nt, hipStream_t 
 }  // namespace
 
 int leapfrog2_partials(const Layout& l, const LBox& box, const Leapfrog2Tiling& t) {
-  return make_plan2(l, box, t).npartials;
+  return make_plan2(l, box, t, box.x0 - 1, box.x1 + 1).npartials;
 }
 
 void launch_leapfrog2(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
                       double* out2, const LBox& box, const double* d_s, double ct2, Partial* partials,
-                      const Leapfrog2Tiling& t, hipStream_t stream) {
+                      const Leapfrog2Tiling& t, hipStream_t stream, i64 sx0, i64 sx1) {
   W3D_REQUIRE(prev != out1 && prev != out2 && cur != out1 && cur != out2 && out1 != out2,
               "leapfrog2 needs four distinct buffers");
-  Plan2 pl = make_plan2(l, box, t);
+  if (sx0 > sx1) {  // default: stage 1 real exactly on the updated region of this rank
+    const LBox full = compute_box(l);
+    sx0 = full.x0;
+    sx1 = full.x1;
+  }
+  Plan2 pl = make_plan2(l, box, t, sx0, sx1);
   if (pl.nblocks == 0) return;
   Lf2Params& p = pl.prm;
-  p.prev = prev;
-  p.cur = cur;
-  p.out1 = out1;
-  p.out2 = out2;
+  const i64 kb = l.kbase();
+  p.prev = prev + kb;
+  p.cur = cur + kb;
+  p.out1 = out1 + kb;
+  p.out2 = out2 + kb;
   p.s = d_s;
   p.partials = partials;
   p.ihx2 = c.ihx2;

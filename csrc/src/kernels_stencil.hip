@@ -63,7 +63,7 @@ struct InitParams {
   double* u0;
   double* u1;
   const double* s;
-  i64 plane, N, nx, ny, nz, gx0, gy0, gz0, zs;
+  i64 plane, N, nx, ny, nz, gx0, gy0, gz0, zs, xg;
   int pairs_per_row, pairs_per_plane;
   double ihx2, ihy2, ihz2, half_tau2;
 };
@@ -71,7 +71,7 @@ struct InitParams {
 __global__ __launch_bounds__(256) void k_init_first(const InitParams p) {
   const int q = static_cast<int>(blockIdx.x) * 256 + static_cast<int>(threadIdx.x);
   if (q >= p.pairs_per_plane) return;
-  const i64 ix = static_cast<i64>(blockIdx.y) - 1;
+  const i64 ix = static_cast<i64>(blockIdx.y) - p.xg;
   const int r = q / p.pairs_per_row;
   const int c = q - r * p.pairs_per_row;
   const i64 iy = r - 1;
@@ -663,8 +663,9 @@ InitParams init_params(const Layout& l, const Coeffs& c, const double* d_s, doub
   p.gy0 = l.gy0;
   p.gz0 = l.gz0;
   p.zs = l.zs;
+  p.xg = l.xg;
   W3D_REQUIRE(l.pitch % 2 == 0 && l.plane / 2 < (1ll << 31), "plane too large for the init kernel");
-  W3D_REQUIRE(l.nx + 2 <= 65535, "too many planes for the init kernel grid");
+  W3D_REQUIRE(l.nx + 2 * l.xg <= 65535, "too many planes for the init kernel grid");
   p.pairs_per_row = static_cast<int>(l.pitch / 2);
   p.pairs_per_plane = static_cast<int>(l.plane / 2);
   p.ihx2 = c.ihx2;
@@ -678,7 +679,7 @@ InitParams init_params(const Layout& l, const Coeffs& c, const double* d_s, doub
 void launch_init_first(const Layout& l, const Coeffs& c, const double* d_s, double* u0, double* u1,
                        hipStream_t stream) {
   const InitParams p = init_params(l, c, d_s, u0, u1);
-  const dim3 grid(static_cast<unsigned>(ceil_div(p.pairs_per_plane, 256)), static_cast<unsigned>(l.nx + 2));
+  const dim3 grid(static_cast<unsigned>(ceil_div(p.pairs_per_plane, 256)), static_cast<unsigned>(l.nx + 2 * l.xg));
   hipLaunchKernelGGL(k_init_first, grid, dim3(256), 0, stream, p);
   W3D_HIP_CHECK(hipGetLastError());
 }
@@ -692,8 +693,8 @@ void launch_leapfrog(const Layout& l, const Coeffs& c, const double* cur, double
   Plan pl = make_plan(l, boxes, nbox, t);
   if (pl.nblocks == 0) return;
   LfParams& p = pl.prm;
-  p.cur = cur;
-  p.out = old_out;
+  p.cur = cur + l.kbase();
+  p.out = old_out + l.kbase();
   p.s = d_s;
   p.partials = partials;
   p.ihx2 = c.ihx2;
@@ -728,7 +729,7 @@ void launch_error(const Layout& l, const double* u, const LBox& b, const double*
                   hipStream_t stream) {
   if (b.empty()) return;
   ErrParams p;
-  p.u = u;
+  p.u = u + l.kbase();
   p.s = d_s;
   p.partials = partials;
   p.plane = l.plane;

@@ -86,12 +86,35 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
       loopback_(loopback) {
   prob_.validate();
   W3D_REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
-  W3D_REQUIRE(world == 1 || comm_ || loopback_, "world > 1 needs an RCCL communicator (or the loopback group)");
+  W3D_REQUIRE(world == 1 || comm_ || loopback_ || opt_.fake_comm,
+              "world > 1 needs an RCCL communicator (or the loopback group)");
   dims_ = parse_dims(opt_.decomp, world, prob_.N);
   const Box box = rank_box(prob_, dims_, rank);
   W3D_REQUIRE(box.nx() >= 1 && box.ny() >= 1 && box.nz() >= 1,
               "decomposition leaves a rank without nodes; use fewer ranks or a larger N");
-  lay_ = make_layout(prob_, box);
+  // schedule mode: temporal blocking on one rank, or on a 1-D slab decomposition with 2-deep x halos
+  mode_ = Mode::kSingleStep;
+  if (opt_.temporal == 2 && world == 1) mode_ = Mode::kFusedSingle;
+  // (measured with --fake-rank on 512³: the fused pass wins from ~128 local planes up, but at 64 planes the two
+  // 2-plane shell passes and the per-chunk stage-1 recompute cost more than the saved traffic)
+  if (opt_.temporal == 2 && world > 1 && dims_.py == 1 && dims_.pz == 1 && box.nx() >= opt_.deep_min_planes &&
+      box.nx() >= 3 && pairable())
+    mode_ = Mode::kDeep;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    lay_ = make_layout(prob_, box, 16, mode_ == Mode::kDeep ? 2 : 1);
+    // memory plan: temporal blocking needs four field buffers; fall back to the two-buffer in-place scheme when four
+    // do not fit next to the other allocations (2049³ fp64 is 68.8 GB per buffer)
+    size_t free_b = 0, total_b = 0;
+    W3D_HIP(hipMemGetInfo(&free_b, &total_b));
+    const double need2 = 2.0 * static_cast<double>(lay_.bytes()), headroom = 2.0e9;
+    if (mode_ != Mode::kSingleStep && 2.0 * need2 + headroom > static_cast<double>(free_b)) {
+      mode_ = Mode::kSingleStep;
+      continue;
+    }
+    W3D_REQUIRE(need2 + 1.0e8 < static_cast<double>(free_b),
+                "not enough device memory for two field buffers of " + std::to_string(lay_.bytes()) + " bytes");
+    break;
+  }
   plan_ = make_halo_plan(lay_, dims_, rank);
   full_ = compute_box(lay_);
 
@@ -121,23 +144,32 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   }
   if (interior_.x1 < interior_.x0 || interior_.y1 < interior_.y0 || interior_.z1 < interior_.z0) interior_ = LBox{};
 
+  // deep-halo slab: the 2 owned planes next to each neighbour are the shell (they are what the neighbours receive);
+  // stage-1 values are real one ghost plane beyond each neighbour face
+  if (mode_ == Mode::kDeep) {
+    i64 lo = full_.x0, hi = full_.x1;
+    if (nb[0][0]) {
+      const i64 e = imin(full_.x0 + 2, full_.x1);
+      dshell_.push_back(LBox{full_.x0, e, full_.y0, full_.y1, full_.z0, full_.z1});
+      lo = e;
+    }
+    if (nb[0][1]) {
+      const i64 b = imax(full_.x1 - 2, lo);
+      if (b < full_.x1) dshell_.push_back(LBox{b, full_.x1, full_.y0, full_.y1, full_.z0, full_.z1});
+      hi = b;
+    }
+    dint_ = hi > lo ? LBox{lo, hi, full_.y0, full_.y1, full_.z0, full_.z1} : LBox{};
+    sx0_ = full_.x0 - (nb[0][0] ? 1 : 0);
+    sx1_ = full_.x1 + (nb[0][1] ? 1 : 0);
+  }
+
   // device memory
   W3D_HIP(hipStreamCreateWithFlags(&s0_, hipStreamNonBlocking));
   W3D_HIP(hipStreamCreateWithFlags(&s1_, hipStreamNonBlocking));
   W3D_HIP(hipEventCreateWithFlags(&ev_shell_, hipEventDisableTiming));
   W3D_HIP(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
   W3D_HIP(hipEventCreateWithFlags(&ev_packed_, hipEventDisableTiming));
-  // memory plan: temporal blocking needs four field buffers; fall back to the two-buffer in-place scheme when four
-  // do not fit next to the other allocations (2049³ fp64 is 68.8 GB per buffer)
-  nbuf_ = (opt_.temporal == 2 && !plan_.any() && world_ == 1) ? 4 : 2;
-  {
-    size_t free_b = 0, total_b = 0;
-    W3D_HIP(hipMemGetInfo(&free_b, &total_b));
-    const double need2 = 2.0 * static_cast<double>(lay_.bytes()), headroom = 2.0e9;
-    W3D_REQUIRE(need2 + 1.0e8 < static_cast<double>(free_b),
-                "not enough device memory for two field buffers of " + std::to_string(lay_.bytes()) + " bytes");
-    if (nbuf_ == 4 && 2.0 * need2 + headroom > static_cast<double>(free_b)) nbuf_ = 2;
-  }
+  nbuf_ = mode_ == Mode::kSingleStep ? 2 : 4;
   for (int b = 0; b < nbuf_; ++b) {
     W3D_HIP(hipMalloc(&u_[b], static_cast<size_t>(lay_.bytes())));
     W3D_HIP(hipMemset(u_[b], 0, static_cast<size_t>(lay_.bytes())));
@@ -152,8 +184,15 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   n_full_ = leapfrog_blocks(lay_, &full_, 1, opt_.tiling);
   n_shell_ = leapfrog_blocks(lay_, shell_.data(), static_cast<int>(shell_.size()), opt_.tiling);
   n_int_ = leapfrog_blocks(lay_, &interior_, 1, opt_.tiling);
-  n_fused_ = (nbuf_ == 4 && !full_.empty()) ? leapfrog2_partials(lay_, full_, opt_.tiling2) : 0;
-  n_partials_ = std::max({n_full_, n_shell_ + n_int_, error_blocks(lay_, full_), n_fused_,
+  n_fused_ = (mode_ == Mode::kFusedSingle && !full_.empty()) ? leapfrog2_partials(lay_, full_, opt_.tiling2) : 0;
+  int n_deep = 0;
+  for (const LBox& b : dshell_) {
+    n_dshell_.push_back(leapfrog2_partials(lay_, b, opt_.tiling2));
+    n_deep += n_dshell_.back();
+  }
+  n_dint_ = dint_.empty() ? 0 : leapfrog2_partials(lay_, dint_, opt_.tiling2);
+  n_deep += n_dint_;
+  n_partials_ = std::max({n_full_, n_shell_ + n_int_, error_blocks(lay_, full_), n_fused_, n_deep,
                           opt_.init2 ? init_two_partials(lay_) : 0, 1});
   W3D_HIP(hipMalloc(&partials_, static_cast<size_t>(n_partials_) * sizeof(Partial)));
   W3D_HIP(hipMalloc(&errlog_, static_cast<size_t>(prob_.K + 1) * sizeof(Partial)));
@@ -191,35 +230,80 @@ std::vector<int> GpuSolver::check_steps() const {
   return v;
 }
 
-void GpuSolver::exchange(double* field, hipStream_t st) {
-  if (!plan_.any()) return;
-  if (plan_.packed_doubles > 0) launch_pack(lay_, plan_, field, send_buf_, st);
-  ncclComm_t c = static_cast<ncclComm_t>(comm_->raw());
-  W3D_NCCL(ncclGroupStart());
+std::string GpuSolver::mode() const {
+  switch (mode_) {
+    case Mode::kFusedSingle: return "fused-single";
+    case Mode::kDeep: return "deep-halo";
+    default: return "single-step";
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// schedule
+// ------------------------------------------------------------------------------------------------------------------
+bool GpuSolver::split() const { return opt_.overlap && plan_.any(); }
+bool GpuSolver::post_exchange() const { return mode_ == Mode::kDeep || split(); }
+
+bool GpuSolver::needs_exchange(int i) const {
+  if (!plan_.any()) return false;
+  return post_exchange() ? i + 1 < static_cast<int>(units_.size()) : i > 0;
+}
+
+hipStream_t GpuSolver::xstream() const { return post_exchange() && opt_.overlap ? s1_ : s0_; }
+
+// Deep-halo fused passes need every unit to be a pair with no error check on its intermediate step, starting from the
+// analytic (u¹, u²): K even and no odd check step below K.
+bool GpuSolver::pairable() const {
+  const int K = prob_.K;
+  if (!opt_.init2 || K < 4 || (K - 2) % 2 != 0) return false;
+  for (int n : check_steps())
+    if (n > 2 && n < K && (n % 2) != 0) return false;
+  return true;
+}
+
+void GpuSolver::build_units() {
+  units_.clear();
+  const int K = prob_.K;
+  int n = start_n_;
+  if (mode_ == Mode::kFusedSingle) {
+    while (n <= K - 1) {
+      const bool f = n + 2 <= K && !is_check_[static_cast<size_t>(n + 1)];
+      units_.push_back(Unit{n, f});
+      n += f ? 2 : 1;
+    }
+  } else if (mode_ == Mode::kDeep) {
+    for (; n <= K - 1; n += 2) units_.push_back(Unit{n, true});
+  } else {
+    for (; n <= K - 1; ++n) units_.push_back(Unit{n, false});
+  }
+}
+
+void GpuSolver::build_msgs(int i) {
+  msgs_.clear();
+  if (mode_ == Mode::kDeep) {
+    // after a fused pass the next one needs u^{n+2} on 2 ghost planes and u^{n+1} on 1 (x faces of a slab rank)
+    double* out1 = u_[uf_[0]];
+    double* out2 = u_[uf_[1]];
+    const i64 P = lay_.plane, nx = lay_.nx;
+    for (const Face& f : plan_.faces) {
+      W3D_REQUIRE(f.axis == 0, "deep-halo mode is slab-only");
+      if (f.side == 0) {
+        msgs_.push_back(Msg{f.peer, 0, out2 + lay_.plane_off(0), out2 + lay_.plane_off(-2), 2 * P});
+        msgs_.push_back(Msg{f.peer, 1, out1 + lay_.plane_off(0), out1 + lay_.plane_off(-1), P});
+      } else {
+        msgs_.push_back(Msg{f.peer, 0, out2 + lay_.plane_off(nx - 2), out2 + lay_.plane_off(nx), 2 * P});
+        msgs_.push_back(Msg{f.peer, 1, out1 + lay_.plane_off(nx - 1), out1 + lay_.plane_off(nx), P});
+      }
+    }
+    return;
+  }
+  double* field = post_exchange() ? u_[old_] : u_[cur_];
   for (const Face& f : plan_.faces) {
     const double* sp = f.contiguous ? field + f.send_off : send_buf_ + f.pack_off;
     double* rp = f.contiguous ? field + f.recv_off : recv_buf_ + f.pack_off;
-    W3D_NCCL(ncclSend(sp, static_cast<size_t>(f.count), ncclFloat64, f.peer, c, st));
-    W3D_NCCL(ncclRecv(rp, static_cast<size_t>(f.count), ncclFloat64, f.peer, c, st));
+    msgs_.push_back(Msg{f.peer, 0, sp, rp, f.count});
   }
-  W3D_NCCL(ncclGroupEnd());
-  if (plan_.packed_doubles > 0) launch_unpack(lay_, plan_, recv_buf_, field, st);
 }
-
-// ------------------------------------------------------------------------------------------------------------------
-// step phases. One step n (u^{n+1} from u^n, u^{n−1}) is: shell → exchange → interior. With overlap the exchange
-// carries the NEW field's shell faces on the side stream s1 while the interior runs on s0; without overlap the
-// exchange carries the CURRENT field's faces on s0 before the whole-box update.
-// ------------------------------------------------------------------------------------------------------------------
-bool GpuSolver::split() const { return opt_.overlap && plan_.any(); }
-
-bool GpuSolver::needs_exchange(int n) const {
-  if (!plan_.any()) return false;
-  return split() ? n < prob_.K - 1 : n > start_n_;
-}
-
-double* GpuSolver::xfield() const { return split() ? u_[old_] : u_[cur_]; }
-hipStream_t GpuSolver::xstream() const { return split() ? s1_ : s0_; }
 
 // Per-phase device timers (SolverOptions::timers, eager launches only): every timed launch group is bracketed by two
 // events on its stream; after the solve the intervals are summed per phase. The reference reports its GPU time as
@@ -255,7 +339,7 @@ void GpuSolver::phase_init() {
   marks_.clear();
   W3D_HIP(hipMemsetAsync(errlog_, 0, static_cast<size_t>(K + 1) * sizeof(Partial), s0_));
   if (opt_.init2 && K >= 2) {
-    // u¹ -> buf 0, u² -> buf 1 analytically (no read pass); the first leapfrog step is n = 2
+    // u¹ -> buf 0, u² -> buf 1 analytically (no read pass), ghosts included; the first leapfrog step is n = 2
     timed(kPhaseInit, s0_, [&] {
       launch_init_two(lay_, coef_, s, u_[0], u_[1], ct_[2], is_check_[2] ? partials_ : nullptr, s0_);
     });
@@ -279,114 +363,134 @@ void GpuSolver::phase_init() {
   }
   cur_ = 1;
   old_ = 0;
+  build_units();
 }
 
-void GpuSolver::phase_shell(int n) {
-  const bool chk = is_check_[static_cast<size_t>(n + 1)] != 0;
-  if (split()) {
+void GpuSolver::unit_shell(int i) {
+  const Unit& u = units_[static_cast<size_t>(i)];
+  if (u.fused) {
+    int k = 0;
+    for (int b = 0; b < 4; ++b)
+      if (b != cur_ && b != old_) uf_[k++] = b;
+  }
+  const int nc = u.fused ? u.n + 2 : u.n + 1;
+  const bool chk = is_check_[static_cast<size_t>(nc)] != 0;
+  if (mode_ == Mode::kDeep) {
+    int off = 0;
+    for (size_t k = 0; k < dshell_.size(); ++k) {
+      timed(kPhaseShell, s0_, [&] {
+        launch_leapfrog2(lay_, coef_, u_[old_], u_[cur_], u_[uf_[0]], u_[uf_[1]], dshell_[k], d_s_ + 1,
+                         ct_[static_cast<size_t>(nc)], chk ? partials_ + off : nullptr, opt_.tiling2, s0_, sx0_, sx1_);
+      });
+      off += n_dshell_[k];
+    }
+  } else if (mode_ == Mode::kSingleStep && split()) {
     timed(kPhaseShell, s0_, [&] {
       launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], shell_.data(), static_cast<int>(shell_.size()), d_s_ + 1,
-                      ct_[static_cast<size_t>(n + 1)], chk ? partials_ : nullptr, opt_.tiling, s0_);
+                      ct_[static_cast<size_t>(nc)], chk ? partials_ : nullptr, opt_.tiling, s0_);
     });
   }
-  if (needs_exchange(n)) W3D_HIP(hipEventRecord(ev_shell_, s0_));
+  if (needs_exchange(i)) {
+    build_msgs(i);
+    W3D_HIP(hipEventRecord(ev_shell_, s0_));
+  }
 }
 
-void GpuSolver::phase_exchange_rccl(int n) {
-  if (!needs_exchange(n)) return;
+void GpuSolver::exchange(hipStream_t st) {
+  const bool packed = mode_ == Mode::kSingleStep && plan_.packed_doubles > 0;
+  double* field = post_exchange() ? u_[old_] : u_[cur_];
+  if (packed) launch_pack(lay_, plan_, field, send_buf_, st);
+  if (!opt_.fake_comm) {  // fake_comm (perf study): one rank's schedule timed alone, ghosts keep stale values
+    ncclComm_t c = static_cast<ncclComm_t>(comm_->raw());
+    W3D_NCCL(ncclGroupStart());
+    for (const Msg& m : msgs_) {
+      W3D_NCCL(ncclSend(m.send, static_cast<size_t>(m.count), ncclFloat64, m.peer, c, st));
+      W3D_NCCL(ncclRecv(m.recv, static_cast<size_t>(m.count), ncclFloat64, m.peer, c, st));
+    }
+    W3D_NCCL(ncclGroupEnd());
+  }
+  if (packed) launch_unpack(lay_, plan_, recv_buf_, field, st);
+}
+
+void GpuSolver::unit_exchange_rccl(int i) {
+  if (!needs_exchange(i)) return;
   hipStream_t xs = xstream();
   if (xs != s0_) W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
-  if (opt_.poison_ghosts) poison(xfield(), xs);
-  timed(kPhaseComm, xs, [&] { exchange(xfield(), xs); });
-  if (split()) W3D_HIP(hipEventRecord(ev_halo_, xs));
+  if (opt_.poison_ghosts) poison(xs);
+  timed(kPhaseComm, xs, [&] { exchange(xs); });
+  if (xs != s0_) W3D_HIP(hipEventRecord(ev_halo_, xs));
 }
 
-void GpuSolver::phase_interior(int n) {
-  const bool chk = is_check_[static_cast<size_t>(n + 1)] != 0;
-  const double ct = ct_[static_cast<size_t>(n + 1)];
-  if (split()) {
+void GpuSolver::unit_interior(int i) {
+  const Unit& u = units_[static_cast<size_t>(i)];
+  const int nc = u.fused ? u.n + 2 : u.n + 1;
+  const bool chk = is_check_[static_cast<size_t>(nc)] != 0;
+  const double ct = ct_[static_cast<size_t>(nc)];
+  const double* s = d_s_ + 1;
+  const bool wait = needs_exchange(i) && xstream() != s0_;
+  int np = 0;  // partials to reduce
+  if (mode_ == Mode::kDeep) {
+    int off = 0;
+    for (int n : n_dshell_) off += n;
+    if (!dint_.empty()) {
+      timed(kPhaseCompute, s0_, [&] {
+        launch_leapfrog2(lay_, coef_, u_[old_], u_[cur_], u_[uf_[0]], u_[uf_[1]], dint_, s, ct,
+                         chk ? partials_ + off : nullptr, opt_.tiling2, s0_, sx0_, sx1_);
+      });
+    }
+    np = off + n_dint_;
+  } else if (mode_ == Mode::kFusedSingle) {
     timed(kPhaseCompute, s0_, [&] {
-      launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &interior_, 1, d_s_ + 1, ct,
-                      chk ? partials_ + n_shell_ : nullptr, opt_.tiling, s0_);
+      if (u.fused)
+        launch_leapfrog2(lay_, coef_, u_[old_], u_[cur_], u_[uf_[0]], u_[uf_[1]], full_, s, ct,
+                         chk ? partials_ : nullptr, opt_.tiling2, s0_);
+      else
+        launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &full_, 1, s, ct, chk ? partials_ : nullptr, opt_.tiling,
+                        s0_);
     });
-    if (needs_exchange(n)) W3D_HIP(hipStreamWaitEvent(s0_, ev_halo_, 0));
-    if (chk) timed(kPhaseCheck, s0_, [&] { launch_reduce(partials_, n_shell_ + n_int_, errlog_ + n + 1, s0_); });
-  } else {
+    np = u.fused ? n_fused_ : n_full_;
+  } else if (split()) {
     timed(kPhaseCompute, s0_, [&] {
-      launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &full_, 1, d_s_ + 1, ct, chk ? partials_ : nullptr,
+      launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &interior_, 1, s, ct, chk ? partials_ + n_shell_ : nullptr,
                       opt_.tiling, s0_);
     });
-    if (chk) timed(kPhaseCheck, s0_, [&] { launch_reduce(partials_, n_full_, errlog_ + n + 1, s0_); });
+    np = n_shell_ + n_int_;
+  } else {
+    timed(kPhaseCompute, s0_, [&] {
+      launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &full_, 1, s, ct, chk ? partials_ : nullptr, opt_.tiling,
+                      s0_);
+    });
+    np = n_full_;
   }
+  if (wait) W3D_HIP(hipStreamWaitEvent(s0_, ev_halo_, 0));
+  if (chk) timed(kPhaseCheck, s0_, [&] { launch_reduce(partials_, np, errlog_ + nc, s0_); });
   if (opt_.debug_sync) W3D_HIP(hipDeviceSynchronize());
-  std::swap(cur_, old_);
-  if (n == prob_.K - 1) final_buf_ = cur_;
+  if (u.fused) {
+    old_ = uf_[0];
+    cur_ = uf_[1];
+  } else {
+    std::swap(cur_, old_);
+  }
+  final_buf_ = cur_;
+  prev_buf_ = old_;
 }
 
 void GpuSolver::enqueue_solve() {
-  if (fused()) {
-    enqueue_solve_fused();
-    return;
-  }
   phase_init();
-  for (int n = start_n_; n <= prob_.K - 1; ++n) {
-    phase_shell(n);
-    phase_exchange_rccl(n);
-    phase_interior(n);
+  for (int i = 0; i < static_cast<int>(units_.size()); ++i) {
+    unit_shell(i);
+    unit_exchange_rccl(i);
+    unit_interior(i);
   }
   final_buf_ = cur_;
   prev_buf_ = old_;
 }
 
-bool GpuSolver::fused() const { return opt_.temporal == 2 && !plan_.any() && nbuf_ == 4 && !full_.empty(); }
-
-// Single rank with temporal blocking: steps are taken two at a time (u^{n+1}, u^{n+2} in one HBM pass) whenever the
-// intermediate step n+1 needs no error check; otherwise one in-place step. Four buffers rotate (see kernels.hpp).
-void GpuSolver::enqueue_solve_fused() {
-  phase_init();  // (u0, u1) or (u1, u2) -> bufs (0, 1); cur_ = 1, old_ = 0
-  const int K = prob_.K;
-  const double* s = d_s_ + 1;
-  int n = start_n_;  // u^n is current
-  while (n <= K - 1) {
-    if (n + 2 <= K && !is_check_[static_cast<size_t>(n + 1)]) {
-      int f[2], k = 0;
-      for (int b = 0; b < 4; ++b)
-        if (b != cur_ && b != old_) f[k++] = b;
-      const bool chk = is_check_[static_cast<size_t>(n + 2)] != 0;
-      timed(kPhaseCompute, s0_, [&] {
-        launch_leapfrog2(lay_, coef_, u_[old_], u_[cur_], u_[f[0]], u_[f[1]], full_, s,
-                         ct_[static_cast<size_t>(n + 2)], chk ? partials_ : nullptr, opt_.tiling2, s0_);
-      });
-      if (chk) timed(kPhaseCheck, s0_, [&] { launch_reduce(partials_, n_fused_, errlog_ + n + 2, s0_); });
-      old_ = f[0];
-      cur_ = f[1];
-      n += 2;
-    } else {
-      const bool chk = is_check_[static_cast<size_t>(n + 1)] != 0;
-      timed(kPhaseCompute, s0_, [&] {
-        launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &full_, 1, s, ct_[static_cast<size_t>(n + 1)],
-                        chk ? partials_ : nullptr, opt_.tiling, s0_);
-      });
-      if (chk) timed(kPhaseCheck, s0_, [&] { launch_reduce(partials_, n_full_, errlog_ + n + 1, s0_); });
-      std::swap(cur_, old_);
-      n += 1;
-    }
-    if (opt_.debug_sync) W3D_HIP(hipDeviceSynchronize());
-  }
-  final_buf_ = cur_;
-  prev_buf_ = old_;
-}
-
-// Debug aid: fill the ghost layers that the next exchange must overwrite with NaN, so a halo that
+// Debug aid: fill the ghost regions that the next exchange must overwrite with NaN, so a halo that
 // is not delivered shows up in the error norms at once instead of silently reusing stale values.
-void GpuSolver::poison(double* field, hipStream_t st) {
-  for (const Face& f : plan_.faces) {
-    if (f.contiguous) {
-      W3D_HIP(hipMemsetAsync(field + f.recv_off, 0xFF, static_cast<size_t>(f.count) * sizeof(double), st));
-    }
-  }
-  if (plan_.packed_doubles > 0)
-    W3D_HIP(hipMemsetAsync(recv_buf_, 0xFF, static_cast<size_t>(plan_.packed_doubles) * sizeof(double), st));
+void GpuSolver::poison(hipStream_t st) {
+  for (const Msg& m : msgs_)
+    W3D_HIP(hipMemsetAsync(m.recv, 0xFF, static_cast<size_t>(m.count) * sizeof(double), st));
 }
 
 void GpuSolver::collect_phases(RunResult& r) {
@@ -406,51 +510,45 @@ void GpuSolver::collect_phases(RunResult& r) {
 
 // ------------------------------------------------------------------------------------------------------------------
 // loopback transport (GpuGroup): P ranks in one process on one device, halos moved by device copies. Test-only
-// stand-in for RCCL that exercises the identical shell/interior split, halo plans, pack/unpack and stream/event
-// ordering of the production path on a single GPU (RCCL refuses two ranks on one device).
+// stand-in for RCCL that exercises the identical schedules, shell/interior splits, message plans, pack/unpack and
+// stream/event ordering of the production path on a single GPU (RCCL refuses two ranks on one device).
 // ------------------------------------------------------------------------------------------------------------------
-void GpuSolver::lb_pack(int n) {
-  if (!needs_exchange(n)) return;
+void GpuSolver::lb_pack(int i) {
+  if (!needs_exchange(i)) return;
   hipStream_t xs = xstream();
   if (xs != s0_) W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
-  if (plan_.packed_doubles > 0) launch_pack(lay_, plan_, xfield(), send_buf_, xs);
+  if (mode_ == Mode::kSingleStep && plan_.packed_doubles > 0)
+    launch_pack(lay_, plan_, post_exchange() ? u_[old_] : u_[cur_], send_buf_, xs);
   W3D_HIP(hipEventRecord(ev_packed_, xs));
 }
 
-void GpuSolver::lb_pull(int n, const std::vector<GpuSolver*>& ranks) {
-  if (!needs_exchange(n)) return;
+void GpuSolver::lb_pull(int i, const std::vector<GpuSolver*>& ranks) {
+  if (!needs_exchange(i)) return;
   hipStream_t xs = xstream();
-  const int b = split() ? old_ : cur_;
-  if (opt_.poison_ghosts) poison(u_[b], xs);
-  for (const Face& f : plan_.faces) {
-    const GpuSolver* q = ranks[static_cast<size_t>(f.peer)];
-    const Face* g = nullptr;
-    for (const Face& h : q->plan_.faces)
-      if (h.peer == rank_) g = &h;
-    W3D_REQUIRE(g && g->count == f.count, "loopback: mismatched faces");
+  if (opt_.poison_ghosts) poison(xs);
+  for (const Msg& m : msgs_) {
+    const GpuSolver* q = ranks[static_cast<size_t>(m.peer)];
+    const Msg* g = nullptr;
+    for (const Msg& h : q->msgs_)
+      if (h.peer == rank_ && h.tag == m.tag) g = &h;
+    W3D_REQUIRE(g && g->count == m.count, "loopback: mismatched messages");
     W3D_HIP(hipStreamWaitEvent(xs, q->ev_packed_, 0));
-    const double* src = g->contiguous ? q->u_[b] + g->send_off : q->send_buf_ + g->pack_off;
-    double* dst = f.contiguous ? u_[b] + f.recv_off : recv_buf_ + f.pack_off;
-    W3D_HIP(hipMemcpyAsync(dst, src, static_cast<size_t>(f.count) * sizeof(double), hipMemcpyDeviceToDevice, xs));
+    W3D_HIP(hipMemcpyAsync(m.recv, g->send, static_cast<size_t>(m.count) * sizeof(double), hipMemcpyDeviceToDevice,
+                           xs));
   }
-  if (plan_.packed_doubles > 0) launch_unpack(lay_, plan_, recv_buf_, u_[b], xs);
+  if (mode_ == Mode::kSingleStep && plan_.packed_doubles > 0)
+    launch_unpack(lay_, plan_, recv_buf_, post_exchange() ? u_[old_] : u_[cur_], xs);
   W3D_HIP(hipEventRecord(ev_halo_, xs));
 }
 
-void GpuSolver::lb_fence(int n, const std::vector<GpuSolver*>& ranks) {
+void GpuSolver::lb_fence(int i, const std::vector<GpuSolver*>& ranks) {
   // the peers have read this rank's send regions once their pulls are done: keep both streams behind them
-  if (!needs_exchange(n)) return;
-  for (const Face& f : plan_.faces) {
-    const GpuSolver* q = ranks[static_cast<size_t>(f.peer)];
+  if (!needs_exchange(i)) return;
+  for (const Msg& m : msgs_) {
+    const GpuSolver* q = ranks[static_cast<size_t>(m.peer)];
     W3D_HIP(hipStreamWaitEvent(s0_, q->ev_halo_, 0));
-    if (s1_ != s0_) W3D_HIP(hipStreamWaitEvent(s1_, q->ev_halo_, 0));
+    W3D_HIP(hipStreamWaitEvent(s1_, q->ev_halo_, 0));
   }
-}
-
-RunResult GpuSolver::collect_local() {
-  RunResult r;
-  gather_errors(r);
-  return r;
 }
 
 void GpuSolver::gather_errors(RunResult& r) {
@@ -562,19 +660,18 @@ RunResult GpuGroup::run() {
   const int K = rs[0]->prob_.K;
   const double t0 = now_s();
   for (auto* s : rs) s->phase_init();
-  for (int n = rs[0]->start_n_; n <= K - 1; ++n) {
-    for (auto* s : rs) s->phase_shell(n);
-    for (auto* s : rs) s->lb_pack(n);
-    for (auto* s : rs) s->lb_pull(n, rs);
-    for (auto* s : rs) s->lb_fence(n, rs);
-    for (auto* s : rs) s->phase_interior(n);
+  const int nu = static_cast<int>(rs[0]->units_.size());
+  for (int i = 0; i < nu; ++i) {
+    for (auto* s : rs) s->unit_shell(i);
+    for (auto* s : rs) s->lb_pack(i);
+    for (auto* s : rs) s->lb_pull(i, rs);
+    for (auto* s : rs) s->lb_fence(i, rs);
+    for (auto* s : rs) s->unit_interior(i);
   }
   // combine the per-rank error logs in rank order (what the RCCL all-gather does across processes)
   const size_t per = static_cast<size_t>(K + 1);
   std::vector<Partial> all(per * rs.size());
   for (size_t q = 0; q < rs.size(); ++q) {
-    rs[q]->final_buf_ = rs[q]->cur_;
-    rs[q]->prev_buf_ = rs[q]->old_;
     W3D_HIP(hipMemcpyAsync(all.data() + q * per, rs[q]->errlog_, per * sizeof(Partial), hipMemcpyDeviceToHost,
                            rs[q]->s0_));
   }

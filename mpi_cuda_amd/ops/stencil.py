@@ -30,10 +30,11 @@ def sin_table_ext(problem, device="cpu") -> torch.Tensor:
 
 
 def grid_view(layout, u: torch.Tensor) -> torch.Tensor:
-    """Dense (nx+2, ny+2, nz+2) view (ghosts included) of a padded flat field."""
+    """Dense (nx+2, ny+2, nz+2) view (one ghost layer on every side) of a padded flat field."""
     nx, ny, nz, p, zs = int(layout.nx), int(layout.ny), int(layout.nz), int(layout.pitch), int(layout.zs)
-    rows = u.view(nx + 2, ny + 2, p)
-    return rows[:, :, zs: zs + nz + 2]
+    xg = int(getattr(layout, "xg", 1))
+    rows = u.view(nx + 2 * xg, ny + 2, p)
+    return rows[xg - 1: xg + nx + 1, :, zs: zs + nz + 2]
 
 
 def to_grid(layout, u: torch.Tensor) -> torch.Tensor:

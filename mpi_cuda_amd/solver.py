@@ -74,7 +74,7 @@ class Solver:
                  overlap: bool = True, graph: bool = True, threads: int = 0, tiling: dict | None = None,
                  comm=None, group=None, stage_via_host: bool = False, force: bool = False, temporal: int = 2,
                  tiling2: dict | None = None, init2: bool = True, timers: bool = False,
-                 debug_sync: bool = False, poison_ghosts: bool = False):
+                 debug_sync: bool = False, poison_ghosts: bool = False, deep_min_planes: int | None = None):
         import torch.distributed as dist
 
         if not spec.cfl_ok and not force:
@@ -102,6 +102,8 @@ class Solver:
         if self.backend == "hip" and self.transport == "loopback":
             opts = self._options(C, decomp, spec, overlap, False, tiling, temporal, tiling2, init2)
             opts.timers, opts.debug_sync, opts.poison_ghosts = timers, debug_sync, poison_ghosts
+            if deep_min_planes is not None:
+                opts.deep_min_planes = deep_min_planes
             self._impl = C.GpuGroup(spec.native(), opts, world)
             self.dims = self._impl.dims().as_tuple()
         elif self.backend == "hip" and self.transport == "rccl":
@@ -109,6 +111,8 @@ class Solver:
 
             opts = self._options(C, decomp, spec, overlap, graph, tiling, temporal, tiling2, init2)
             opts.timers, opts.debug_sync, opts.poison_ghosts = timers, debug_sync, poison_ghosts
+            if deep_min_planes is not None:
+                opts.deep_min_planes = deep_min_planes
             if comm is None and world > 1:
                 comm = make_comm(rank, world, group)
             self.comm = comm

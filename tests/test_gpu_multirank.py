@@ -22,7 +22,7 @@ CASES = [(2, "slab"), (3, "slab"), (8, "slab"), (4, "block"), (8, "2x2x2"), (6, 
 
 @pytest.fixture(scope="module")
 def single():
-    spec = ProblemSpec(N=70, tau=1e-3, K=9, check_every=2)
+    spec = ProblemSpec(N=70, tau=1e-3, K=9, check_every=2)  # K odd: single-step schedule
     s = Solver(spec, backend="hip", device=0)
     r = s.run()
     return spec, r, s.global_field(0), s.global_field(1)
@@ -113,3 +113,43 @@ def test_phase_timers(gpu):
     assert ph["init_ms"] > 0 and ph["compute_ms"] > 0 and ph["check_ms"] > 0
     ref = Solver(spec, backend="hip", device=0).run()
     assert r.max_err == ref.max_err
+
+
+@pytest.fixture(scope="module")
+def single_even():
+    spec = ProblemSpec(N=66, tau=1e-3, K=10, check_every=2)
+    s = Solver(spec, backend="hip", device=0)
+    r = s.run()
+    return spec, r, s.global_field(0), s.global_field(1)
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("world", [2, 3, 4, 8, 16])
+def test_deep_halo_temporal_blocking_bitexact(gpu, single_even, world, overlap):
+    """Slab ranks with 2-deep x halos run the fused two-step kernel (one exchange of 3 planes per face per pass):
+    bit-identical to one GPU, also with NaN-poisoned ghosts."""
+    spec, r1, f0, f1 = single_even
+    g = Solver(spec, backend="hip", transport="loopback", world=world, rank=0, decomp="slab", overlap=overlap,
+               device=0, poison_ghosts=True, deep_min_planes=3)
+    assert g.native.mode() == "deep-halo"
+    r = g.run()
+    assert r.steps == r1.steps and r.max_err == r1.max_err
+    for a, b in zip(r.rms_err, r1.rms_err):
+        assert math.isclose(a, b, rel_tol=1e-12)
+    assert torch.equal(g.global_field(0), f0)
+    assert torch.equal(g.global_field(1), f1)
+
+
+def test_schedule_modes(gpu):
+    even = ProblemSpec(N=40, tau=1e-3, K=10)
+    odd_check = ProblemSpec(N=40, tau=1e-3, K=10, check_every=1)
+    assert Solver(even, backend="hip", device=0).native.mode == "fused-single"
+    assert Solver(even, backend="hip", device=0, temporal=1).native.mode == "single-step"
+    assert Solver(even, backend="hip", transport="loopback", world=4, rank=0, decomp="2x2x1",
+                  device=0).native.mode() == "single-step"
+    assert Solver(odd_check, backend="hip", transport="loopback", world=2, rank=0, decomp="slab",
+                  device=0, deep_min_planes=3).native.mode() == "single-step"
+    assert Solver(even, backend="hip", transport="loopback", world=2, rank=0, decomp="slab",
+                  device=0, deep_min_planes=3).native.mode() == "deep-halo"
+    assert Solver(even, backend="hip", transport="loopback", world=2, rank=0, decomp="slab",
+                  device=0).native.mode() == "single-step"  # 20 planes per rank < default 96

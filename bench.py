@@ -137,7 +137,7 @@ def main() -> int:
         par = f"{a.decomp}{world}" if world > 1 else "single"
         dims = "x".join(str(d) for d in solver.dims)
         line = {
-            "metric": "gcell_updates_per_s_512cube_K20",
+            "metric": f"gcell_updates_per_s_{a.N}cube_K{a.K}",
             "value": round(value, 3),
             "unit": "GCell-updates/s",
             "n_gpus": world,

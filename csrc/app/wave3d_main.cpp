@@ -45,7 +45,7 @@ struct Args {
   int temporal = 2;
   bool init2 = true;
   int fake_rank = -1, fake_world = 0;
-  int t2_rows = 0, t2_target = -1, deep_min = -1;
+  int t2_rows = 0, t2_target = -1, deep_min = -1, t2_occ = -1;
   bool force = false;
   int repeat = 1;
   int warmup = 0;
@@ -114,6 +114,7 @@ Args parse(int argc, char** argv) {
     else if (s == "--t2-rows") a.t2_rows = std::stoi(next());
     else if (s == "--deep-min-planes") a.deep_min = std::stoi(next());
     else if (s == "--t2-target") a.t2_target = std::stoi(next());
+    else if (s == "--t2-occ") a.t2_occ = std::stoi(next());
     else if (s == "--fake-rank") {
       const std::string v = next();  // R/P: time rank R of a P-rank decomposition alone, no transport
       a.fake_rank = std::stoi(v.substr(0, v.find('/')));
@@ -318,6 +319,7 @@ int run_gpu(const Args& a) {
   o.fake_comm = fake;
   if (a.t2_rows > 0) o.tiling2.rows = a.t2_rows;
   if (a.deep_min >= 0) o.deep_min_planes = a.deep_min;
+  if (a.t2_occ >= 0) o.tiling2.occupancy = a.t2_occ;
   if (a.t2_target >= 0) o.tiling2.target_waves = a.t2_target;
   if (a.variant >= 0) o.tiling.variant = a.variant;
   if (a.tile_rows > 0) (o.tiling.variant == 1 ? o.tiling.rows : o.tiling.ty) = a.tile_rows;

@@ -55,6 +55,7 @@ void launch_leapfrog(const Layout& l, const Coeffs& c, const double* cur, double
 // error of u^{n+2} vs φ·ct2 is reduced per wave.
 struct Leapfrog2Tiling {
   int rows = 2;           // output rows per wave (1, 2 or 4)
+  int occupancy = 0;      // rows = 2 only: >= 3 builds for 3 waves/SIMD (register cap, some spills)
   int target_waves = 0;   // x-chunking target (0 = auto)
   bool xcd_remap = true;
   bool nt_store = true;

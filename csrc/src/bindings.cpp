@@ -295,6 +295,7 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init<>())
       .def_readwrite("rows", &Leapfrog2Tiling::rows)
       .def_readwrite("target_waves", &Leapfrog2Tiling::target_waves)
+      .def_readwrite("occupancy", &Leapfrog2Tiling::occupancy)
       .def_readwrite("xcd_remap", &Leapfrog2Tiling::xcd_remap)
       .def_readwrite("nt_store", &Leapfrog2Tiling::nt_store);
   m.def("gpu_leapfrog2_partials", &leapfrog2_partials);

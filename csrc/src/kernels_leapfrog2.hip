@@ -64,8 +64,10 @@ struct Lf2Params {
   int ntz, nty, xchunk, ntiles, nblocks, xcd_remap;
 };
 
-template <int R, bool CHECK, bool NT>
-__global__ __launch_bounds__(64 * kWaves) void k_leapfrog2_rq(const Lf2Params p) {
+// OCC > 1 asks the compiler for at least OCC waves per SIMD (fewer VGPRs, possibly some scratch spills)
+template <int R, bool CHECK, bool NT, int OCC>
+__global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(OCC))) void k_leapfrog2_rq(
+    const Lf2Params p) {
   constexpr int E = R + 4;  // extended rows: e ↔ y = yt − 2 + e
   const int lane = static_cast<int>(threadIdx.x) & 63;
   const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);  // wave-uniform: tile math stays scalar
@@ -316,19 +318,19 @@ Plan2 make_plan2(const Layout& l, const LBox& b, const Leapfrog2Tiling& t, i64 s
   return pl;
 }
 
-template <int R>
-void launch_r(const Lf2Params& p, int nblocks, bool check, bool nt, hipStream_t st) {
+template <int R, int OCC>
+void launch_ro(const Lf2Params& p, int nblocks, bool check, bool nt, hipStream_t st) {
   const dim3 block(64 * kWaves), grid(nblocks);
   if (check) {
     if (nt)
-      hipLaunchKernelGGL((k_leapfrog2_rq<R, true, true>), grid, block, 0, st, p);
+      hipLaunchKernelGGL((k_leapfrog2_rq<R, true, true, OCC>), grid, block, 0, st, p);
     else
-      hipLaunchKernelGGL((k_leapfrog2_rq<R, true, false>), grid, block, 0, st, p);
+      hipLaunchKernelGGL((k_leapfrog2_rq<R, true, false, OCC>), grid, block, 0, st, p);
   } else {
     if (nt)
-      hipLaunchKernelGGL((k_leapfrog2_rq<R, false, true>), grid, block, 0, st, p);
+      hipLaunchKernelGGL((k_leapfrog2_rq<R, false, true, OCC>), grid, block, 0, st, p);
     else
-      hipLaunchKernelGGL((k_leapfrog2_rq<R, false, false>), grid, block, 0, st, p);
+      hipLaunchKernelGGL((k_leapfrog2_rq<R, false, false, OCC>), grid, block, 0, st, p);
   }
 }
 
@@ -365,9 +367,14 @@ void launch_leapfrog2(const Layout& l, const Coeffs& c, const double* prev, cons
   p.ct2 = ct2;
   const bool check = partials != nullptr;
   switch (t.rows) {
-    case 1: launch_r<1>(p, pl.nblocks, check, t.nt_store, stream); break;
-    case 2: launch_r<2>(p, pl.nblocks, check, t.nt_store, stream); break;
-    default: launch_r<4>(p, pl.nblocks, check, t.nt_store, stream); break;
+    case 1: launch_ro<1, 1>(p, pl.nblocks, check, t.nt_store, stream); break;
+    case 2:
+      if (t.occupancy >= 3)
+        launch_ro<2, 3>(p, pl.nblocks, check, t.nt_store, stream);
+      else
+        launch_ro<2, 1>(p, pl.nblocks, check, t.nt_store, stream);
+      break;
+    default: launch_ro<4, 1>(p, pl.nblocks, check, t.nt_store, stream); break;
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) fail(std::string("leapfrog2 launch: ") + hipGetErrorString(e));

@@ -165,7 +165,13 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
 
   // device memory
   W3D_HIP(hipStreamCreateWithFlags(&s0_, hipStreamNonBlocking));
-  W3D_HIP(hipStreamCreateWithFlags(&s1_, hipStreamNonBlocking));
+  {
+    // the exchange stream gets the highest priority so RCCL's copy kernels are dispatched ahead of the waiting
+    // interior workgroups: the halo overlaps the interior update instead of queueing behind it
+    int lo = 0, hi = 0;
+    W3D_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    W3D_HIP(hipStreamCreateWithPriority(&s1_, hipStreamNonBlocking, hi));
+  }
   W3D_HIP(hipEventCreateWithFlags(&ev_shell_, hipEventDisableTiming));
   W3D_HIP(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
   W3D_HIP(hipEventCreateWithFlags(&ev_packed_, hipEventDisableTiming));

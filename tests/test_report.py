@@ -1,0 +1,33 @@
+"""utils/report.py and tools/scaling_report.py: reference output conventions (report.pdf p.15-17, readme.md:84-114)."""
+import json
+import os
+import subprocess
+import sys
+
+from mpi_cuda_amd.utils.report import error_line, gcell_per_s, parse_error_line, speedup_table
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_error_line_format_roundtrip():
+    line = error_line(2, 0.002, 3.967859e-11, 1.406978e-11)
+    assert line == "Step 2, t = 0.002000, Max Error = 3.967859e-11, L2 Error = 1.406978e-11"
+    assert parse_error_line(line) == (2, 0.002, 3.967859e-11, 1.406978e-11)
+    assert parse_error_line("Total time: 1 s") is None
+
+
+def test_speedup_conventions():
+    # readme.md:99-100: GPU speedups vs the 21.98 s sequential run, efficiency divided by the number of ranks
+    rows = speedup_table(21.98, {1: 0.752, 2: 0.505})
+    assert abs(rows[0]["speedup"] - 29.23) < 0.01 and abs(rows[1]["speedup"] - 43.52) < 0.01
+    assert abs(rows[1]["efficiency"] - 21.76) < 0.01
+    assert abs(gcell_per_s(512, 20, 0.752) - 3.570) < 1e-3
+
+
+def test_scaling_report_table(tmp_path):
+    p = tmp_path / "s.jsonl"
+    rows = [{"n_gpus": 1, "ms_per_step": 9.0, "value": 298.0}, {"n_gpus": 2, "ms_per_step": 5.0, "value": 536.0}]
+    p.write_text("\n".join(json.dumps(r) for r in rows) + "\n")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scaling_report.py"), str(p)], check=True,
+                         capture_output=True, text=True).stdout
+    assert "| 2 | 0.00500 |" in out and "1.80" in out and "101.0x" in out

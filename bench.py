@@ -53,6 +53,8 @@ def main() -> int:
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-temporal", action="store_true", help="one leapfrog step per HBM pass (no temporal blocking)")
+    ap.add_argument("--temporal", type=int, default=4, help="at most this many leapfrog steps per HBM pass (2..4)")
+    ap.add_argument("--no-tb", action="store_true", help="one rank: two-step register-queue passes, not the LDS kernel")
     ap.add_argument("--variant", type=int, default=1, help="leapfrog kernel (1 = register-queue, 0 = LDS tile)")
     ap.add_argument("--tile-rows", type=int, default=0, help="rows per wave (v1) / per workgroup (v0); 0 = default")
     ap.add_argument("--cpu", action="store_true", help="CPU backend (contract test without a GPU)")
@@ -79,7 +81,8 @@ def main() -> int:
     def make(transport, group=None):
         return Solver(spec, backend=backend, transport=transport, decomp=a.decomp, rank=rank, world=world,
                       device=None if a.cpu else local, overlap=not a.no_overlap, graph=not a.no_graph,
-                      tiling=_tiling(a), group=group, temporal=1 if a.no_temporal else 2)
+                      tiling=_tiling(a), group=group, temporal=1 if a.no_temporal else a.temporal,
+                      tb=not a.no_tb)
 
     # The native RCCL runtime is the production path. If it fails on some rank (it throws; stuck exchanges time out),
     # every rank switches together to the torch.distributed transport (RCCL through ProcessGroupNCCL) so the scaling

@@ -42,7 +42,9 @@ struct Args {
   bool timers = false;
   bool debug_sync = false;
   bool poison = false;
-  int temporal = 2;
+  int temporal = 4;
+  bool tb = true;
+  int tb_threads = 0;
   bool init2 = true;
   int fake_rank = -1, fake_world = 0;
   int t2_rows = 0, t2_target = -1, deep_min = -1, t2_occ = -1;
@@ -73,6 +75,9 @@ struct Args {
                "  --no-graph         eager launches instead of one captured hipGraph\n"
                "  --timers           per-phase GPU timers (init / compute / exchange / check)\n"
                "  --no-temporal      one leapfrog step per HBM pass (disable temporal blocking)\n"
+               "  --temporal S       at most S (2..4) leapfrog steps per HBM pass (default 4)\n"
+               "  --no-tb            one rank: two-step register-queue passes instead of the LDS S-step kernel\n"
+               "  --tb-threads T     LDS S-step kernel workgroup size (512 or 1024)\n"
                "  --no-init2         start from u0,u1 + a first step instead of analytic u1,u2\n"
                "  --debug-sync       synchronize after every step (race triage)\n"
                "  --poison-ghosts    NaN-fill ghost layers before every exchange (missed-halo detector)\n"
@@ -110,6 +115,9 @@ Args parse(int argc, char** argv) {
     else if (s == "--debug-sync") a.debug_sync = true;
     else if (s == "--poison-ghosts") a.poison = true;
     else if (s == "--no-temporal") a.temporal = 1;
+    else if (s == "--temporal") a.temporal = std::stoi(next());
+    else if (s == "--no-tb") a.tb = false;
+    else if (s == "--tb-threads") a.tb_threads = std::stoi(next());
     else if (s == "--no-init2") a.init2 = false;
     else if (s == "--t2-rows") a.t2_rows = std::stoi(next());
     else if (s == "--deep-min-planes") a.deep_min = std::stoi(next());
@@ -315,6 +323,8 @@ int run_gpu(const Args& a) {
   o.debug_sync = a.debug_sync;
   o.poison_ghosts = a.poison;
   o.temporal = a.temporal;
+  o.tb = a.tb;
+  if (a.tb_threads > 0) o.tiling_tb.threads = a.tb_threads;
   o.init2 = a.init2;
   o.fake_comm = fake;
   if (a.t2_rows > 0) o.tiling2.rows = a.t2_rows;

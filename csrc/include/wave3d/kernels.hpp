@@ -68,6 +68,25 @@ void launch_leapfrog2(const Layout& l, const Coeffs& c, const double* prev, cons
                       double* out2, const LBox& box, const double* d_s, double ct2, Partial* partials,
                       const Leapfrog2Tiling& t, hipStream_t stream, i64 sx0 = 1, i64 sx1 = 0);
 
+// Deep temporal blocking: S = 2..4 leapfrog steps in one pass, all intermediate levels in LDS (32 × 32 (y,z) tiles
+// marching in x, one workgroup per CU). Reads u^{n−1}, u^n; writes u^{n+S−1} into out1 and u^{n+S} into out2: 32/S
+// compulsory bytes per node-step. Same preconditions as launch_leapfrog2 with S−1 stage-1 planes beyond the box.
+// Error check of u^{n+k} when bit k−1 of `check_mask` is set (ct[k−1] = its time factor); stage k's partials go to
+// partials + (k−1)·leapfrog_tb_partials().
+struct LeapfrogTbTiling {
+  int stages = 4;         // 2, 3 or 4 steps per pass
+  int threads = 1024;     // workgroup size (512 or 1024; 1024 measured faster at every S)
+  bool xcd_remap = true;
+  bool nt_store = true;
+};
+// Raise the dynamic-LDS limit of every instantiation (call before capturing launches into a graph).
+void leapfrog_tb_prepare();
+size_t leapfrog_tb_lds_bytes(int stages);
+int leapfrog_tb_partials(const Layout& l, const LBox& box, const LeapfrogTbTiling& t);
+void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
+                        double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
+                        Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, i64 sx0 = 1, i64 sx1 = 0);
+
 // Error of a stored field vs φ·ct over `box` (step 1 / standalone check). Writes leapfrog-compatible partials and
 // returns how many.
 int error_blocks(const Layout& l, const LBox& box);

@@ -38,10 +38,13 @@ struct SolverOptions {
   bool poison_ghosts = false;   // NaN-fill ghost layers before each exchange (a missed halo poisons the errors)
   bool fake_comm = false;       // perf study only: run rank `rank` of `world` alone, exchanges replaced by no-ops
   LeapfrogTiling tiling;
-  // Temporal blocking: 2 = fuse pairs of steps into one HBM pass (k_leapfrog2) wherever no halo exchange and no
-  // intermediate error check intervene (single rank); 1 = one step per pass everywhere.
-  int temporal = 2;
+  // Temporal blocking: up to `temporal` (2..4) steps per HBM pass wherever no halo exchange intervenes. One rank:
+  // k_leapfrog_tb passes (all levels in LDS, error checks at any level), the steps split into passes by measured
+  // per-step cost; slab ranks: two-step k_leapfrog2 passes with 2-deep halos. 1 = one step per pass everywhere.
+  int temporal = 4;
+  bool tb = true;  // one rank: LDS kernel (false: k_leapfrog2 pairs, only where the intermediate step has no check)
   Leapfrog2Tiling tiling2;
+  LeapfrogTbTiling tiling_tb;
   // Start from u¹, u² computed analytically in one write-only pass (k_init_two) instead of u⁰, u¹ + a first step.
   bool init2 = true;
   // Slab ranks use the deep-halo fused schedule only from this many owned x-planes up (below, single steps are faster).
@@ -117,12 +120,13 @@ class GpuSolver {
   void enqueue_solve();  // all device work of one solve on s0/s1 (graph-capturable)
   void exchange(hipStream_t st);
   void gather_errors(RunResult& r);
-  // Schedule: a solve is phase_init() followed by units; a unit advances one step (in place over u^{n−1}) or two
+  // Schedule: a solve is phase_init() followed by units; a unit advances one step (in place over u^{n−1}) or 2..4
   // (a fused pass into the two free buffers). Multi-rank units run shell -> exchange -> interior.
   enum class Mode { kSingleStep, kFusedSingle, kDeep };
   struct Unit {
-    int n;       // current level u^n before the unit
-    bool fused;  // two steps (u^{n+1}, u^{n+2}) in one pass
+    int n;      // current level u^n before the unit
+    int steps;  // 1: in-place single step; >= 2: one fused pass writing u^{n+steps−1}, u^{n+steps}
+    bool fused() const { return steps >= 2; }
   };
   // one point-to-point message of an exchange: `tag` pairs it with the peer's matching message
   struct Msg {
@@ -182,6 +186,7 @@ class GpuSolver {
   hipStream_t s0_ = nullptr, s1_ = nullptr;
   hipEvent_t ev_shell_ = nullptr, ev_halo_ = nullptr, ev_packed_ = nullptr;
   int n_full_ = 0, n_shell_ = 0, n_int_ = 0, n_fused_ = 0;  // error partials of each launch kind
+  int n_tb_ = 0;                                            // ... per level of a k_leapfrog_tb pass
   int cur_ = 1, old_ = 0;                     // buffer roles during enqueue
   int start_n_ = 1;                           // first leapfrog step after the init kernel
   std::vector<char> is_check_;

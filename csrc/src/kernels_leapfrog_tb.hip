@@ -1,0 +1,467 @@
+// Deep temporal blocking: S (2..4) leapfrog steps per pass over HBM, intermediate levels on chip (gfx950).
+// See wave3d/kernels.hpp.
+//
+// The two-step register-queue kernel (kernels_leapfrog2.hip) moves 16 B per node-step and already streams at the HBM
+// rate of a half-write workload, so the remaining lever is more steps per pass. Design:
+//   * a workgroup owns a 32 × 32 tile of the (y,z) plane (256 tiles at 512³: one per CU) and marches along x through
+//     the whole box. Iteration i loads plane i+2 of u^n, and stage k = 1..S computes u^{n+k} at plane i−(k−1) — a
+//     skewed wavefront over the shrinking regions "tile + (S−k) halo" (redundant halo work ≈ 1.2× at S = 4);
+//   * every thread owns fixed (y,z) nodes of the stage-1 region in EVERY level, so the x neighbours and the "old"
+//     level of a node are the thread's own earlier results: per level a 4-deep register queue of planes (the x loop
+//     is unrolled by 4 so queue slots are static registers);
+//   * only the four y/z neighbours go through LDS: one plane per level in two parity slots. Stage k reads the plane
+//     of u^{n+k−1} that stage k−1 wrote in the PREVIOUS iteration, so one barrier per iteration suffices;
+//   * u^n is prefetched two planes ahead (global → register queue; the halo ring of the tile → two ring registers),
+//     u^{n−1} one plane ahead straight into registers (it is only ever the "old" level of the thread's own nodes);
+//   * stages S−1 and S store the tile (u^{n+S−1}, u^{n+S}): 2 reads + 2 writes per node per pass = 32/S B/node-step;
+//   * (y,z) positions outside the global interior load the boundary node (y,z) = (0,0) of their plane instead, which
+//     is 0 in every buffer on every init path (φ = 0 on it: sin-table boundary zero; the updates never write it), so
+//     no select follows a load and its wait is deferred to the first use; planes beyond the boundary only feed stage
+//     values outside the interior, which are forced to 0 like every stage output there;
+//   * any subset of the S new levels can carry the fused error check (per-stage partials).
+// Formulas and operation order are those of stencil.hpp: one pass is bit-identical to S single steps. The pass
+// semantics (which plane of which level each stage reads) are mirrored by tools/tb_emulate.py (CPU tests).
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <type_traits>
+
+#include "wave3d/kernels.hpp"
+#include "wave3d/stencil.hpp"
+
+namespace wave3d {
+
+namespace {
+
+constexpr int kTile = 32;  // tile edge (y and z)
+
+__device__ __forceinline__ void wave_reduce(double& m, double& s) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const double om = __shfl_xor(m, o, 64);
+    const double os = __shfl_xor(s, o, 64);
+    m = om > m ? om : m;
+    s = s + os;
+  }
+}
+
+struct TbParams {
+  const double* prev;  // u^{n−1}
+  const double* cur;   // u^n
+  double* out1;        // u^{n+S−1}
+  double* out2;        // u^{n+S}
+  const double* s;     // sin table, global index −1..N+1
+  Partial* partials;   // [S][nblocks]; stage k's block at (k−1)·nblocks (checked stages only)
+  i64 plane, pitch, zs;
+  int x0, x1;          // output x range (local)
+  int sx0, sx1;        // x range where stage outputs are real (outside: Dirichlet 0)
+  int ax0, ax1;        // allocated x range (local planes that may be read)
+  int N, gx0, gy0, gz0;
+  int y0, y1, z0, z1;  // output (y, z) range (local)
+  double ihx2, ihy2, ihz2, tau2;
+  double ct[4];        // time factor of u^{n+k} (k = 1..S) for the check
+  int check_mask;      // bit k−1: check u^{n+k}
+  int nty, ntz, nblocks, xcd_remap;
+};
+
+template <int S, int T, int NT>
+struct TbGeom {
+  static constexpr int H1 = T + 2 * (S - 1);  // stage-1 region edge: the thread-owned positions
+  static constexpr int NP = H1 * H1;
+  static constexpr int Q = (NP + NT - 1) / NT;  // positions per thread
+  static constexpr int W0 = T + 2 * S;          // u^n region edge = LDS plane edge (all levels share the indexing)
+  static constexpr int PL = W0 * W0;
+  static constexpr int NR = PL - NP;            // u^n halo ring (not thread-owned)
+  static constexpr int QR = (NR + NT - 1) / NT;
+  static constexpr int lds_doubles() { return S * 2 * PL; }  // levels 0..S−1 × 2 parity slots
+};
+
+// + the sin factors of the tile (y, z) and of the owned planes (x) for the error check: a global load of the per-plane
+// x factor would be a vector load (the table may alias the outputs, so no scalar load) whose wait drains the prefetch
+template <int S, int T, int NT>
+constexpr size_t tb_lds_bytes(int nxo = 0) {
+  return (static_cast<size_t>(TbGeom<S, T, NT>::lds_doubles()) + 2 * T + static_cast<size_t>(nxo)) * sizeof(double);
+}
+
+template <int S, int T, int NT, bool NTS>
+__global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
+  using G = TbGeom<S, T, NT>;
+  constexpr int Q = G::Q, QR = G::QR, H1 = G::H1, W0 = G::W0, PL = G::PL;
+  constexpr int kOwn = 1 << 30;  // gof flag: tile node inside the output box
+  constexpr int kReal = 1 << 8;  // regm flag: node inside the global interior
+  extern __shared__ double lds[];
+  const int tid = static_cast<int>(threadIdx.x);
+  int blk = static_cast<int>(blockIdx.x);
+  if (p.xcd_remap) blk = (blk & 7) * (p.nblocks >> 3) + (blk >> 3);
+  const bool active = blk < p.nty * p.ntz;
+  const int tzi = active ? blk % p.ntz : 0, tyi = active ? blk / p.ntz : 0;
+  const int ty0 = p.y0 + tyi * T, tz0 = p.z0 + tzi * T;
+  const int N = p.N;
+  const i64 P = p.plane;
+  const int R = static_cast<int>(p.pitch), zs1 = static_cast<int>(p.zs) + 1;
+  const double ihx2 = p.ihx2, ihy2 = p.ihy2, ihz2 = p.ihz2, tau2 = p.tau2;
+  auto inside = [&](int g) { return static_cast<unsigned>(g - 1) < static_cast<unsigned>(N - 1); };
+
+  double emax[S], esum[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) emax[k] = esum[k] = 0.0;
+
+  if (active) {
+    // ---- per-thread descriptors of the owned positions (stage-1 region coordinates a, b ∈ [0, H1))
+    // zero node: (y, z) = (0, 0), a global boundary node for whole-plane ranks (gy0 = gz0 = 0)
+    const int zero_off = R + zs1;
+    int lid[Q];   // LDS index (u^n-region coordinates a+1, b+1), −1: no position
+    int gof[Q];   // in-plane offset to load (zero node outside the interior) | kOwn
+    int regm[Q];  // bit k−1: inside stage k's region (halo S−k); kReal
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int idx = tid + q * NT;
+      const int a = idx / H1, b = idx - (idx / H1) * H1;
+      const int y = ty0 - (S - 1) + a, z = tz0 - (S - 1) + b;
+      const bool valid = idx < G::NP;
+      const bool real = valid && inside(p.gy0 + y) && inside(p.gz0 + z);
+      const bool own = real && a >= S - 1 && a < S - 1 + T && b >= S - 1 && b < S - 1 + T && y < p.y1 && z < p.z1;
+      lid[q] = valid ? (a + 1) * W0 + (b + 1) : -1;
+      gof[q] = real ? (((y + 1) * R + z + zs1) | (own ? kOwn : 0)) : zero_off;
+      int m = real ? kReal : 0;
+#pragma unroll
+      for (int k = 1; k <= S; ++k)
+        if (valid && a >= k - 1 && a < H1 - (k - 1) && b >= k - 1 && b < H1 - (k - 1)) m |= 1 << (k - 1);
+      regm[q] = m;
+    }
+    // u^n halo ring: LDS index and global offset (−1: outside the interior; lrid −1: no ring node)
+    int lrid[QR], grof[QR];
+#pragma unroll
+    for (int r = 0; r < QR; ++r) {
+      const int ridx = tid + r * NT;
+      int a0 = 0, b0 = 0;
+      if (ridx < W0) {
+        b0 = ridx;
+      } else if (ridx < 2 * W0) {
+        a0 = W0 - 1;
+        b0 = ridx - W0;
+      } else if (ridx < 3 * W0 - 2) {
+        a0 = 1 + ridx - 2 * W0;
+      } else {
+        a0 = 1 + ridx - (3 * W0 - 2);
+        b0 = W0 - 1;
+      }
+      const int y = ty0 - S + a0, z = tz0 - S + b0;
+      const bool valid = ridx < G::NR;
+      lrid[r] = valid ? a0 * W0 + b0 : -1;
+      grof[r] = (valid && inside(p.gy0 + y) && inside(p.gz0 + z)) ? (y + 1) * R + z + zs1 : zero_off;
+    }
+    // sin factors for the check: y and z of the tile, x of the owned planes (clamped into −1..N+1; only owned nodes,
+    // all interior, use them)
+    double* sty = lds + G::lds_doubles();
+    double* stz = sty + T;
+    double* stx = stz + T;
+    if (p.check_mask) {
+      auto sc = [&](int g) { return p.s[g < -1 ? -1 : g > N + 1 ? N + 1 : g]; };
+      for (int t = tid; t < T; t += NT) {
+        sty[t] = sc(p.gy0 + ty0 + t);
+        stz[t] = sc(p.gz0 + tz0 + t);
+      }
+      for (int x = tid; x < p.x1 - p.x0; x += NT) stx[x] = p.s[p.gx0 + p.x0 + x];
+    }
+
+    // ---- register queues: plane x of level j at slot (x − i0) & 3; u^{n−1} and the ring: slot (x − i0) & 1
+    double L[S][Q][4];  // L[0] = u^n, L[k] = u^{n+k} (k < S)
+    double Lm[Q][2];    // u^{n−1}
+    double Rg[QR][2];   // u^n ring
+    const int x0 = p.x0, x1 = p.x1;
+    const int i0 = x0 - S + 1, i1 = x1 + S - 2;
+    auto lds_plane = [&](int j, int par) { return lds + (j * 2 + par) * PL; };
+
+    // plane x of u^n: owned positions into L[0][q][slot], ring into Rg[r][rs]
+    auto load_cur = [&](auto slot_c, auto rs_c, int x) {
+      constexpr int slot = decltype(slot_c)::value, rs = decltype(rs_c)::value;
+      const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;  // always an allocated plane
+      const double* base = p.cur + static_cast<i64>(xs + 1) * P;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) L[0][q][slot] = base[gof[q] & (kOwn - 1)];
+#pragma unroll
+      for (int r = 0; r < QR; ++r) Rg[r][rs] = base[grof[r]];
+    };
+    auto load_prev = [&](auto slot_c, int x) {
+      constexpr int slot = decltype(slot_c)::value;
+      const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
+      const double* base = p.prev + static_cast<i64>(xs + 1) * P;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) Lm[q][slot] = base[gof[q] & (kOwn - 1)];
+    };
+    auto commit_cur = [&](auto slot_c, auto rs_c, int par) {
+      constexpr int slot = decltype(slot_c)::value, rs = decltype(rs_c)::value;
+      double* d = lds_plane(0, par);
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (lid[q] >= 0) d[lid[q]] = L[0][q][slot];
+#pragma unroll
+      for (int r = 0; r < QR; ++r)
+        if (lrid[r] >= 0) d[lrid[r]] = Rg[r][rs];
+    };
+
+    // stage k at plane xp; D = (xp − i0) & 3 (static), parity of xp = D & 1
+    auto stage = [&](auto kc, auto dc, int xp) {
+      constexpr int k = decltype(kc)::value, D = decltype(dc)::value;
+      constexpr int sm = (D + 3) & 3, s0 = D, sp = (D + 1) & 3;
+      const double* nb = lds_plane(k - 1, D & 1);
+      double* dst = lds_plane(k < S ? k : 0, D & 1);
+      const bool xreal = xp >= p.sx0 && xp < p.sx1 && inside(p.gx0 + xp);
+      const bool xown = xp >= x0 && xp < x1;
+      const bool chk = (p.check_mask >> (k - 1)) & 1;
+      double* outp = (k == S ? p.out2 : p.out1) + static_cast<i64>(xp + 1) * P;
+      const double sxc = (chk && xown) ? stx[xp - x0] : 0.0;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        if (!((regm[q] >> (k - 1)) & 1)) continue;
+        const int li = lid[q];
+        const double c = L[k - 1][q][s0];
+        const double lap = lap7(c, L[k - 1][q][sm], L[k - 1][q][sp], nb[li - W0], nb[li + W0], nb[li - 1], nb[li + 1],
+                                ihx2, ihy2, ihz2);
+        double o;
+        if constexpr (k == 1)
+          o = Lm[q][D & 1];
+        else
+          o = L[k - 2][q][s0];
+        const int g = gof[q];
+        const double v = (xreal && (regm[q] & kReal)) ? leapfrog(c, o, lap, tau2) : 0.0;
+        if constexpr (k < S) {
+          L[k][q][s0] = v;
+          dst[li] = v;
+        }
+        const bool own = xown && (g & kOwn);
+        if constexpr (k >= S - 1) {
+          if (own && xreal) {
+            double* qp = outp + (g & (kOwn - 1));
+            if constexpr (NTS)
+              __builtin_nontemporal_store(v, qp);
+            else
+              *qp = v;
+          }
+        }
+        if (chk && own && xreal) {
+          const int a = li / W0 - 1 - (S - 1), b = li - (li / W0) * W0 - 1 - (S - 1);  // tile coordinates
+          const double e = fabs(v - ((sxc * sty[a]) * stz[b]) * p.ct[k - 1]);
+          emax[k - 1] = e > emax[k - 1] ? e : emax[k - 1];
+          esum[k - 1] += e * e;
+        }
+      }
+    };
+
+    // iteration i with phase F = (i − i0) & 3
+    auto iteration = [&](auto fc, int i) {
+      constexpr int F = decltype(fc)::value;
+      __syncthreads();  // every read of the slots overwritten below (iteration i−1) is done; i−1's writes visible
+      commit_cur(std::integral_constant<int, (F + 1) & 3>{}, std::integral_constant<int, (F + 1) & 1>{},
+                 (F + 1) & 1);  // u^n plane i+1 → LDS (loaded one iteration ago)
+      load_cur(std::integral_constant<int, (F + 2) & 3>{}, std::integral_constant<int, (F + 2) & 1>{}, i + 2);
+      load_prev(std::integral_constant<int, (F + 1) & 1>{}, i + 1);
+#define W3D_TB_STAGE(K)                                                                                          \
+  if constexpr (K <= S) {                                                                                        \
+    const int xp = i - (K - 1);                                                                                  \
+    if (xp >= x0 - (S - K) && xp < x1 + (S - K))                                                                 \
+      stage(std::integral_constant<int, K>{}, std::integral_constant<int, (F - (K - 1) + 8) & 3>{}, xp);         \
+  }
+      W3D_TB_STAGE(1)
+      W3D_TB_STAGE(2)
+      W3D_TB_STAGE(3)
+      W3D_TB_STAGE(4)
+#undef W3D_TB_STAGE
+    };
+
+    // prologue: u^n planes i0−1, i0 (registers; plane i0 also to LDS), plane i0+1 and u^{n−1} plane i0 in flight
+    load_cur(std::integral_constant<int, 3>{}, std::integral_constant<int, 1>{}, i0 - 1);
+    load_cur(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, i0);
+    commit_cur(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0);
+    load_cur(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, i0 + 1);
+    load_prev(std::integral_constant<int, 0>{}, i0);
+    for (int ib = i0; ib <= i1; ib += 4) {
+      iteration(std::integral_constant<int, 0>{}, ib);
+      if (ib + 1 > i1) break;
+      iteration(std::integral_constant<int, 1>{}, ib + 1);
+      if (ib + 2 > i1) break;
+      iteration(std::integral_constant<int, 2>{}, ib + 2);
+      if (ib + 3 > i1) break;
+      iteration(std::integral_constant<int, 3>{}, ib + 3);
+    }
+  }
+
+  if (p.partials == nullptr) return;
+  __shared__ double red_m[NT / 64], red_s[NT / 64];
+#pragma unroll
+  for (int k = 0; k < S; ++k) {
+    if (!((p.check_mask >> k) & 1)) continue;
+    double m = emax[k], sm = esum[k];
+    wave_reduce(m, sm);
+    __syncthreads();
+    if ((tid & 63) == 0) {
+      red_m[tid >> 6] = m;
+      red_s[tid >> 6] = sm;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double mm = red_m[0], ss = red_s[0];
+      for (int w = 1; w < NT / 64; ++w) {
+        mm = red_m[w] > mm ? red_m[w] : mm;
+        ss += red_s[w];
+      }
+      p.partials[k * p.nblocks + static_cast<int>(blockIdx.x)] = make_double2(mm, ss);
+    }
+  }
+}
+
+struct TbPlan {
+  TbParams prm{};
+  int nblocks = 0;
+};
+
+TbPlan make_plan_tb(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, i64 sx0, i64 sx1) {
+  W3D_REQUIRE(t.stages >= 2 && t.stages <= 4, "leapfrog_tb: stages must be 2, 3 or 4");
+  W3D_REQUIRE(t.threads == 512 || t.threads == 1024, "leapfrog_tb: threads must be 512 or 1024");
+  const LBox full = compute_box(l);
+  // no halo exchange inside a pass: every (y,z) node of the plane must be local (slab ranks / one rank)
+  W3D_REQUIRE(l.gy0 == 0 && l.gz0 == 0 && l.ny == l.N + 1 && l.nz == l.N + 1,
+              "leapfrog_tb needs whole (y,z) planes on the rank");
+  W3D_REQUIRE(b.x0 >= full.x0 && b.x1 <= full.x1 && b.y0 >= full.y0 && b.y1 <= full.y1 && b.z0 >= full.z0 &&
+                  b.z1 <= full.z1,
+              "leapfrog_tb box outside the compute box");
+  W3D_REQUIRE(l.N < (1 << 20), "leapfrog_tb: N too large for 32-bit node indices");
+  const i64 S = t.stages;
+  // u^{n+k} (k < S) is read up to S−k planes beyond the box: its values there must be real (sx range) unless they lie
+  // beyond the global boundary (structural zeros); u^n is read S planes beyond the box, within the allocation
+  const bool lo_ok = sx0 <= b.x0 - (S - 1) || l.gx0 + sx0 <= 1;
+  const bool hi_ok = sx1 >= b.x1 + (S - 1) || l.gx0 + sx1 >= l.N;
+  W3D_REQUIRE(lo_ok && hi_ok, "leapfrog_tb: stage-1 range does not cover the box halo");
+  W3D_REQUIRE(l.gx0 + b.x0 - S <= 0 || b.x0 - S >= -l.xg, "leapfrog_tb: x halo deeper than the ghost layers");
+  W3D_REQUIRE(l.gx0 + b.x1 + S - 1 >= l.N || b.x1 + S - 1 < l.nx + l.xg, "leapfrog_tb: x halo deeper than the ghosts");
+  TbPlan pl;
+  TbParams& p = pl.prm;
+  p.plane = l.plane;
+  p.pitch = l.pitch;
+  p.zs = l.zs;
+  p.x0 = static_cast<int>(b.x0);
+  p.x1 = static_cast<int>(b.x1);
+  p.sx0 = static_cast<int>(sx0);
+  p.sx1 = static_cast<int>(sx1);
+  p.ax0 = static_cast<int>(-l.xg);
+  p.ax1 = static_cast<int>(l.nx + l.xg);
+  p.N = static_cast<int>(l.N);
+  p.gx0 = static_cast<int>(l.gx0);
+  p.gy0 = static_cast<int>(l.gy0);
+  p.gz0 = static_cast<int>(l.gz0);
+  p.y0 = static_cast<int>(b.y0);
+  p.y1 = static_cast<int>(b.y1);
+  p.z0 = static_cast<int>(b.z0);
+  p.z1 = static_cast<int>(b.z1);
+  if (b.x1 <= b.x0 || b.y1 <= b.y0 || b.z1 <= b.z0) return pl;
+  p.nty = static_cast<int>(ceil_div(b.y1 - b.y0, kTile));
+  p.ntz = static_cast<int>(ceil_div(b.z1 - b.z0, kTile));
+  const int tiles = p.nty * p.ntz;
+  pl.nblocks = t.xcd_remap ? static_cast<int>(round_up(tiles, 8)) : tiles;
+  p.nblocks = pl.nblocks;
+  p.xcd_remap = t.xcd_remap ? 1 : 0;
+  return pl;
+}
+
+template <int NT>
+constexpr size_t max_dyn_lds() {
+  return 160 * 1024 - 2 * (NT / 64) * sizeof(double);  // minus the static reduction arrays
+}
+
+// allow the dynamic LDS size once per instantiation (outside any stream capture: see leapfrog_tb_prepare)
+template <int S, int NT, bool NTS>
+void prepare_cfg() {
+  static_assert(tb_lds_bytes<S, kTile, NT>() <= max_dyn_lds<NT>(), "leapfrog_tb tile does not fit in LDS");
+  static const hipError_t attr =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(k_leapfrog_tb<S, kTile, NT, NTS>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(max_dyn_lds<NT>()));
+  if (attr != hipSuccess) fail(std::string("leapfrog_tb LDS attribute: ") + hipGetErrorString(attr));
+}
+
+template <int S, int NT, bool NTS>
+void launch_cfg(const TbParams& p, int nblocks, hipStream_t st) {
+  prepare_cfg<S, NT, NTS>();
+  const size_t shmem = tb_lds_bytes<S, kTile, NT>(p.check_mask ? p.x1 - p.x0 : 0);
+  W3D_REQUIRE(shmem <= max_dyn_lds<NT>(), "leapfrog_tb: too many owned planes for the LDS sin table");
+  hipLaunchKernelGGL((k_leapfrog_tb<S, kTile, NT, NTS>), dim3(nblocks), dim3(NT), shmem, st, p);
+}
+
+template <int S>
+void launch_s(const TbParams& p, int nblocks, const LeapfrogTbTiling& t, hipStream_t st) {
+  if (t.threads == 1024) {
+    if (t.nt_store)
+      launch_cfg<S, 1024, true>(p, nblocks, st);
+    else
+      launch_cfg<S, 1024, false>(p, nblocks, st);
+  } else {
+    if (t.nt_store)
+      launch_cfg<S, 512, true>(p, nblocks, st);
+    else
+      launch_cfg<S, 512, false>(p, nblocks, st);
+  }
+}
+
+}  // namespace
+
+void leapfrog_tb_prepare() {
+  prepare_cfg<2, 512, true>();
+  prepare_cfg<3, 512, true>();
+  prepare_cfg<4, 512, true>();
+  prepare_cfg<2, 512, false>();
+  prepare_cfg<3, 512, false>();
+  prepare_cfg<4, 512, false>();
+  prepare_cfg<2, 1024, true>();
+  prepare_cfg<3, 1024, true>();
+  prepare_cfg<4, 1024, true>();
+  prepare_cfg<2, 1024, false>();
+  prepare_cfg<3, 1024, false>();
+  prepare_cfg<4, 1024, false>();
+}
+
+size_t leapfrog_tb_lds_bytes(int stages) {
+  return stages == 2 ? tb_lds_bytes<2, kTile, 512>() : stages == 3 ? tb_lds_bytes<3, kTile, 512>()
+                                                                   : tb_lds_bytes<4, kTile, 512>();
+}
+
+int leapfrog_tb_partials(const Layout& l, const LBox& box, const LeapfrogTbTiling& t) {
+  const LBox full = compute_box(l);
+  return make_plan_tb(l, box, t, full.x0, full.x1).nblocks;
+}
+
+void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
+                        double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
+                        Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, i64 sx0, i64 sx1) {
+  W3D_REQUIRE(prev != out1 && prev != out2 && cur != out1 && cur != out2 && out1 != out2,
+              "leapfrog_tb needs four distinct buffers");
+  if (sx0 > sx1) {
+    const LBox full = compute_box(l);
+    sx0 = full.x0;
+    sx1 = full.x1;
+  }
+  TbPlan pl = make_plan_tb(l, box, t, sx0, sx1);
+  if (pl.nblocks == 0) return;
+  TbParams& p = pl.prm;
+  const i64 kb = l.kbase();
+  p.prev = prev + kb;
+  p.cur = cur + kb;
+  p.out1 = out1 + kb;
+  p.out2 = out2 + kb;
+  p.s = d_s;
+  p.ihx2 = c.ihx2;
+  p.ihy2 = c.ihy2;
+  p.ihz2 = c.ihz2;
+  p.tau2 = c.tau2;
+  p.check_mask = partials != nullptr ? (check_mask & ((1 << t.stages) - 1)) : 0;
+  p.partials = p.check_mask != 0 ? partials : nullptr;
+  for (int k = 0; k < 4; ++k) p.ct[k] = (ct != nullptr && k < t.stages) ? ct[k] : 0.0;
+  switch (t.stages) {
+    case 2: launch_s<2>(p, pl.nblocks, t, stream); break;
+    case 3: launch_s<3>(p, pl.nblocks, t, stream); break;
+    default: launch_s<4>(p, pl.nblocks, t, stream); break;
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) fail(std::string("leapfrog_tb launch: ") + hipGetErrorString(e));
+}
+
+}  // namespace wave3d

@@ -94,10 +94,11 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
               "decomposition leaves a rank without nodes; use fewer ranks or a larger N");
   // schedule mode: temporal blocking on one rank, or on a 1-D slab decomposition with 2-deep x halos
   mode_ = Mode::kSingleStep;
-  if (opt_.temporal == 2 && world == 1) mode_ = Mode::kFusedSingle;
+  W3D_REQUIRE(opt_.temporal >= 1 && opt_.temporal <= 4, "temporal must be 1..4");
+  if (opt_.temporal >= 2 && world == 1) mode_ = Mode::kFusedSingle;
   // (measured with --fake-rank on 512³: the fused pass wins from ~128 local planes up, but at 64 planes the two
   // 2-plane shell passes and the per-chunk stage-1 recompute cost more than the saved traffic)
-  if (opt_.temporal == 2 && world > 1 && dims_.py == 1 && dims_.pz == 1 && box.nx() >= opt_.deep_min_planes &&
+  if (opt_.temporal >= 2 && world > 1 && dims_.py == 1 && dims_.pz == 1 && box.nx() >= opt_.deep_min_planes &&
       box.nx() >= 3 && pairable())
     mode_ = Mode::kDeep;
   for (int attempt = 0; attempt < 2; ++attempt) {
@@ -191,6 +192,12 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   n_shell_ = leapfrog_blocks(lay_, shell_.data(), static_cast<int>(shell_.size()), opt_.tiling);
   n_int_ = leapfrog_blocks(lay_, &interior_, 1, opt_.tiling);
   n_fused_ = (mode_ == Mode::kFusedSingle && !full_.empty()) ? leapfrog2_partials(lay_, full_, opt_.tiling2) : 0;
+  if (mode_ == Mode::kFusedSingle && opt_.tb && !full_.empty()) {
+    LeapfrogTbTiling t = opt_.tiling_tb;
+    t.stages = 4;  // partials per level do not depend on the stage count
+    n_tb_ = leapfrog_tb_partials(lay_, full_, t);
+    leapfrog_tb_prepare();
+  }
   int n_deep = 0;
   for (const LBox& b : dshell_) {
     n_dshell_.push_back(leapfrog2_partials(lay_, b, opt_.tiling2));
@@ -198,7 +205,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   }
   n_dint_ = dint_.empty() ? 0 : leapfrog2_partials(lay_, dint_, opt_.tiling2);
   n_deep += n_dint_;
-  n_partials_ = std::max({n_full_, n_shell_ + n_int_, error_blocks(lay_, full_), n_fused_, n_deep,
+  n_partials_ = std::max({n_full_, n_shell_ + n_int_, error_blocks(lay_, full_), n_fused_, n_deep, 4 * n_tb_,
                           opt_.init2 ? init_two_partials(lay_) : 0, 1});
   W3D_HIP(hipMalloc(&partials_, static_cast<size_t>(n_partials_) * sizeof(Partial)));
   W3D_HIP(hipMalloc(&errlog_, static_cast<size_t>(prob_.K + 1) * sizeof(Partial)));
@@ -271,16 +278,36 @@ void GpuSolver::build_units() {
   units_.clear();
   const int K = prob_.K;
   int n = start_n_;
-  if (mode_ == Mode::kFusedSingle) {
+  if (mode_ == Mode::kFusedSingle && opt_.tb) {
+    // split the K − n remaining steps into passes of 1..temporal steps minimising the summed cost; relative per-step
+    // cost of a pass of s steps measured at 512³ (tools/tune_leapfrog.py --tb: 610, 500, 343, 321 µs per step)
+    static const double kStepCost[5] = {0.0, 1.90, 1.56, 1.07, 1.00};
+    const int rem = K - n, smax = opt_.temporal;
+    std::vector<double> best(static_cast<size_t>(rem + 1), 1e300);
+    std::vector<int> take(static_cast<size_t>(rem + 1), 1);
+    best[0] = 0.0;
+    for (int r = 1; r <= rem; ++r)
+      for (int st = 1; st <= std::min(smax, r); ++st) {
+        const double c = best[static_cast<size_t>(r - st)] + st * kStepCost[st];
+        if (c < best[static_cast<size_t>(r)]) {
+          best[static_cast<size_t>(r)] = c;
+          take[static_cast<size_t>(r)] = st;
+        }
+      }
+    for (int r = rem; r > 0; r -= take[static_cast<size_t>(r)]) {
+      units_.push_back(Unit{n, take[static_cast<size_t>(r)]});
+      n += take[static_cast<size_t>(r)];
+    }
+  } else if (mode_ == Mode::kFusedSingle) {
     while (n <= K - 1) {
       const bool f = n + 2 <= K && !is_check_[static_cast<size_t>(n + 1)];
-      units_.push_back(Unit{n, f});
+      units_.push_back(Unit{n, f ? 2 : 1});
       n += f ? 2 : 1;
     }
   } else if (mode_ == Mode::kDeep) {
-    for (; n <= K - 1; n += 2) units_.push_back(Unit{n, true});
+    for (; n <= K - 1; n += 2) units_.push_back(Unit{n, 2});
   } else {
-    for (; n <= K - 1; ++n) units_.push_back(Unit{n, false});
+    for (; n <= K - 1; ++n) units_.push_back(Unit{n, 1});
   }
 }
 
@@ -374,12 +401,12 @@ void GpuSolver::phase_init() {
 
 void GpuSolver::unit_shell(int i) {
   const Unit& u = units_[static_cast<size_t>(i)];
-  if (u.fused) {
+  if (u.fused()) {
     int k = 0;
     for (int b = 0; b < 4; ++b)
       if (b != cur_ && b != old_) uf_[k++] = b;
   }
-  const int nc = u.fused ? u.n + 2 : u.n + 1;
+  const int nc = u.n + u.steps;
   const bool chk = is_check_[static_cast<size_t>(nc)] != 0;
   if (mode_ == Mode::kDeep) {
     int off = 0;
@@ -429,7 +456,7 @@ void GpuSolver::unit_exchange_rccl(int i) {
 
 void GpuSolver::unit_interior(int i) {
   const Unit& u = units_[static_cast<size_t>(i)];
-  const int nc = u.fused ? u.n + 2 : u.n + 1;
+  const int nc = u.n + u.steps;
   const bool chk = is_check_[static_cast<size_t>(nc)] != 0;
   const double ct = ct_[static_cast<size_t>(nc)];
   const double* s = d_s_ + 1;
@@ -445,16 +472,37 @@ void GpuSolver::unit_interior(int i) {
       });
     }
     np = off + n_dint_;
+  } else if (mode_ == Mode::kFusedSingle && opt_.tb && u.fused()) {
+    // S steps in one LDS pass; every checked level has its own block of partials
+    LeapfrogTbTiling t = opt_.tiling_tb;
+    t.stages = u.steps;
+    double cts[4] = {0, 0, 0, 0};
+    int mask = 0;
+    for (int k = 1; k <= u.steps; ++k) {
+      cts[k - 1] = ct_[static_cast<size_t>(u.n + k)];
+      if (is_check_[static_cast<size_t>(u.n + k)]) mask |= 1 << (k - 1);
+    }
+    timed(kPhaseCompute, s0_, [&] {
+      launch_leapfrog_tb(lay_, coef_, u_[old_], u_[cur_], u_[uf_[0]], u_[uf_[1]], full_, s, cts, mask,
+                         mask ? partials_ : nullptr, t, s0_);
+    });
+    if (mask) {
+      timed(kPhaseCheck, s0_, [&] {
+        for (int k = 1; k <= u.steps; ++k)
+          if (mask >> (k - 1) & 1)
+            launch_reduce(partials_ + (k - 1) * n_tb_, n_tb_, errlog_ + u.n + k, s0_);
+      });
+    }
   } else if (mode_ == Mode::kFusedSingle) {
     timed(kPhaseCompute, s0_, [&] {
-      if (u.fused)
+      if (u.fused())
         launch_leapfrog2(lay_, coef_, u_[old_], u_[cur_], u_[uf_[0]], u_[uf_[1]], full_, s, ct,
                          chk ? partials_ : nullptr, opt_.tiling2, s0_);
       else
         launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &full_, 1, s, ct, chk ? partials_ : nullptr, opt_.tiling,
                         s0_);
     });
-    np = u.fused ? n_fused_ : n_full_;
+    np = u.fused() ? n_fused_ : n_full_;
   } else if (split()) {
     timed(kPhaseCompute, s0_, [&] {
       launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], &interior_, 1, s, ct, chk ? partials_ + n_shell_ : nullptr,
@@ -469,9 +517,9 @@ void GpuSolver::unit_interior(int i) {
     np = n_full_;
   }
   if (wait) W3D_HIP(hipStreamWaitEvent(s0_, ev_halo_, 0));
-  if (chk) timed(kPhaseCheck, s0_, [&] { launch_reduce(partials_, np, errlog_ + nc, s0_); });
+  if (chk && np > 0) timed(kPhaseCheck, s0_, [&] { launch_reduce(partials_, np, errlog_ + nc, s0_); });
   if (opt_.debug_sync) W3D_HIP(hipDeviceSynchronize());
-  if (u.fused) {
+  if (u.fused()) {
     old_ = uf_[0];
     cur_ = uf_[1];
   } else {

@@ -38,6 +38,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-temporal", action="store_true")
+    ap.add_argument("--temporal", type=int, default=4, help="at most this many steps per HBM pass (2..4)")
+    ap.add_argument("--no-tb", action="store_true", help="two-step register-queue passes instead of the LDS kernel")
     ap.add_argument("--timers", action="store_true")
     ap.add_argument("--json", default="")
     ap.add_argument("--dump", default="", help="write u^K to PREFIX[.rankR].bin/.json")
@@ -73,7 +75,7 @@ def main(argv=None) -> int:
     if a.resume:
         transport = "torch"
     kw = dict(backend=backend, transport=transport, decomp=a.decomp, overlap=not a.no_overlap,
-              graph=not a.no_graph, threads=a.threads, force=a.force, temporal=1 if a.no_temporal else 2)
+              graph=not a.no_graph, threads=a.threads, force=a.force, temporal=1 if a.no_temporal else a.temporal, tb=not a.no_tb)
     if backend == "hip":
         kw["device"] = local if a.world == 0 else 0
         kw["timers"] = a.timers

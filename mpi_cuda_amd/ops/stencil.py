@@ -108,6 +108,33 @@ def leapfrog2(layout, coeffs, prev: torch.Tensor, cur: torch.Tensor, out1: torch
     return float(o[0]), float(o[1])
 
 
+def leapfrog_tb(layout, coeffs, prev: torch.Tensor, cur: torch.Tensor, out1: torch.Tensor, out2: torch.Tensor, box,
+                s_ext: torch.Tensor, stages: int = 4, ct=None, check_mask: int = 0, threads: int = 512):
+    """``stages`` fused leapfrog steps held in LDS (HIP only): out1 = u^{n+S-1}, out2 = u^{n+S}.
+
+    ``ct[k-1]`` is the time factor of u^{n+k}; for every bit k-1 set in ``check_mask`` the (L∞, Σe²) error of u^{n+k}
+    is returned in a dict {k: (max, sumsq)}."""
+    C = _C()
+    if not cur.is_cuda:
+        raise ValueError("leapfrog_tb is a GPU kernel; on the CPU take single leapfrog() steps")
+    t = C.LeapfrogTbTiling()
+    t.stages = stages
+    t.threads = threads
+    nb = C.gpu_leapfrog_tb_partials(layout, box, t)
+    ct = list(ct) if ct is not None else [0.0] * stages
+    part = torch.empty((stages * max(nb, 1), 2), dtype=torch.float64, device=cur.device) if check_mask else None
+    C.gpu_leapfrog_tb(layout, coeffs, prev.data_ptr(), cur.data_ptr(), out1.data_ptr(), out2.data_ptr(), box,
+                      s_ext.data_ptr(), ct, check_mask, part.data_ptr() if check_mask else 0, t, _stream())
+    res = {}
+    for k in range(1, stages + 1):
+        if check_mask >> (k - 1) & 1:
+            out = torch.empty(2, dtype=torch.float64, device=cur.device)
+            C.gpu_reduce(part[(k - 1) * nb:].data_ptr(), nb, out.data_ptr(), _stream())
+            o = out.cpu()
+            res[k] = (float(o[0]), float(o[1]))
+    return res
+
+
 def error(layout, u: torch.Tensor, box, s_ext: torch.Tensor, ct: float):
     C = _C()
     if u.is_cuda:

@@ -72,8 +72,9 @@ class Solver:
     def __init__(self, spec: ProblemSpec, backend: str = "auto", transport: str = "auto", decomp: str = "slab",
                  rank: int | None = None, world: int | None = None, device: int | None = None,
                  overlap: bool = True, graph: bool = True, threads: int = 0, tiling: dict | None = None,
-                 comm=None, group=None, stage_via_host: bool = False, force: bool = False, temporal: int = 2,
-                 tiling2: dict | None = None, init2: bool = True, timers: bool = False,
+                 comm=None, group=None, stage_via_host: bool = False, force: bool = False, temporal: int = 4,
+                 tiling2: dict | None = None, init2: bool = True, timers: bool = False, tb: bool = True,
+                 tiling_tb: dict | None = None,
                  debug_sync: bool = False, poison_ghosts: bool = False, deep_min_planes: int | None = None):
         import torch.distributed as dist
 
@@ -100,7 +101,7 @@ class Solver:
         else:
             self.device = torch.device("cpu")
         if self.backend == "hip" and self.transport == "loopback":
-            opts = self._options(C, decomp, spec, overlap, False, tiling, temporal, tiling2, init2)
+            opts = self._options(C, decomp, spec, overlap, False, tiling, temporal, tiling2, init2, tb, tiling_tb)
             opts.timers, opts.debug_sync, opts.poison_ghosts = timers, debug_sync, poison_ghosts
             if deep_min_planes is not None:
                 opts.deep_min_planes = deep_min_planes
@@ -109,7 +110,7 @@ class Solver:
         elif self.backend == "hip" and self.transport == "rccl":
             from .parallel.rccl import make_comm
 
-            opts = self._options(C, decomp, spec, overlap, graph, tiling, temporal, tiling2, init2)
+            opts = self._options(C, decomp, spec, overlap, graph, tiling, temporal, tiling2, init2, tb, tiling_tb)
             opts.timers, opts.debug_sync, opts.poison_ghosts = timers, debug_sync, poison_ghosts
             if deep_min_planes is not None:
                 opts.deep_min_planes = deep_min_planes
@@ -130,13 +131,18 @@ class Solver:
             self.dims = (1, 1, 1)
 
     @staticmethod
-    def _options(C, decomp, spec, overlap, graph, tiling, temporal=2, tiling2=None, init2=True):
+    def _options(C, decomp, spec, overlap, graph, tiling, temporal=4, tiling2=None, init2=True, tb=True,
+                 tiling_tb=None):
         opts = C.SolverOptions()
         opts.temporal = temporal
         opts.init2 = init2
+        opts.tb = tb
         if tiling2:
             for k, v in tiling2.items():
                 setattr(opts.tiling2, k, v)
+        if tiling_tb:
+            for k, v in tiling_tb.items():
+                setattr(opts.tiling_tb, k, v)
         opts.decomp = decomp
         opts.check_every = spec.check_every
         opts.overlap = overlap

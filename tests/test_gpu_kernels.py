@@ -160,6 +160,42 @@ def test_leapfrog2_equals_two_single_steps(gpu, rows, N, target_waves):
     assert e_gpu[0] == e_cpu[0] and math.isclose(e_gpu[1], e_cpu[1], rel_tol=1e-12)
 
 
+@pytest.mark.parametrize("stages", [2, 3, 4])
+@pytest.mark.parametrize("N", [40, 77, 130])
+@pytest.mark.parametrize("threads", [512, 1024])
+def test_leapfrog_tb_equals_single_steps(gpu, stages, N, threads):
+    """Deep temporal blocking: one LDS pass of S steps == S CPU steps, bit for bit, with every level checked."""
+    C = gpu
+    prob, co, lay, _ = _setup(C, N)
+    box = C.compute_box(lay)
+    torch.manual_seed(N * 11 + stages)
+
+    def rand_field():
+        g = torch.zeros((int(lay.nx) + 2, int(lay.ny) + 2, int(lay.nz) + 2), dtype=torch.float64)
+        g[2:-2, 2:-2, 2:-2] = torch.randn(int(lay.nx) - 2, int(lay.ny) - 2, int(lay.nz) - 2, dtype=torch.float64)
+        return ops.from_grid(lay, g)
+
+    prev, cur = rand_field(), rand_field()
+    s = ops.sin_table_ext(prob)
+    ct = [math.cos(prob.a_t * (5 + k) * prob.tau) for k in range(1, stages + 1)]
+    a, b = prev.clone(), cur.clone()
+    e_cpu = {}
+    for k in range(1, stages + 1):  # u^{n+k} in place over u^{n+k-2}
+        e_cpu[k] = ops.leapfrog(lay, co, b, a, [box], s, ct[k - 1], check=True)
+        a, b = b, a
+    # now b = u^{n+S}, a = u^{n+S-1}
+    o1 = torch.zeros(int(lay.total), dtype=torch.float64, device="cuda")
+    o2 = torch.zeros_like(o1)
+    mask = (1 << stages) - 1
+    e_gpu = ops.leapfrog_tb(lay, co, prev.cuda(), cur.cuda(), o1, o2, box, s.cuda(), stages, ct, mask, threads)
+    torch.cuda.synchronize()
+    assert torch.equal(ops.to_grid(lay, o1.cpu()), ops.to_grid(lay, a))
+    assert torch.equal(ops.to_grid(lay, o2.cpu()), ops.to_grid(lay, b))
+    for k in range(1, stages + 1):
+        assert e_gpu[k][0] == e_cpu[k][0]
+        assert math.isclose(e_gpu[k][1], e_cpu[k][1], rel_tol=1e-12)
+
+
 @pytest.mark.parametrize("N,world,rank,decomp", [(36, 1, 0, "slab"), (53, 1, 0, "slab"), (40, 2, 1, "slab"),
                                                  (45, 8, 5, "2x2x2"), (38, 6, 2, "1x2x3")])
 @pytest.mark.parametrize("check", [False, True])

@@ -69,11 +69,14 @@ def test_tilings_agree(gpu, tiling):
     assert torch.equal(a.owned_field(0), b.owned_field(0))
 
 
-@pytest.mark.parametrize("N,K,ce", [(64, 20, 2), (65, 9, 3), (50, 7, 0), (48, 6, 1)])
-def test_temporal_blocking_identical(gpu, N, K, ce):
+@pytest.mark.parametrize("N,K,ce", [(64, 20, 2), (65, 9, 3), (50, 7, 0), (48, 6, 1), (70, 13, 1)])
+@pytest.mark.parametrize("temporal,tb", [(2, False), (2, True), (3, True), (4, True)])
+def test_temporal_blocking_identical(gpu, N, K, ce, temporal, tb):
+    """Every temporal-blocking schedule (two-step register kernel, 2..4-step LDS kernel with checks at any level)
+    reproduces the single-step solve bit for bit."""
     spec = ProblemSpec(N=N, tau=1e-3, K=K, check_every=ce)
     a = Solver(spec, backend="hip", device=0, temporal=1)
-    b = Solver(spec, backend="hip", device=0, temporal=2)
+    b = Solver(spec, backend="hip", device=0, temporal=temporal, tb=tb)
     ra, rb = a.run(), b.run()
     assert ra.steps == rb.steps and ra.max_err == rb.max_err
     for x, y in zip(ra.rms_err, rb.rms_err):
@@ -84,7 +87,7 @@ def test_temporal_blocking_identical(gpu, N, K, ce):
     assert rb2.max_err == rb.max_err
 
 
-@pytest.mark.parametrize("temporal", [1, 2])
+@pytest.mark.parametrize("temporal", [1, 2, 4])
 @pytest.mark.parametrize("N,K,ce", [(60, 12, 2), (45, 2, 1), (50, 5, 1), (33, 1, 2)])
 def test_init2_identical(gpu, temporal, N, K, ce):
     spec = ProblemSpec(N=N, tau=1e-3, K=K, check_every=ce)

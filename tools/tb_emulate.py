@@ -1,0 +1,128 @@
+"""Host emulation of k_leapfrog_tb (csrc/src/kernels_leapfrog_tb.hip): same tiling, rings, stage schedule, masks and
+global offsets, executed workgroup by workgroup with numpy, with every global and LDS index bounds-checked.
+
+Used by tests/test_tb_emulate.py (CPU) to validate the algorithm and its address arithmetic bit-exactly against the
+native CPU leapfrog before the kernel runs on a GPU, where an out-of-range access faults the device.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+T = 32  # tile edge (kTile)
+
+
+class Geom:
+    def __init__(self, S: int):
+        self.S = S
+
+    def halo(self, j):
+        return self.S - 1 if j < 0 else self.S - j
+
+    def W(self, j):
+        return T + 2 * self.halo(j)
+
+
+def lap7(c, xm, xp, ym, yp, zm, zp, ihx2, ihy2, ihz2):
+    c2 = 2.0 * c
+    return (xp - c2 + xm) * ihx2 + (yp - c2 + ym) * ihy2 + (zp - c2 + zm) * ihz2
+
+
+def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2: np.ndarray, box, s_ext: np.ndarray,
+             S: int, sx, ct=None, check_mask: int = 0):
+    """Emulate one launch. Arrays are the flat padded fields (layout.total doubles); s_ext is the extended sin table
+    (element g+1 ↔ global g). Returns {k: (max, sumsq)} for checked stages (per-tile partials combined in order)."""
+    G = Geom(S)
+    N = int(lay.N)
+    P, R, zs, xg = int(lay.plane), int(lay.pitch), int(lay.zs), int(lay.xg)
+    gx0, gy0, gz0 = int(lay.gx0), int(lay.gy0), int(lay.gz0)
+    total = int(lay.total)
+    kb = (xg - 1) * P
+    x0, x1, y0, y1, z0, z1 = int(box.x0), int(box.x1), int(box.y0), int(box.y1), int(box.z0), int(box.z1)
+    sx0, sx1 = sx  # the kernel's default is the rank's compute-box x range
+    ax0, ax1 = -xg, int(lay.nx) + xg
+    ihx2, ihy2, ihz2, tau2 = co.ihx2, co.ihy2, co.ihz2, co.tau2
+    ct = list(ct) if ct is not None else [0.0] * S
+
+    def inside(g):
+        return (g >= 1) & (g <= N - 1)
+
+    def goff(x, y, z):
+        o = kb + (x + 1) * P + (y + 1) * R + (z + 1 + zs)
+        if np.any(o < 0) or np.any(o >= total):
+            raise IndexError(f"global offset out of range at x={x}")
+        return o
+
+    def sget(g):
+        g = np.asarray(g)
+        if np.any(g < -1) or np.any(g > N + 1):
+            raise IndexError(f"sin table index out of range: {g.min()}..{g.max()}")
+        return s_ext[g + 1]
+
+    nty, ntz = -(-(y1 - y0) // T), -(-(z1 - z0) // T)
+    errs = {k: [0.0, 0.0] for k in range(1, S + 1) if check_mask >> (k - 1) & 1}
+    for tyi in range(nty):
+        for tzi in range(ntz):
+            ty0, tz0 = y0 + tyi * T, z0 + tzi * T
+            ring = {j: [np.zeros((G.W(j), G.W(j))) for _ in range(1 if j < 0 else 3)] for j in range(-1, S)}
+            emax = [0.0] * S
+            esum = [0.0] * S
+
+            def fetch(j, src, x):
+                h, w = G.halo(j), G.W(j)
+                a = np.arange(w)
+                y = ty0 - h + a[:, None] + 0 * a[None, :]
+                z = tz0 - h + a[None, :] + 0 * a[:, None]
+                v = np.zeros((w, w))
+                if ax0 <= x < ax1 and 1 <= gx0 + x <= N - 1:
+                    m = inside(gy0 + y) & inside(gz0 + z)
+                    v[m] = src[goff(x, y[m], z[m])]
+                return v
+
+            def commit(x):
+                ring[0][x % 3] = fetch(0, cur, x)
+                ring[-1][0] = fetch(-1, prev, x - 1)
+
+            def stage(k, xp):
+                hk, wk = G.halo(k), G.W(k)
+                di = G.halo(k - 1) - hk
+                dd = G.halo(k - 2) - hk
+                im, ic, ip = (ring[k - 1][(xp - 1) % 3], ring[k - 1][xp % 3], ring[k - 1][(xp + 1) % 3])
+                od = ring[-1][0] if k == 1 else ring[k - 2][xp % 3]
+                wi = G.W(k - 1)
+                assert wi == wk + 2 * di and di == 1
+                sl = slice(di, di + wk)
+                c = ic[sl, sl]
+                lap = lap7(c, im[sl, sl], ip[sl, sl], ic[di - 1: di - 1 + wk, sl], ic[di + 1: di + 1 + wk, sl],
+                           ic[sl, di - 1: di - 1 + wk], ic[sl, di + 1: di + 1 + wk], ihx2, ihy2, ihz2)
+                o = od[dd: dd + wk, dd: dd + wk]
+                a = np.arange(wk)
+                y = ty0 - hk + a[:, None] + 0 * a[None, :]
+                z = tz0 - hk + a[None, :] + 0 * a[:, None]
+                xreal = sx0 <= xp < sx1 and 1 <= gx0 + xp <= N - 1
+                real = xreal & inside(gy0 + y) & inside(gz0 + z)
+                v = np.where(real, (2.0 * c - o) + tau2 * lap, 0.0)
+                if k < S:
+                    ring[k][xp % 3] = v
+                xown = x0 <= xp < x1
+                aa, bb = a[:, None] + 0 * a[None, :], a[None, :] + 0 * a[:, None]
+                own = real & xown & (aa >= hk) & (aa < hk + T) & (bb >= hk) & (bb < hk + T) & (y < y1) & (z < z1)
+                if k >= S - 1 and own.any():
+                    (out2 if k == S else out1)[goff(xp, y[own], z[own])] = v[own]
+                if k in errs and own.any():
+                    e = np.abs(v[own] - ((sget(gx0 + xp) * sget(gy0 + y[own])) * sget(gz0 + z[own])) * ct[k - 1])
+                    emax[k - 1] = max(emax[k - 1], float(e.max()))
+                    esum[k - 1] += float((e * e).sum())
+
+            i0, i1 = x0 - S + 1, x1 + S - 2
+            commit(i0 - 1)
+            commit(i0)
+            for i in range(i0, i1 + 1):
+                commit(i + 1)
+                for k in range(1, S + 1):
+                    xp = i - (k - 1)
+                    if x0 - (S - k) <= xp < x1 + (S - k):
+                        stage(k, xp)
+            for k in errs:
+                errs[k][0] = max(errs[k][0], emax[k - 1])
+                errs[k][1] += esum[k - 1]
+    return {k: tuple(v) for k, v in errs.items()}

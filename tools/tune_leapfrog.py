@@ -44,6 +44,8 @@ def main() -> int:
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--minimal", action="store_true", help="only the default single-step and two-step kernels "
                     "(for counter collection under rocprofv3)")
+    ap.add_argument("--tb", action="store_true", help="only the deep temporal-blocking kernel (k_leapfrog_tb) sweep "
+                    "plus the default two-step kernel")
     a = ap.parse_args()
     import torch
 
@@ -84,6 +86,8 @@ def main() -> int:
         configs = [c for c in configs if c["target_blocks"] == 0 and c["xcd_remap"]]
     if a.minimal:
         configs = [dict(variant=1, rows=2, target_blocks=0, xcd_remap=True, nt_store=True)]
+    if a.tb:
+        configs = []
     for cfg, chk in itertools.product(configs, [False, True] if not (a.quick or a.minimal) else [False]):
         tl = C.LeapfrogTiling()
         for k, v in cfg.items():
@@ -103,8 +107,8 @@ def main() -> int:
     bufs = [ops.alloc_field(lay, "cuda") for _ in range(2)]
     sweep2 = list(itertools.product([1, 2, 4], [0, 4096, 8192, 16384], [True, False],
                                     [False, True] if not a.quick else [False]))
-    if a.minimal:
-        sweep2 = [(1, 0, True, False), (2, 0, True, False)]
+    if a.minimal or a.tb:
+        sweep2 = [(2, 0, True, False)]
     for rows, tw, nt, chk in sweep2:
         t2 = C.Leapfrog2Tiling()
         t2.rows, t2.target_waves, t2.nt_store = rows, tw, nt
@@ -119,12 +123,36 @@ def main() -> int:
         t = timeit(pass2, a.iters)
         out.append({"kernel": "k_leapfrog2", "rows": rows, "target_waves": tw, "nt_store": nt, "partials": nb,
                     "check": chk, "us": t, "us_per_step": t / 2, "TBps": 32 * nodes / t / 1e6})
+    # deep temporal blocking: S steps per pass, 32 B per node per pass
+    sweep_tb = list(itertools.product([2, 3, 4], [512, 1024], [True, False], [False, True]))
+    if a.minimal:
+        sweep_tb = [(4, 1024, True, False)]
+    if a.quick:
+        sweep_tb = [c for c in sweep_tb if c[2] and not c[3]]
+    for stages, threads, nt, chk in sweep_tb:
+        tt = C.LeapfrogTbTiling()
+        tt.stages, tt.threads, tt.nt_store = stages, threads, nt
+        nb = C.gpu_leapfrog_tb_partials(lay, box, tt)
+        part = torch.empty((stages * nb, 2), dtype=torch.float64, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+        mask = (1 << stages) - 1 if chk else 0
+
+        def pass_tb():
+            C.gpu_leapfrog_tb(lay, co, u0.data_ptr(), u1.data_ptr(), bufs[0].data_ptr(), bufs[1].data_ptr(), box,
+                              s.data_ptr(), [0.5] * stages, mask, part.data_ptr() if chk else 0, tt, st)
+
+        t = timeit(pass_tb, a.iters)
+        out.append({"kernel": "k_leapfrog_tb", "stages": stages, "threads": threads, "nt_store": nt, "partials": nb,
+                    "check": chk, "us": t, "us_per_step": t / stages, "TBps": 32 * nodes / t / 1e6})
     for r in out:
         print(json.dumps(r), flush=True)
-    best = min((r for r in out if r["kernel"] == "k_leapfrog"), key=lambda r: r["us"])
-    print("BEST", json.dumps(best))
+    if any(r["kernel"] == "k_leapfrog" for r in out):
+        best = min((r for r in out if r["kernel"] == "k_leapfrog"), key=lambda r: r["us"])
+        print("BEST", json.dumps(best))
     best2 = min((r for r in out if r["kernel"] == "k_leapfrog2"), key=lambda r: r["us"])
     print("BEST2", json.dumps(best2))
+    best_tb = min((r for r in out if r["kernel"] == "k_leapfrog_tb"), key=lambda r: r["us_per_step"])
+    print("BEST_TB", json.dumps(best_tb))
     if a.json:
         with open(a.json, "w") as f:
             json.dump(out, f, indent=1)

@@ -72,8 +72,11 @@ struct TbGeom {
   static constexpr int W0 = T + 2 * S;          // u^n region edge = LDS plane edge (all levels share the indexing)
   static constexpr int PL = W0 * W0;
   static constexpr int NR = PL - NP;            // u^n halo ring (not thread-owned)
+  // plane stride in LDS: the plane plus a pad holding a dummy node (and its 4 neighbours) for lanes without a position
+  static constexpr int PLP = PL + 2 * W0 + 2;
+  static constexpr int DUMMY = PL + W0 + 1;
   static constexpr int QR = (NR + NT - 1) / NT;
-  static constexpr int lds_doubles() { return S * 2 * PL; }  // levels 0..S−1 × 2 parity slots
+  static constexpr int lds_doubles() { return S * 2 * PLP; }  // levels 0..S−1 × 2 parity slots
 };
 
 // + the sin factors of the tile (y, z) and of the owned planes (x) for the error check: a global load of the per-plane
@@ -86,9 +89,9 @@ constexpr size_t tb_lds_bytes(int nxo = 0) {
 template <int S, int T, int NT, bool NTS>
 __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
   using G = TbGeom<S, T, NT>;
-  constexpr int Q = G::Q, QR = G::QR, H1 = G::H1, W0 = G::W0, PL = G::PL;
+  constexpr int Q = G::Q, QR = G::QR, H1 = G::H1, W0 = G::W0, PLP = G::PLP;
   constexpr int kOwn = 1 << 30;  // gof flag: tile node inside the output box
-  constexpr int kReal = 1 << 8;  // regm flag: node inside the global interior
+  constexpr int kReal = 1;        // flags: node inside the global interior
   extern __shared__ double lds[];
   const int tid = static_cast<int>(threadIdx.x);
   int blk = static_cast<int>(blockIdx.x);
@@ -110,9 +113,9 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     // ---- per-thread descriptors of the owned positions (stage-1 region coordinates a, b ∈ [0, H1))
     // zero node: (y, z) = (0, 0), a global boundary node for whole-plane ranks (gy0 = gz0 = 0)
     const int zero_off = R + zs1;
-    int lid[Q];   // LDS index (u^n-region coordinates a+1, b+1), −1: no position
+    int lid[Q];   // LDS index (u^n-region coordinates a+1, b+1); the pad's dummy node for lanes without a position
     int gof[Q];   // in-plane offset to load (zero node outside the interior) | kOwn
-    int regm[Q];  // bit k−1: inside stage k's region (halo S−k); kReal
+    int flags[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const int idx = tid + q * NT;
@@ -121,15 +124,11 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       const bool valid = idx < G::NP;
       const bool real = valid && inside(p.gy0 + y) && inside(p.gz0 + z);
       const bool own = real && a >= S - 1 && a < S - 1 + T && b >= S - 1 && b < S - 1 + T && y < p.y1 && z < p.z1;
-      lid[q] = valid ? (a + 1) * W0 + (b + 1) : -1;
+      lid[q] = valid ? (a + 1) * W0 + (b + 1) : G::DUMMY;
       gof[q] = real ? (((y + 1) * R + z + zs1) | (own ? kOwn : 0)) : zero_off;
-      int m = real ? kReal : 0;
-#pragma unroll
-      for (int k = 1; k <= S; ++k)
-        if (valid && a >= k - 1 && a < H1 - (k - 1) && b >= k - 1 && b < H1 - (k - 1)) m |= 1 << (k - 1);
-      regm[q] = m;
+      flags[q] = real ? kReal : 0;
     }
-    // u^n halo ring: LDS index and global offset (−1: outside the interior; lrid −1: no ring node)
+    // u^n halo ring: LDS index (dummy: no ring node) and global offset (zero node outside the interior)
     int lrid[QR], grof[QR];
 #pragma unroll
     for (int r = 0; r < QR; ++r) {
@@ -148,7 +147,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       }
       const int y = ty0 - S + a0, z = tz0 - S + b0;
       const bool valid = ridx < G::NR;
-      lrid[r] = valid ? a0 * W0 + b0 : -1;
+      lrid[r] = valid ? a0 * W0 + b0 : G::DUMMY;
       grof[r] = (valid && inside(p.gy0 + y) && inside(p.gz0 + z)) ? (y + 1) * R + z + zs1 : zero_off;
     }
     // sin factors for the check: y and z of the tile, x of the owned planes (clamped into −1..N+1; only owned nodes,
@@ -166,12 +165,15 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     }
 
     // ---- register queues: plane x of level j at slot (x − i0) & 3; u^{n−1} and the ring: slot (x − i0) & 1
-    double L[S][Q][4];  // L[0] = u^n, L[k] = u^{n+k} (k < S)
-    double Lm[Q][2];    // u^{n−1}
-    double Rg[QR][2];   // u^n ring
+    // Stages also run on the positions outside their (shrinking) region: those values are never read by a node
+    // inside the region (its neighbours lie in the previous stage's region), and skipping them per lane costs more
+    // exec-mask branching than the arithmetic. Zero-initialised so every value is defined.
+    double L[S][Q][4] = {};  // L[0] = u^n, L[k] = u^{n+k} (k < S)
+    double Lm[Q][2] = {};    // u^{n−1}
+    double Rg[QR][2] = {};   // u^n ring
     const int x0 = p.x0, x1 = p.x1;
     const int i0 = x0 - S + 1, i1 = x1 + S - 2;
-    auto lds_plane = [&](int j, int par) { return lds + (j * 2 + par) * PL; };
+    auto lds_plane = [&](int j, int par) { return lds + (j * 2 + par) * PLP; };
 
     // plane x of u^n: owned positions into L[0][q][slot], ring into Rg[r][rs]
     auto load_cur = [&](auto slot_c, auto rs_c, int x) {
@@ -194,11 +196,9 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       constexpr int slot = decltype(slot_c)::value, rs = decltype(rs_c)::value;
       double* d = lds_plane(0, par);
 #pragma unroll
-      for (int q = 0; q < Q; ++q)
-        if (lid[q] >= 0) d[lid[q]] = L[0][q][slot];
+      for (int q = 0; q < Q; ++q) d[lid[q]] = L[0][q][slot];
 #pragma unroll
-      for (int r = 0; r < QR; ++r)
-        if (lrid[r] >= 0) d[lrid[r]] = Rg[r][rs];
+      for (int r = 0; r < QR; ++r) d[lrid[r]] = Rg[r][rs];
     };
 
     // stage k at plane xp; D = (xp − i0) & 3 (static), parity of xp = D & 1
@@ -214,7 +214,6 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       const double sxc = (chk && xown) ? stx[xp - x0] : 0.0;
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
-        if (!((regm[q] >> (k - 1)) & 1)) continue;
         const int li = lid[q];
         const double c = L[k - 1][q][s0];
         const double lap = lap7(c, L[k - 1][q][sm], L[k - 1][q][sp], nb[li - W0], nb[li + W0], nb[li - 1], nb[li + 1],
@@ -225,7 +224,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         else
           o = L[k - 2][q][s0];
         const int g = gof[q];
-        const double v = (xreal && (regm[q] & kReal)) ? leapfrog(c, o, lap, tau2) : 0.0;
+        const double v = (xreal && (flags[q] & kReal)) ? leapfrog(c, o, lap, tau2) : 0.0;
         if constexpr (k < S) {
           L[k][q][s0] = v;
           dst[li] = v;

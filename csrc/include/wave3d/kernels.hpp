@@ -76,8 +76,7 @@ void launch_leapfrog2(const Layout& l, const Coeffs& c, const double* prev, cons
 struct LeapfrogTbTiling {
   int stages = 4;         // 2, 3 or 4 steps per pass
   int threads = 1024;     // workgroup size (512 or 1024; 1024 measured faster at every S)
-  bool xcd_remap = true;
-  bool nt_store = true;
+  bool xcd_remap = true;  // (stores are always non-temporal: measured faster at every S)
 };
 // Raise the dynamic-LDS limit of every instantiation (call before capturing launches into a graph).
 void leapfrog_tb_prepare();

@@ -86,12 +86,15 @@ constexpr size_t tb_lds_bytes(int nxo = 0) {
   return (static_cast<size_t>(TbGeom<S, T, NT>::lds_doubles()) + 2 * T + static_cast<size_t>(nxo)) * sizeof(double);
 }
 
-template <int S, int T, int NT, bool NTS>
+// CM: compile-time superset of the levels that may be checked (bit k−1 ↔ u^{n+k}); levels outside it carry no error
+// accumulators or check code (registers: the S = 4 kernel sits at the 128-VGPR limit of 4 waves per SIMD)
+template <int S, int T, int NT, int CM>
 __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
   using G = TbGeom<S, T, NT>;
   constexpr int Q = G::Q, QR = G::QR, H1 = G::H1, W0 = G::W0, PLP = G::PLP;
-  constexpr int kOwn = 1 << 30;  // gof flag: tile node inside the output box
-  constexpr int kReal = 1;        // flags: node inside the global interior
+  constexpr int kOwn = 1 << 30;   // gof flag: tile node inside the output box
+  constexpr int kReal = 1 << 29;  // gof flag: node inside the global interior
+  constexpr int kOff = kReal - 1;  // gof bits of the in-plane offset
   extern __shared__ double lds[];
   const int tid = static_cast<int>(threadIdx.x);
   int blk = static_cast<int>(blockIdx.x);
@@ -114,8 +117,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     // zero node: (y, z) = (0, 0), a global boundary node for whole-plane ranks (gy0 = gz0 = 0)
     const int zero_off = R + zs1;
     int lid[Q];   // LDS index (u^n-region coordinates a+1, b+1); the pad's dummy node for lanes without a position
-    int gof[Q];   // in-plane offset to load (zero node outside the interior) | kOwn
-    int flags[Q];
+    int gof[Q];   // in-plane offset to load (zero node outside the interior) | kReal | kOwn
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const int idx = tid + q * NT;
@@ -125,8 +127,8 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       const bool real = valid && inside(p.gy0 + y) && inside(p.gz0 + z);
       const bool own = real && a >= S - 1 && a < S - 1 + T && b >= S - 1 && b < S - 1 + T && y < p.y1 && z < p.z1;
       lid[q] = valid ? (a + 1) * W0 + (b + 1) : G::DUMMY;
-      gof[q] = real ? (((y + 1) * R + z + zs1) | (own ? kOwn : 0)) : zero_off;
-      flags[q] = real ? kReal : 0;
+      gof[q] = real ? (((y + 1) * R + z + zs1) | kReal | (own ? kOwn : 0)) : zero_off;
+
     }
     // u^n halo ring: LDS index (dummy: no ring node) and global offset (zero node outside the interior)
     int lrid[QR], grof[QR];
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;  // always an allocated plane
       const double* base = p.cur + static_cast<i64>(xs + 1) * P;
 #pragma unroll
-      for (int q = 0; q < Q; ++q) L[0][q][slot] = base[gof[q] & (kOwn - 1)];
+      for (int q = 0; q < Q; ++q) L[0][q][slot] = base[gof[q] & kOff];
 #pragma unroll
       for (int r = 0; r < QR; ++r) Rg[r][rs] = base[grof[r]];
     };
@@ -190,7 +192,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
       const double* base = p.prev + static_cast<i64>(xs + 1) * P;
 #pragma unroll
-      for (int q = 0; q < Q; ++q) Lm[q][slot] = base[gof[q] & (kOwn - 1)];
+      for (int q = 0; q < Q; ++q) Lm[q][slot] = base[gof[q] & kOff];
     };
     auto commit_cur = [&](auto slot_c, auto rs_c, int par) {
       constexpr int slot = decltype(slot_c)::value, rs = decltype(rs_c)::value;
@@ -209,7 +211,8 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       double* dst = lds_plane(k < S ? k : 0, D & 1);
       const bool xreal = xp >= p.sx0 && xp < p.sx1 && inside(p.gx0 + xp);
       const bool xown = xp >= x0 && xp < x1;
-      const bool chk = (p.check_mask >> (k - 1)) & 1;
+      constexpr bool kChk = (CM >> (k - 1)) & 1;
+      const bool chk = kChk && ((p.check_mask >> (k - 1)) & 1);
       double* outp = (k == S ? p.out2 : p.out1) + static_cast<i64>(xp + 1) * P;
       const double sxc = (chk && xown) ? stx[xp - x0] : 0.0;
 #pragma unroll
@@ -224,7 +227,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         else
           o = L[k - 2][q][s0];
         const int g = gof[q];
-        const double v = (xreal && (flags[q] & kReal)) ? leapfrog(c, o, lap, tau2) : 0.0;
+        const double v = (xreal && (gof[q] & kReal)) ? leapfrog(c, o, lap, tau2) : 0.0;
         if constexpr (k < S) {
           L[k][q][s0] = v;
           dst[li] = v;
@@ -232,18 +235,16 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         const bool own = xown && (g & kOwn);
         if constexpr (k >= S - 1) {
           if (own && xreal) {
-            double* qp = outp + (g & (kOwn - 1));
-            if constexpr (NTS)
-              __builtin_nontemporal_store(v, qp);
-            else
-              *qp = v;
+            __builtin_nontemporal_store(v, outp + (g & kOff));
           }
         }
-        if (chk && own && xreal) {
-          const int a = li / W0 - 1 - (S - 1), b = li - (li / W0) * W0 - 1 - (S - 1);  // tile coordinates
-          const double e = fabs(v - ((sxc * sty[a]) * stz[b]) * p.ct[k - 1]);
-          emax[k - 1] = e > emax[k - 1] ? e : emax[k - 1];
-          esum[k - 1] += e * e;
+        if constexpr (kChk) {
+          if (chk && own && xreal) {
+            const int a = li / W0 - 1 - (S - 1), b = li - (li / W0) * W0 - 1 - (S - 1);  // tile coordinates
+            const double e = fabs(v - ((sxc * sty[a]) * stz[b]) * p.ct[k - 1]);
+            emax[k - 1] = e > emax[k - 1] ? e : emax[k - 1];
+            esum[k - 1] += e * e;
+          }
         }
       }
     };
@@ -290,7 +291,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
   __shared__ double red_m[NT / 64], red_s[NT / 64];
 #pragma unroll
   for (int k = 0; k < S; ++k) {
-    if (!((p.check_mask >> k) & 1)) continue;
+    if (!((CM >> k) & 1) || !((p.check_mask >> k) & 1)) continue;
     double m = emax[k], sm = esum[k];
     wave_reduce(m, sm);
     __syncthreads();
@@ -325,7 +326,7 @@ TbPlan make_plan_tb(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, i
   W3D_REQUIRE(b.x0 >= full.x0 && b.x1 <= full.x1 && b.y0 >= full.y0 && b.y1 <= full.y1 && b.z0 >= full.z0 &&
                   b.z1 <= full.z1,
               "leapfrog_tb box outside the compute box");
-  W3D_REQUIRE(l.N < (1 << 20), "leapfrog_tb: N too large for 32-bit node indices");
+  W3D_REQUIRE(l.N < (1 << 20) && l.plane < (1 << 29), "leapfrog_tb: plane too large for 29-bit in-plane offsets");
   const i64 S = t.stages;
   // u^{n+k} (k < S) is read up to S−k planes beyond the box: its values there must be real (sx range) unless they lie
   // beyond the global boundary (structural zeros); u^n is read S planes beyond the box, within the allocation
@@ -369,53 +370,69 @@ constexpr size_t max_dyn_lds() {
 }
 
 // allow the dynamic LDS size once per instantiation (outside any stream capture: see leapfrog_tb_prepare)
-template <int S, int NT, bool NTS>
+template <int S, int NT, int CM>
 void prepare_cfg() {
   static_assert(tb_lds_bytes<S, kTile, NT>() <= max_dyn_lds<NT>(), "leapfrog_tb tile does not fit in LDS");
   static const hipError_t attr =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(k_leapfrog_tb<S, kTile, NT, NTS>),
+      hipFuncSetAttribute(reinterpret_cast<const void*>(k_leapfrog_tb<S, kTile, NT, CM>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(max_dyn_lds<NT>()));
   if (attr != hipSuccess) fail(std::string("leapfrog_tb LDS attribute: ") + hipGetErrorString(attr));
 }
 
-template <int S, int NT, bool NTS>
+template <int S, int NT, int CM>
 void launch_cfg(const TbParams& p, int nblocks, hipStream_t st) {
-  prepare_cfg<S, NT, NTS>();
+  prepare_cfg<S, NT, CM>();
   const size_t shmem = tb_lds_bytes<S, kTile, NT>(p.check_mask ? p.x1 - p.x0 : 0);
   W3D_REQUIRE(shmem <= max_dyn_lds<NT>(), "leapfrog_tb: too many owned planes for the LDS sin table");
-  hipLaunchKernelGGL((k_leapfrog_tb<S, kTile, NT, NTS>), dim3(nblocks), dim3(NT), shmem, st, p);
+  hipLaunchKernelGGL((k_leapfrog_tb<S, kTile, NT, CM>), dim3(nblocks), dim3(NT), shmem, st, p);
+}
+
+// instantiated check supersets per S: none, even levels, odd levels, all (checks every 2nd step hit one parity)
+template <int S>
+constexpr int kFull = (1 << S) - 1;
+template <int S>
+constexpr int kEven = 0b1010 & kFull<S>;
+template <int S>
+constexpr int kOdd = 0b0101 & kFull<S>;
+
+template <int S, int NT>
+void launch_nt(const TbParams& p, int nblocks, hipStream_t st) {
+  const int m = p.check_mask;
+  if (m == 0)
+    launch_cfg<S, NT, 0>(p, nblocks, st);
+  else if ((m & ~kEven<S>) == 0)
+    launch_cfg<S, NT, kEven<S>>(p, nblocks, st);
+  else if ((m & ~kOdd<S>) == 0)
+    launch_cfg<S, NT, kOdd<S>>(p, nblocks, st);
+  else
+    launch_cfg<S, NT, kFull<S>>(p, nblocks, st);
 }
 
 template <int S>
 void launch_s(const TbParams& p, int nblocks, const LeapfrogTbTiling& t, hipStream_t st) {
-  if (t.threads == 1024) {
-    if (t.nt_store)
-      launch_cfg<S, 1024, true>(p, nblocks, st);
-    else
-      launch_cfg<S, 1024, false>(p, nblocks, st);
-  } else {
-    if (t.nt_store)
-      launch_cfg<S, 512, true>(p, nblocks, st);
-    else
-      launch_cfg<S, 512, false>(p, nblocks, st);
-  }
+  if (t.threads == 1024)
+    launch_nt<S, 1024>(p, nblocks, st);
+  else
+    launch_nt<S, 512>(p, nblocks, st);
+}
+
+template <int S, int NT>
+void prepare_nt() {
+  prepare_cfg<S, NT, 0>();
+  prepare_cfg<S, NT, kEven<S>>();
+  prepare_cfg<S, NT, kOdd<S>>();
+  prepare_cfg<S, NT, kFull<S>>();
 }
 
 }  // namespace
 
 void leapfrog_tb_prepare() {
-  prepare_cfg<2, 512, true>();
-  prepare_cfg<3, 512, true>();
-  prepare_cfg<4, 512, true>();
-  prepare_cfg<2, 512, false>();
-  prepare_cfg<3, 512, false>();
-  prepare_cfg<4, 512, false>();
-  prepare_cfg<2, 1024, true>();
-  prepare_cfg<3, 1024, true>();
-  prepare_cfg<4, 1024, true>();
-  prepare_cfg<2, 1024, false>();
-  prepare_cfg<3, 1024, false>();
-  prepare_cfg<4, 1024, false>();
+  prepare_nt<2, 512>();
+  prepare_nt<3, 512>();
+  prepare_nt<4, 512>();
+  prepare_nt<2, 1024>();
+  prepare_nt<3, 1024>();
+  prepare_nt<4, 1024>();
 }
 
 size_t leapfrog_tb_lds_bytes(int stages) {

@@ -77,6 +77,7 @@ struct LeapfrogTbTiling {
   int stages = 4;         // 2, 3 or 4 steps per pass
   int threads = 1024;     // workgroup size (512 or 1024; 1024 measured faster at every S)
   bool xcd_remap = true;  // (stores are always non-temporal: measured faster at every S)
+  bool xcd_blocks = false; // with xcd_remap: each XCD owns a square-ish tile block, not two-row strips (measured: no gain)
 };
 // Raise the dynamic-LDS limit of every instantiation (call before capturing launches into a graph).
 void leapfrog_tb_prepare();

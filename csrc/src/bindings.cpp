@@ -314,7 +314,8 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init<>())
       .def_readwrite("stages", &LeapfrogTbTiling::stages)
       .def_readwrite("threads", &LeapfrogTbTiling::threads)
-      .def_readwrite("xcd_remap", &LeapfrogTbTiling::xcd_remap);
+      .def_readwrite("xcd_remap", &LeapfrogTbTiling::xcd_remap)
+      .def_readwrite("xcd_blocks", &LeapfrogTbTiling::xcd_blocks);
   m.def("gpu_leapfrog_tb_lds_bytes", &leapfrog_tb_lds_bytes);
   m.def("gpu_leapfrog_tb_partials", &leapfrog_tb_partials);
   m.def("gpu_leapfrog_tb",

@@ -62,6 +62,7 @@ struct TbParams {
   double ct[4];        // time factor of u^{n+k} (k = 1..S) for the check
   int check_mask;      // bit k−1: check u^{n+k}
   int nty, ntz, nblocks, xcd_remap;
+  int bby, bbz;        // > 0: each XCD's tiles form a bby × bbz block of the tile grid (else two-row strips)
 };
 
 template <int S, int T, int NT>
@@ -100,7 +101,12 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
   int blk = static_cast<int>(blockIdx.x);
   if (p.xcd_remap) blk = (blk & 7) * (p.nblocks >> 3) + (blk >> 3);
   const bool active = blk < p.nty * p.ntz;
-  const int tzi = active ? blk % p.ntz : 0, tyi = active ? blk / p.ntz : 0;
+  int tzi = active ? blk % p.ntz : 0, tyi = active ? blk / p.ntz : 0;
+  if (p.bby > 0) {  // XCD x (= blk / per after the remap) owns block x of the tile grid: halo re-reads stay in its L2
+    const int per = p.bby * p.bbz, x = blk / per, w = blk - x * per, nbz = p.ntz / p.bbz;
+    tyi = (x / nbz) * p.bby + w / p.bbz;
+    tzi = (x - (x / nbz) * nbz) * p.bbz + (w - (w / p.bbz) * p.bbz);
+  }
   const int ty0 = p.y0 + tyi * T, tz0 = p.z0 + tzi * T;
   const int N = p.N;
   const i64 P = p.plane;
@@ -128,7 +134,25 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       const bool own = real && a >= S - 1 && a < S - 1 + T && b >= S - 1 && b < S - 1 + T && y < p.y1 && z < p.z1;
       lid[q] = valid ? (a + 1) * W0 + (b + 1) : G::DUMMY;
       gof[q] = real ? (((y + 1) * R + z + zs1) | kReal | (own ? kOwn : 0)) : zero_off;
-
+    }
+    // wave-uniform stage masks: bit k−1 of wsm[q] is set when some lane of this wave's position set q lies inside stage
+    // k's region (rows [k−1, H1−k+1) of the stage-1 region); other (wave, q, stage) combinations are skipped with a
+    // scalar branch (at 32² tiles and S = 4, 9 of 16 waves hold no position at all in their second set)
+    int wsm[Q];
+    {
+      const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int first = wbase + q * NT, last = imin(first + 63, G::NP - 1);
+        int m = 0;
+        if (first < G::NP) {
+          const int rlo = first / H1, rhi = last / H1;
+#pragma unroll
+          for (int k = 1; k <= S; ++k)
+            if (rhi >= k - 1 && rlo < H1 - (k - 1)) m |= 1 << (k - 1);
+        }
+        wsm[q] = __builtin_amdgcn_readfirstlane(m);
+      }
     }
     // u^n halo ring: LDS index (dummy: no ring node) and global offset (zero node outside the interior)
     int lrid[QR], grof[QR];
@@ -183,7 +207,8 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;  // always an allocated plane
       const double* base = p.cur + static_cast<i64>(xs + 1) * P;
 #pragma unroll
-      for (int q = 0; q < Q; ++q) L[0][q][slot] = base[gof[q] & kOff];
+      for (int q = 0; q < Q; ++q)
+        if (wsm[q]) L[0][q][slot] = base[gof[q] & kOff];
 #pragma unroll
       for (int r = 0; r < QR; ++r) Rg[r][rs] = base[grof[r]];
     };
@@ -192,13 +217,15 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
       const double* base = p.prev + static_cast<i64>(xs + 1) * P;
 #pragma unroll
-      for (int q = 0; q < Q; ++q) Lm[q][slot] = base[gof[q] & kOff];
+      for (int q = 0; q < Q; ++q)
+        if (wsm[q]) Lm[q][slot] = base[gof[q] & kOff];
     };
     auto commit_cur = [&](auto slot_c, auto rs_c, int par) {
       constexpr int slot = decltype(slot_c)::value, rs = decltype(rs_c)::value;
       double* d = lds_plane(0, par);
 #pragma unroll
-      for (int q = 0; q < Q; ++q) d[lid[q]] = L[0][q][slot];
+      for (int q = 0; q < Q; ++q)
+        if (wsm[q]) d[lid[q]] = L[0][q][slot];
 #pragma unroll
       for (int r = 0; r < QR; ++r) d[lrid[r]] = Rg[r][rs];
     };
@@ -217,6 +244,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       const double sxc = (chk && xown) ? stx[xp - x0] : 0.0;
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
+        if (!((wsm[q] >> (k - 1)) & 1)) continue;  // wave-uniform
         const int li = lid[q];
         const double c = L[k - 1][q][s0];
         const double lap = lap7(c, L[k - 1][q][sm], L[k - 1][q][sp], nb[li - W0], nb[li + W0], nb[li - 1], nb[li + 1],
@@ -361,6 +389,23 @@ TbPlan make_plan_tb(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, i
   pl.nblocks = t.xcd_remap ? static_cast<int>(round_up(tiles, 8)) : tiles;
   p.nblocks = pl.nblocks;
   p.xcd_remap = t.xcd_remap ? 1 : 0;
+  // blocked XCD ownership when the tile grid splits into 8 equal blocks (one per XCD), the squarest such block
+  p.bby = p.bbz = 0;
+  if (t.xcd_remap && t.xcd_blocks && tiles == pl.nblocks && tiles % 8 == 0) {
+    const int per = tiles / 8;
+    int best = 1 << 30;
+    for (int by = 1; by <= per; ++by) {
+      if (per % by) continue;
+      const int bz = per / by;
+      if (p.nty % by || p.ntz % bz) continue;
+      const int perim = by + bz;
+      if (perim < best) {
+        best = perim;
+        p.bby = by;
+        p.bbz = bz;
+      }
+    }
+  }
   return pl;
 }
 

@@ -281,8 +281,8 @@ void GpuSolver::build_units() {
   if (mode_ == Mode::kFusedSingle && opt_.tb) {
     // split the K − n remaining steps into passes of 1..temporal steps minimising the summed cost; relative per-step
     // cost of a pass of s steps with every 2nd level checked, measured at 512³ (tools/tune_leapfrog.py --tb:
-    // 610, 509, 349, 315 µs per step)
-    static const double kStepCost[5] = {0.0, 1.94, 1.62, 1.11, 1.00};
+    // 610, 470, 320, 278 µs per step)
+    static const double kStepCost[5] = {0.0, 2.19, 1.69, 1.15, 1.00};
     const int rem = K - n, smax = opt_.temporal;
     std::vector<double> best(static_cast<size_t>(rem + 1), 1e300);
     std::vector<int> take(static_cast<size_t>(rem + 1), 1);

@@ -124,14 +124,14 @@ def main() -> int:
         out.append({"kernel": "k_leapfrog2", "rows": rows, "target_waves": tw, "nt_store": nt, "partials": nb,
                     "check": chk, "us": t, "us_per_step": t / 2, "TBps": 32 * nodes / t / 1e6})
     # deep temporal blocking: S steps per pass, 32 B per node per pass
-    sweep_tb = list(itertools.product([2, 3, 4], [512, 1024], [True], [False, True]))
+    sweep_tb = list(itertools.product([2, 3, 4], [512, 1024], [True, False], [False, True]))
     if a.minimal:
         sweep_tb = [(4, 1024, True, False)]
     if a.quick:
         sweep_tb = [c for c in sweep_tb if c[2] and not c[3]]
     for stages, threads, nt, chk in sweep_tb:
         tt = C.LeapfrogTbTiling()
-        tt.stages, tt.threads = stages, threads
+        tt.stages, tt.threads, tt.xcd_blocks = stages, threads, nt
         nb = C.gpu_leapfrog_tb_partials(lay, box, tt)
         part = torch.empty((stages * nb, 2), dtype=torch.float64, device="cuda")
         st = torch.cuda.current_stream().cuda_stream
@@ -142,7 +142,7 @@ def main() -> int:
                               s.data_ptr(), [0.5] * stages, mask, part.data_ptr() if chk else 0, tt, st)
 
         t = timeit(pass_tb, a.iters)
-        out.append({"kernel": "k_leapfrog_tb", "stages": stages, "threads": threads, "nt_store": nt, "partials": nb,
+        out.append({"kernel": "k_leapfrog_tb", "stages": stages, "threads": threads, "xcd_blocks": nt, "partials": nb,
                     "check": chk, "us": t, "us_per_step": t / stages, "TBps": 32 * nodes / t / 1e6})
     for r in out:
         print(json.dumps(r), flush=True)

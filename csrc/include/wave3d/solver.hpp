@@ -126,6 +126,7 @@ class GpuSolver {
   struct Unit {
     int n;      // current level u^n before the unit
     int steps;  // 1: in-place single step; >= 2: one fused pass writing u^{n+steps−1}, u^{n+steps}
+    bool analytic = false;  // LDS pass from n = 1 computing u⁰, u¹ in the kernel (no init kernel, no reads)
     bool fused() const { return steps >= 2; }
   };
   // one point-to-point message of an exchange: `tag` pairs it with the peer's matching message
@@ -189,6 +190,7 @@ class GpuSolver {
   int n_tb_ = 0;                                            // ... per level of a k_leapfrog_tb pass
   int cur_ = 1, old_ = 0;                     // buffer roles during enqueue
   int start_n_ = 1;                           // first leapfrog step after the init kernel
+  bool analytic_ = false;                     // the first unit computes u⁰, u¹ itself (no init kernel)
   std::vector<char> is_check_;
   hipGraphExec_t graph_exec_ = nullptr;
   int final_buf_ = 0;            // buffer index holding u^K after a solve

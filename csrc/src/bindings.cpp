@@ -321,15 +321,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("gpu_leapfrog_tb",
         [](const Layout& l, const Coeffs& c, std::uintptr_t prev, std::uintptr_t cur, std::uintptr_t out1,
            std::uintptr_t out2, const LBox& box, std::uintptr_t s, std::vector<double> ct, int check_mask,
-           std::uintptr_t partials, const LeapfrogTbTiling& t, std::uintptr_t stream, i64 sx0, i64 sx1) {
+           std::uintptr_t partials, const LeapfrogTbTiling& t, std::uintptr_t stream, i64 sx0, i64 sx1,
+           bool analytic_start) {
           ct.resize(4, 0.0);
           launch_leapfrog_tb(l, c, dptr<const double>(prev), dptr<const double>(cur), dptr<double>(out1),
                              dptr<double>(out2), box, dptr<const double>(s) + 1, ct.data(), check_mask,
-                             dptr<Partial>(partials), t, sptr(stream), sx0, sx1);
+                             dptr<Partial>(partials), t, sptr(stream), sx0, sx1, analytic_start);
         },
         py::arg("layout"), py::arg("coeffs"), py::arg("prev"), py::arg("cur"), py::arg("out1"), py::arg("out2"),
         py::arg("box"), py::arg("s"), py::arg("ct"), py::arg("check_mask"), py::arg("partials"), py::arg("tiling"),
-        py::arg("stream"), py::arg("sx0") = 1, py::arg("sx1") = 0);
+        py::arg("stream"), py::arg("sx0") = 1, py::arg("sx1") = 0, py::arg("analytic_start") = false);
   m.def("gpu_error_blocks", &error_blocks);
   m.def("gpu_error", [](const Layout& l, std::uintptr_t u, const LBox& b, std::uintptr_t s, double ct,
                         std::uintptr_t partials, std::uintptr_t stream) {

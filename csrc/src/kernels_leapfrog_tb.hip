@@ -58,7 +58,7 @@ struct TbParams {
   int ax0, ax1;        // allocated x range (local planes that may be read)
   int N, gx0, gy0, gz0;
   int y0, y1, z0, z1;  // output (y, z) range (local)
-  double ihx2, ihy2, ihz2, tau2;
+  double ihx2, ihy2, ihz2, tau2, half_tau2;
   double ct[4];        // time factor of u^{n+k} (k = 1..S) for the check
   int check_mask;      // bit k−1: check u^{n+k}
   int nty, ntz, nblocks, xcd_remap;
@@ -80,16 +80,24 @@ struct TbGeom {
   static constexpr int lds_doubles() { return S * 2 * PLP; }  // levels 0..S−1 × 2 parity slots
 };
 
-// + the sin factors of the tile (y, z) and of the owned planes (x) for the error check: a global load of the per-plane
-// x factor would be a vector load (the table may alias the outputs, so no scalar load) whose wait drains the prefetch
+// + sin tables (error check, analytic start): y and z over the u^n region ± 1, x over the planes the pass touches ± 1.
+// In LDS because a global load of the per-plane x factor would be a vector load (the table may alias the outputs, so
+// no scalar load) whose wait drains the prefetch queue. nxo = tb_nx_table(x1 − x0) or 0 (no table needed).
 template <int S, int T, int NT>
 constexpr size_t tb_lds_bytes(int nxo = 0) {
-  return (static_cast<size_t>(TbGeom<S, T, NT>::lds_doubles()) + 2 * T + static_cast<size_t>(nxo)) * sizeof(double);
+  return (static_cast<size_t>(TbGeom<S, T, NT>::lds_doubles()) + 2 * (T + 2 * S + 2) + static_cast<size_t>(nxo)) *
+         sizeof(double);
+}
+template <int S>
+constexpr int tb_nx_table(int nx_box) {
+  return nx_box + 2 * S + 4;
 }
 
 // CM: compile-time superset of the levels that may be checked (bit k−1 ↔ u^{n+k}); levels outside it carry no error
-// accumulators or check code (registers: the S = 4 kernel sits at the 128-VGPR limit of 4 waves per SIMD)
-template <int S, int T, int NT, int CM>
+// accumulators or check code (registers: the S = 4 kernel sits at the 128-VGPR limit of 4 waves per SIMD).
+// INIT: analytic start at n = 1 — u^{n−1} = u⁰ = φ and u^n = u¹ = u⁰ + τ²/2·Δ_h u⁰ are computed from the sin tables
+// (k_init_first's formulas and operation order) instead of loaded: the pass reads nothing from HBM.
+template <int S, int T, int NT, int CM, bool INIT>
 __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
   using G = TbGeom<S, T, NT>;
   constexpr int Q = G::Q, QR = G::QR, H1 = G::H1, W0 = G::W0, PLP = G::PLP;
@@ -174,21 +182,41 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       const int y = ty0 - S + a0, z = tz0 - S + b0;
       const bool valid = ridx < G::NR;
       lrid[r] = valid ? a0 * W0 + b0 : G::DUMMY;
-      grof[r] = (valid && inside(p.gy0 + y) && inside(p.gz0 + z)) ? (y + 1) * R + z + zs1 : zero_off;
+      grof[r] = (valid && inside(p.gy0 + y) && inside(p.gz0 + z)) ? ((y + 1) * R + z + zs1) | kReal : zero_off;
     }
-    // sin factors for the check: y and z of the tile, x of the owned planes (clamped into −1..N+1; only owned nodes,
-    // all interior, use them)
-    double* sty = lds + G::lds_doubles();
-    double* stz = sty + T;
-    double* stx = stz + T;
-    if (p.check_mask) {
+    // sin tables: syw[j] = s[y] for y = ty0 − S − 1 + j (the u^n region ± 1), szw likewise, sxw[i] = s[x] for
+    // x = x0 − S − 1 + i; indices clamped into −1..N+1 (only nodes of the interior, and their neighbours, use them)
+    constexpr int NYW = T + 2 * S + 2;
+    double* syw = lds + G::lds_doubles();
+    double* szw = syw + NYW;
+    double* sxw = szw + NYW;
+    if (p.check_mask || INIT) {
       auto sc = [&](int g) { return p.s[g < -1 ? -1 : g > N + 1 ? N + 1 : g]; };
-      for (int t = tid; t < T; t += NT) {
-        sty[t] = sc(p.gy0 + ty0 + t);
-        stz[t] = sc(p.gz0 + tz0 + t);
+      for (int t = tid; t < NYW; t += NT) {
+        syw[t] = sc(p.gy0 + ty0 - S - 1 + t);
+        szw[t] = sc(p.gz0 + tz0 - S - 1 + t);
       }
-      for (int x = tid; x < p.x1 - p.x0; x += NT) stx[x] = p.s[p.gx0 + p.x0 + x];
+      for (int i = tid; i < tb_nx_table<S>(p.x1 - p.x0); i += NT) sxw[i] = sc(p.gx0 + p.x0 - S - 1 + i);
+      __syncthreads();
     }
+    // table indices of an LDS position li (u^n-region coordinates): y ↔ li / W0 + 1, z ↔ li % W0 + 1 (the pad's dummy
+    // node is clamped into the table)
+    auto ytab = [&](int li) { return imin(li / W0 + 1, W0); };
+    auto ztab = [&](int li) { return li - (li / W0) * W0 + 1; };
+    const int xtab0 = S + 1 - p.x0;  // x ↔ sxw[x + xtab0]
+    // analytic u⁰ = φ and u¹ at plane x, LDS position li (INIT)
+    auto phi_at = [&](int x, int li) {
+      return (sxw[x + xtab0] * syw[ytab(li)]) * szw[ztab(li)];
+    };
+    auto u1_at = [&](int x, int li, bool real_yz) {
+      const int xi = x + xtab0, ya = ytab(li), zb = ztab(li);
+      const double sxc = sxw[xi], sy = syw[ya], sz = szw[zb];
+      const double cy = sxc * sy;
+      const double c = cy * sz;
+      const double lap = lap7(c, (sxw[xi - 1] * sy) * sz, (sxw[xi + 1] * sy) * sz, (sxc * syw[ya - 1]) * sz,
+                              (sxc * syw[ya + 1]) * sz, cy * szw[zb - 1], cy * szw[zb + 1], ihx2, ihy2, ihz2);
+      return (real_yz && inside(p.gx0 + x)) ? first_step(c, lap, p.half_tau2) : 0.0;
+    };
 
     // ---- register queues: plane x of level j at slot (x − i0) & 3; u^{n−1} and the ring: slot (x − i0) & 1
     // Stages also run on the positions outside their (shrinking) region: those values are never read by a node
@@ -202,23 +230,39 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     auto lds_plane = [&](int j, int par) { return lds + (j * 2 + par) * PLP; };
 
     // plane x of u^n: owned positions into L[0][q][slot], ring into Rg[r][rs]
+    const int wbase_r = __builtin_amdgcn_readfirstlane(tid & ~63);
     auto load_cur = [&](auto slot_c, auto rs_c, int x) {
       constexpr int slot = decltype(slot_c)::value, rs = decltype(rs_c)::value;
-      const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;  // always an allocated plane
-      const double* base = p.cur + static_cast<i64>(xs + 1) * P;
+      if constexpr (INIT) {
 #pragma unroll
-      for (int q = 0; q < Q; ++q)
-        if (wsm[q]) L[0][q][slot] = base[gof[q] & kOff];
+        for (int q = 0; q < Q; ++q)
+          if (wsm[q]) L[0][q][slot] = u1_at(x, lid[q], gof[q] & kReal);
 #pragma unroll
-      for (int r = 0; r < QR; ++r) Rg[r][rs] = base[grof[r]];
+        for (int r = 0; r < QR; ++r)
+          if (wbase_r + r * NT < G::NR) Rg[r][rs] = u1_at(x, lrid[r], grof[r] & kReal);
+      } else {
+        const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;  // always an allocated plane
+        const double* base = p.cur + static_cast<i64>(xs + 1) * P;
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+          if (wsm[q]) L[0][q][slot] = base[gof[q] & kOff];
+#pragma unroll
+        for (int r = 0; r < QR; ++r) Rg[r][rs] = base[grof[r] & kOff];
+      }
     };
     auto load_prev = [&](auto slot_c, int x) {
       constexpr int slot = decltype(slot_c)::value;
-      const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
-      const double* base = p.prev + static_cast<i64>(xs + 1) * P;
+      if constexpr (INIT) {
 #pragma unroll
-      for (int q = 0; q < Q; ++q)
-        if (wsm[q]) Lm[q][slot] = base[gof[q] & kOff];
+        for (int q = 0; q < Q; ++q)
+          if (wsm[q]) Lm[q][slot] = phi_at(x, lid[q]);
+      } else {
+        const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
+        const double* base = p.prev + static_cast<i64>(xs + 1) * P;
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+          if (wsm[q]) Lm[q][slot] = base[gof[q] & kOff];
+      }
     };
     auto commit_cur = [&](auto slot_c, auto rs_c, int par) {
       constexpr int slot = decltype(slot_c)::value, rs = decltype(rs_c)::value;
@@ -241,7 +285,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       constexpr bool kChk = (CM >> (k - 1)) & 1;
       const bool chk = kChk && ((p.check_mask >> (k - 1)) & 1);
       double* outp = (k == S ? p.out2 : p.out1) + static_cast<i64>(xp + 1) * P;
-      const double sxc = (chk && xown) ? stx[xp - x0] : 0.0;
+      const double sxc = (chk && xown) ? sxw[xp + xtab0] : 0.0;
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         if (!((wsm[q] >> (k - 1)) & 1)) continue;  // wave-uniform
@@ -268,8 +312,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         }
         if constexpr (kChk) {
           if (chk && own && xreal) {
-            const int a = li / W0 - 1 - (S - 1), b = li - (li / W0) * W0 - 1 - (S - 1);  // tile coordinates
-            const double e = fabs(v - ((sxc * sty[a]) * stz[b]) * p.ct[k - 1]);
+            const double e = fabs(v - ((sxc * syw[ytab(li)]) * szw[ztab(li)]) * p.ct[k - 1]);
             emax[k - 1] = e > emax[k - 1] ? e : emax[k - 1];
             esum[k - 1] += e * e;
           }
@@ -415,21 +458,21 @@ constexpr size_t max_dyn_lds() {
 }
 
 // allow the dynamic LDS size once per instantiation (outside any stream capture: see leapfrog_tb_prepare)
-template <int S, int NT, int CM>
+template <int S, int NT, int CM, bool INIT>
 void prepare_cfg() {
   static_assert(tb_lds_bytes<S, kTile, NT>() <= max_dyn_lds<NT>(), "leapfrog_tb tile does not fit in LDS");
   static const hipError_t attr =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(k_leapfrog_tb<S, kTile, NT, CM>),
+      hipFuncSetAttribute(reinterpret_cast<const void*>(k_leapfrog_tb<S, kTile, NT, CM, INIT>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(max_dyn_lds<NT>()));
   if (attr != hipSuccess) fail(std::string("leapfrog_tb LDS attribute: ") + hipGetErrorString(attr));
 }
 
-template <int S, int NT, int CM>
+template <int S, int NT, int CM, bool INIT>
 void launch_cfg(const TbParams& p, int nblocks, hipStream_t st) {
-  prepare_cfg<S, NT, CM>();
-  const size_t shmem = tb_lds_bytes<S, kTile, NT>(p.check_mask ? p.x1 - p.x0 : 0);
-  W3D_REQUIRE(shmem <= max_dyn_lds<NT>(), "leapfrog_tb: too many owned planes for the LDS sin table");
-  hipLaunchKernelGGL((k_leapfrog_tb<S, kTile, NT, CM>), dim3(nblocks), dim3(NT), shmem, st, p);
+  prepare_cfg<S, NT, CM, INIT>();
+  const size_t shmem = tb_lds_bytes<S, kTile, NT>((p.check_mask || INIT) ? tb_nx_table<S>(p.x1 - p.x0) : 0);
+  W3D_REQUIRE(shmem <= max_dyn_lds<NT>(), "leapfrog_tb: too many planes for the LDS sin table");
+  hipLaunchKernelGGL((k_leapfrog_tb<S, kTile, NT, CM, INIT>), dim3(nblocks), dim3(NT), shmem, st, p);
 }
 
 // instantiated check supersets per S: none, even levels, odd levels, all (checks every 2nd step hit one parity)
@@ -440,44 +483,50 @@ constexpr int kEven = 0b1010 & kFull<S>;
 template <int S>
 constexpr int kOdd = 0b0101 & kFull<S>;
 
-template <int S, int NT>
+template <int S, int NT, bool INIT>
 void launch_nt(const TbParams& p, int nblocks, hipStream_t st) {
   const int m = p.check_mask;
   if (m == 0)
-    launch_cfg<S, NT, 0>(p, nblocks, st);
+    launch_cfg<S, NT, 0, INIT>(p, nblocks, st);
   else if ((m & ~kEven<S>) == 0)
-    launch_cfg<S, NT, kEven<S>>(p, nblocks, st);
+    launch_cfg<S, NT, kEven<S>, INIT>(p, nblocks, st);
   else if ((m & ~kOdd<S>) == 0)
-    launch_cfg<S, NT, kOdd<S>>(p, nblocks, st);
+    launch_cfg<S, NT, kOdd<S>, INIT>(p, nblocks, st);
   else
-    launch_cfg<S, NT, kFull<S>>(p, nblocks, st);
+    launch_cfg<S, NT, kFull<S>, INIT>(p, nblocks, st);
 }
 
+// the analytic-start pass is built for 1024-thread workgroups only
 template <int S>
-void launch_s(const TbParams& p, int nblocks, const LeapfrogTbTiling& t, hipStream_t st) {
-  if (t.threads == 1024)
-    launch_nt<S, 1024>(p, nblocks, st);
+void launch_s(const TbParams& p, int nblocks, const LeapfrogTbTiling& t, bool init, hipStream_t st) {
+  if (init)
+    launch_nt<S, 1024, true>(p, nblocks, st);
+  else if (t.threads == 1024)
+    launch_nt<S, 1024, false>(p, nblocks, st);
   else
-    launch_nt<S, 512>(p, nblocks, st);
+    launch_nt<S, 512, false>(p, nblocks, st);
 }
 
-template <int S, int NT>
+template <int S, int NT, bool INIT>
 void prepare_nt() {
-  prepare_cfg<S, NT, 0>();
-  prepare_cfg<S, NT, kEven<S>>();
-  prepare_cfg<S, NT, kOdd<S>>();
-  prepare_cfg<S, NT, kFull<S>>();
+  prepare_cfg<S, NT, 0, INIT>();
+  prepare_cfg<S, NT, kEven<S>, INIT>();
+  prepare_cfg<S, NT, kOdd<S>, INIT>();
+  prepare_cfg<S, NT, kFull<S>, INIT>();
 }
 
 }  // namespace
 
 void leapfrog_tb_prepare() {
-  prepare_nt<2, 512>();
-  prepare_nt<3, 512>();
-  prepare_nt<4, 512>();
-  prepare_nt<2, 1024>();
-  prepare_nt<3, 1024>();
-  prepare_nt<4, 1024>();
+  prepare_nt<2, 512, false>();
+  prepare_nt<3, 512, false>();
+  prepare_nt<4, 512, false>();
+  prepare_nt<2, 1024, false>();
+  prepare_nt<3, 1024, false>();
+  prepare_nt<4, 1024, false>();
+  prepare_nt<2, 1024, true>();
+  prepare_nt<3, 1024, true>();
+  prepare_nt<4, 1024, true>();
 }
 
 size_t leapfrog_tb_lds_bytes(int stages) {
@@ -492,8 +541,9 @@ int leapfrog_tb_partials(const Layout& l, const LBox& box, const LeapfrogTbTilin
 
 void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
                         double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
-                        Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, i64 sx0, i64 sx1) {
-  W3D_REQUIRE(prev != out1 && prev != out2 && cur != out1 && cur != out2 && out1 != out2,
+                        Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, i64 sx0, i64 sx1,
+                        bool analytic_start) {
+  W3D_REQUIRE(out1 != out2 && (analytic_start || (prev != out1 && prev != out2 && cur != out1 && cur != out2)),
               "leapfrog_tb needs four distinct buffers");
   if (sx0 > sx1) {
     const LBox full = compute_box(l);
@@ -504,8 +554,8 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
   if (pl.nblocks == 0) return;
   TbParams& p = pl.prm;
   const i64 kb = l.kbase();
-  p.prev = prev + kb;
-  p.cur = cur + kb;
+  p.prev = analytic_start ? nullptr : prev + kb;
+  p.cur = analytic_start ? nullptr : cur + kb;
   p.out1 = out1 + kb;
   p.out2 = out2 + kb;
   p.s = d_s;
@@ -513,13 +563,14 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
   p.ihy2 = c.ihy2;
   p.ihz2 = c.ihz2;
   p.tau2 = c.tau2;
+  p.half_tau2 = c.half_tau2;
   p.check_mask = partials != nullptr ? (check_mask & ((1 << t.stages) - 1)) : 0;
   p.partials = p.check_mask != 0 ? partials : nullptr;
   for (int k = 0; k < 4; ++k) p.ct[k] = (ct != nullptr && k < t.stages) ? ct[k] : 0.0;
   switch (t.stages) {
-    case 2: launch_s<2>(p, pl.nblocks, t, stream); break;
-    case 3: launch_s<3>(p, pl.nblocks, t, stream); break;
-    default: launch_s<4>(p, pl.nblocks, t, stream); break;
+    case 2: launch_s<2>(p, pl.nblocks, t, analytic_start, stream); break;
+    case 3: launch_s<3>(p, pl.nblocks, t, analytic_start, stream); break;
+    default: launch_s<4>(p, pl.nblocks, t, analytic_start, stream); break;
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) fail(std::string("leapfrog_tb launch: ") + hipGetErrorString(e));

@@ -279,10 +279,11 @@ void GpuSolver::build_units() {
   const int K = prob_.K;
   int n = start_n_;
   if (mode_ == Mode::kFusedSingle && opt_.tb) {
-    // split the K − n remaining steps into passes of 1..temporal steps minimising the summed cost; relative per-step
-    // cost of a pass of s steps with every 2nd level checked, measured at 512³ (tools/tune_leapfrog.py --tb:
-    // 610, 470, 320, 278 µs per step)
-    static const double kStepCost[5] = {0.0, 2.19, 1.69, 1.15, 1.00};
+    // split the K − n remaining steps into passes of 1..temporal steps minimising the summed cost: µs per step of a
+    // pass of s steps with every 2nd level checked, measured at 512³ (tools/tune_leapfrog.py --tb); the analytic
+    // first pass reads nothing but computes u⁰, u¹ (compute-bound)
+    static const double kStepCost[5] = {0.0, 610.0, 451.0, 310.0, 283.0};
+    static const double kAnalyticCost[5] = {0.0, 1e9, 380.0, 328.0, 306.0};
     const int rem = K - n, smax = opt_.temporal;
     std::vector<double> best(static_cast<size_t>(rem + 1), 1e300);
     std::vector<int> take(static_cast<size_t>(rem + 1), 1);
@@ -295,7 +296,21 @@ void GpuSolver::build_units() {
           take[static_cast<size_t>(r)] = st;
         }
       }
-    for (int r = rem; r > 0; r -= take[static_cast<size_t>(r)]) {
+    if (analytic_) {
+      // the analytic first pass takes 2..temporal steps: minimise its cost plus the best split of the rest
+      int bf = 2;
+      double bc = 1e300;
+      for (int f = 2; f <= std::min(smax, rem); ++f) {
+        const double c = f * kAnalyticCost[f] + best[static_cast<size_t>(rem - f)];
+        if (c < bc) {
+          bc = c;
+          bf = f;
+        }
+      }
+      units_.push_back(Unit{n, bf, true});
+      n += bf;
+    }
+    for (int r = K - n; r > 0; r -= take[static_cast<size_t>(r)]) {
       units_.push_back(Unit{n, take[static_cast<size_t>(r)]});
       n += take[static_cast<size_t>(r)];
     }
@@ -372,7 +387,11 @@ void GpuSolver::phase_init() {
   ev_next_ = 0;
   marks_.clear();
   W3D_HIP(hipMemsetAsync(errlog_, 0, static_cast<size_t>(K + 1) * sizeof(Partial), s0_));
-  if (opt_.init2 && K >= 2) {
+  // one rank on the LDS kernel: the first pass starts from the analytic u⁰, u¹ itself (no init kernel, no reads)
+  analytic_ = mode_ == Mode::kFusedSingle && opt_.tb && opt_.init2 && opt_.temporal >= 2 && K >= 3 && !is_check_[1];
+  if (analytic_) {
+    start_n_ = 1;
+  } else if (opt_.init2 && K >= 2) {
     // u¹ -> buf 0, u² -> buf 1 analytically (no read pass), ghosts included; the first leapfrog step is n = 2
     timed(kPhaseInit, s0_, [&] {
       launch_init_two(lay_, coef_, s, u_[0], u_[1], ct_[2], is_check_[2] ? partials_ : nullptr, s0_);
@@ -485,7 +504,7 @@ void GpuSolver::unit_interior(int i) {
     }
     timed(kPhaseCompute, s0_, [&] {
       launch_leapfrog_tb(lay_, coef_, u_[old_], u_[cur_], u_[uf_[0]], u_[uf_[1]], full_, s, cts, mask,
-                         mask ? partials_ : nullptr, t, s0_);
+                         mask ? partials_ : nullptr, t, s0_, 1, 0, u.analytic);
     });
     if (mask) {
       timed(kPhaseCheck, s0_, [&] {

@@ -109,26 +109,30 @@ def leapfrog2(layout, coeffs, prev: torch.Tensor, cur: torch.Tensor, out1: torch
 
 
 def leapfrog_tb(layout, coeffs, prev: torch.Tensor, cur: torch.Tensor, out1: torch.Tensor, out2: torch.Tensor, box,
-                s_ext: torch.Tensor, stages: int = 4, ct=None, check_mask: int = 0, threads: int = 512):
+                s_ext: torch.Tensor, stages: int = 4, ct=None, check_mask: int = 0, threads: int = 1024,
+                analytic_start: bool = False):
     """``stages`` fused leapfrog steps held in LDS (HIP only): out1 = u^{n+S-1}, out2 = u^{n+S}.
 
     ``ct[k-1]`` is the time factor of u^{n+k}; for every bit k-1 set in ``check_mask`` the (L∞, Σe²) error of u^{n+k}
-    is returned in a dict {k: (max, sumsq)}."""
+    is returned in a dict {k: (max, sumsq)}. ``analytic_start``: n = 1, u⁰ and u¹ are computed in the kernel
+    (``prev``/``cur`` are not read)."""
     C = _C()
-    if not cur.is_cuda:
+    if not out1.is_cuda:
         raise ValueError("leapfrog_tb is a GPU kernel; on the CPU take single leapfrog() steps")
     t = C.LeapfrogTbTiling()
     t.stages = stages
     t.threads = threads
     nb = C.gpu_leapfrog_tb_partials(layout, box, t)
     ct = list(ct) if ct is not None else [0.0] * stages
-    part = torch.empty((stages * max(nb, 1), 2), dtype=torch.float64, device=cur.device) if check_mask else None
-    C.gpu_leapfrog_tb(layout, coeffs, prev.data_ptr(), cur.data_ptr(), out1.data_ptr(), out2.data_ptr(), box,
-                      s_ext.data_ptr(), ct, check_mask, part.data_ptr() if check_mask else 0, t, _stream())
+    part = torch.empty((stages * max(nb, 1), 2), dtype=torch.float64, device=out1.device) if check_mask else None
+    C.gpu_leapfrog_tb(layout, coeffs, prev.data_ptr() if prev is not None else 0,
+                      cur.data_ptr() if cur is not None else 0, out1.data_ptr(), out2.data_ptr(), box,
+                      s_ext.data_ptr(), ct, check_mask, part.data_ptr() if check_mask else 0, t, _stream(),
+                      analytic_start=analytic_start)
     res = {}
     for k in range(1, stages + 1):
         if check_mask >> (k - 1) & 1:
-            out = torch.empty(2, dtype=torch.float64, device=cur.device)
+            out = torch.empty(2, dtype=torch.float64, device=out1.device)
             C.gpu_reduce(part[(k - 1) * nb:].data_ptr(), nb, out.data_ptr(), _stream())
             o = out.cpu()
             res[k] = (float(o[0]), float(o[1]))

@@ -196,6 +196,35 @@ def test_leapfrog_tb_equals_single_steps(gpu, stages, N, threads):
         assert math.isclose(e_gpu[k][1], e_cpu[k][1], rel_tol=1e-12)
 
 
+@pytest.mark.parametrize("stages", [2, 3, 4])
+@pytest.mark.parametrize("N", [40, 77, 130])
+def test_leapfrog_tb_analytic_start(gpu, stages, N):
+    """Analytic-start pass (u⁰ = φ, u¹ computed in the kernel) == init_first + S CPU steps on the interior."""
+    C = gpu
+    prob, co, lay, _ = _setup(C, N)
+    box = C.compute_box(lay)
+    s = ops.sin_table_ext(prob)
+    u0, u1 = ops.alloc_field(lay), ops.alloc_field(lay)
+    ops.init_first(lay, co, s, u0, u1)
+    ct = [math.cos(prob.a_t * (1 + k) * prob.tau) for k in range(1, stages + 1)]
+    a, b = u0.clone(), u1.clone()
+    e_cpu = {}
+    for k in range(1, stages + 1):
+        e_cpu[k] = ops.leapfrog(lay, co, b, a, [box], s, ct[k - 1], check=True)
+        a, b = b, a
+    o1 = torch.zeros(int(lay.total), dtype=torch.float64, device="cuda")
+    o2 = torch.zeros_like(o1)
+    e_gpu = ops.leapfrog_tb(lay, co, None, None, o1, o2, box, s.cuda(), stages, ct, (1 << stages) - 1,
+                            analytic_start=True)
+    torch.cuda.synchronize()
+    inner = (slice(1, -1),) * 3  # u⁰ = φ also fills the ghosts of the CPU buffers; the pass writes the interior only
+    assert torch.equal(ops.to_grid(lay, o1.cpu())[inner], ops.to_grid(lay, a)[inner])
+    assert torch.equal(ops.to_grid(lay, o2.cpu())[inner], ops.to_grid(lay, b)[inner])
+    for k in range(1, stages + 1):
+        assert e_gpu[k][0] == e_cpu[k][0]
+        assert math.isclose(e_gpu[k][1], e_cpu[k][1], rel_tol=1e-12)
+
+
 @pytest.mark.parametrize("N,world,rank,decomp", [(36, 1, 0, "slab"), (53, 1, 0, "slab"), (40, 2, 1, "slab"),
                                                  (45, 8, 5, "2x2x2"), (38, 6, 2, "1x2x3")])
 @pytest.mark.parametrize("check", [False, True])

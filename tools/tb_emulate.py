@@ -28,9 +28,11 @@ def lap7(c, xm, xp, ym, yp, zm, zp, ihx2, ihy2, ihz2):
 
 
 def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2: np.ndarray, box, s_ext: np.ndarray,
-             S: int, sx, ct=None, check_mask: int = 0):
+             S: int, sx, ct=None, check_mask: int = 0, analytic_start: bool = False):
     """Emulate one launch. Arrays are the flat padded fields (layout.total doubles); s_ext is the extended sin table
-    (element g+1 ↔ global g). Returns {k: (max, sumsq)} for checked stages (per-tile partials combined in order)."""
+    (element g+1 ↔ global g). Returns {k: (max, sumsq)} for checked stages (per-tile partials combined in order).
+    analytic_start: u^{n-1} = φ and u^n = u¹ come from the kernel's LDS sin tables (same index math and clamping)
+    instead of prev/cur."""
     G = Geom(S)
     N = int(lay.N)
     P, R, zs, xg = int(lay.plane), int(lay.pitch), int(lay.zs), int(lay.xg)
@@ -59,6 +61,7 @@ def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2:
         return s_ext[g + 1]
 
     nty, ntz = -(-(y1 - y0) // T), -(-(z1 - z0) // T)
+    i0, i1 = x0 - S + 1, x1 + S - 2
     errs = {k: [0.0, 0.0] for k in range(1, S + 1) if check_mask >> (k - 1) & 1}
     for tyi in range(nty):
         for tzi in range(ntz):
@@ -67,12 +70,46 @@ def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2:
             emax = [0.0] * S
             esum = [0.0] * S
 
+            # the kernel's sin tables: syw[j] ↔ y = ty0 - S - 1 + j, sxw[i] ↔ x = x0 - S - 1 + i, clamped to -1..N+1
+            W0 = T + 2 * S
+            nyw = T + 2 * S + 2
+
+            def sc(g):
+                return s_ext[np.clip(g, -1, N + 1) + 1]
+
+            syw = sc(gy0 + ty0 - S - 1 + np.arange(nyw))
+            szw = sc(gz0 + tz0 - S - 1 + np.arange(nyw))
+            sxw = sc(gx0 + x0 - S - 1 + np.arange(x1 - x0 + 2 * S + 4))
+            xtab0 = S + 1 - x0
+
+            def tables(h, w, x):
+                # LDS position (level-0 coordinates) of the level's region → table indices (ytab, ztab)
+                a = np.arange(w)
+                li_a = a + (S - h)  # level-0 row of region row a
+                ya = np.minimum(li_a + 1, W0)[:, None] + 0 * a[None, :]
+                zb = (li_a + 1)[None, :] + 0 * a[:, None]
+                xi = x + xtab0
+                if xi - 1 < 0 or xi + 1 >= len(sxw) or ya.max() + 1 >= nyw or zb.max() + 1 >= nyw:
+                    raise IndexError(f"sin table index out of range: x={x} xi={xi} n={len(sxw)} ya={ya.max()} zb={zb.max()} nyw={nyw}")
+                return ya, zb, xi
+
             def fetch(j, src, x):
                 h, w = G.halo(j), G.W(j)
                 a = np.arange(w)
                 y = ty0 - h + a[:, None] + 0 * a[None, :]
                 z = tz0 - h + a[None, :] + 0 * a[:, None]
                 v = np.zeros((w, w))
+                if analytic_start:
+                    ya, zb, xi = tables(h, w, x)
+                    sxc, sy, sz = sxw[xi], syw[ya], szw[zb]
+                    cy = sxc * sy
+                    c = cy * sz
+                    if j < 0:  # u0 = φ
+                        return c
+                    lap = lap7(c, (sxw[xi - 1] * sy) * sz, (sxw[xi + 1] * sy) * sz, (sxc * syw[ya - 1]) * sz,
+                               (sxc * syw[ya + 1]) * sz, cy * szw[zb - 1], cy * szw[zb + 1], co.ihx2, co.ihy2, co.ihz2)
+                    real = inside(gy0 + y) & inside(gz0 + z) & (1 <= gx0 + x <= N - 1)
+                    return np.where(real, c + co.half_tau2 * lap, 0.0)
                 if ax0 <= x < ax1 and 1 <= gx0 + x <= N - 1:
                     m = inside(gy0 + y) & inside(gz0 + z)
                     v[m] = src[goff(x, y[m], z[m])]
@@ -80,7 +117,8 @@ def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2:
 
             def commit(x):
                 ring[0][x % 3] = fetch(0, cur, x)
-                ring[-1][0] = fetch(-1, prev, x - 1)
+                if x - 1 >= i0:  # like the kernel, u^{n-1} is only fetched from plane i0 on
+                    ring[-1][0] = fetch(-1, prev, x - 1)
 
             def stage(k, xp):
                 hk, wk = G.halo(k), G.W(k)
@@ -113,7 +151,6 @@ def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2:
                     emax[k - 1] = max(emax[k - 1], float(e.max()))
                     esum[k - 1] += float((e * e).sum())
 
-            i0, i1 = x0 - S + 1, x1 + S - 2
             commit(i0 - 1)
             commit(i0)
             for i in range(i0, i1 + 1):

@@ -144,6 +144,22 @@ def main() -> int:
         t = timeit(pass_tb, a.iters)
         out.append({"kernel": "k_leapfrog_tb", "stages": stages, "threads": threads, "xcd_blocks": nt, "partials": nb,
                     "check": chk, "us": t, "us_per_step": t / stages, "TBps": 32 * nodes / t / 1e6})
+    # analytic-start pass (no HBM reads): u⁰, u¹ computed in the kernel; production check pattern (odd levels)
+    for stages in ([4] if a.minimal else [2, 3, 4]):
+        tt = C.LeapfrogTbTiling()
+        tt.stages, tt.threads = stages, 1024
+        nb = C.gpu_leapfrog_tb_partials(lay, box, tt)
+        part = torch.empty((stages * nb, 2), dtype=torch.float64, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+        mask = 0b0101 & ((1 << stages) - 1)
+
+        def pass_an():
+            C.gpu_leapfrog_tb(lay, co, 0, 0, bufs[0].data_ptr(), bufs[1].data_ptr(), box, s.data_ptr(),
+                              [0.5] * stages, mask, part.data_ptr(), tt, st, analytic_start=True)
+
+        t = timeit(pass_an, a.iters)
+        out.append({"kernel": "k_leapfrog_tb analytic", "stages": stages, "threads": 1024, "check": True, "us": t,
+                    "us_per_step": t / stages, "TBps": 16 * nodes / t / 1e6})
     for r in out:
         print(json.dumps(r), flush=True)
     if any(r["kernel"] == "k_leapfrog" for r in out):

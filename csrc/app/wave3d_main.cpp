@@ -47,7 +47,7 @@ struct Args {
   int tb_threads = 0;
   bool init2 = true;
   int fake_rank = -1, fake_world = 0;
-  int t2_rows = 0, t2_target = -1, deep_min = -1, t2_occ = -1;
+  int t2_rows = 0, t2_target = -1, deep_min = -1, t2_occ = -1, tb_min = -1;
   bool force = false;
   int repeat = 1;
   int warmup = 0;
@@ -76,7 +76,9 @@ struct Args {
                "  --timers           per-phase GPU timers (init / compute / exchange / check)\n"
                "  --no-temporal      one leapfrog step per HBM pass (disable temporal blocking)\n"
                "  --temporal S       at most S (2..4) leapfrog steps per HBM pass (default 4)\n"
-               "  --no-tb            one rank: two-step register-queue passes instead of the LDS S-step kernel\n"
+               "  --no-tb            two-step register-queue passes instead of the LDS S-step kernel\n"
+               "  --tb-min-planes M  slab ranks: LDS S-step passes with S-deep halos from M owned planes (default 16)\n"
+               "  --deep-min-planes M  slab ranks without the LDS kernel: two-step passes from M planes (default 96)\n"
                "  --tb-threads T     LDS S-step kernel workgroup size (512 or 1024)\n"
                "  --no-init2         start from u0,u1 + a first step instead of analytic u1,u2\n"
                "  --debug-sync       synchronize after every step (race triage)\n"
@@ -121,6 +123,7 @@ Args parse(int argc, char** argv) {
     else if (s == "--no-init2") a.init2 = false;
     else if (s == "--t2-rows") a.t2_rows = std::stoi(next());
     else if (s == "--deep-min-planes") a.deep_min = std::stoi(next());
+    else if (s == "--tb-min-planes") a.tb_min = std::stoi(next());
     else if (s == "--t2-target") a.t2_target = std::stoi(next());
     else if (s == "--t2-occ") a.t2_occ = std::stoi(next());
     else if (s == "--fake-rank") {
@@ -329,6 +332,7 @@ int run_gpu(const Args& a) {
   o.fake_comm = fake;
   if (a.t2_rows > 0) o.tiling2.rows = a.t2_rows;
   if (a.deep_min >= 0) o.deep_min_planes = a.deep_min;
+  if (a.tb_min >= 0) o.tb_min_planes = a.tb_min;
   if (a.t2_occ >= 0) o.tiling2.occupancy = a.t2_occ;
   if (a.t2_target >= 0) o.tiling2.target_waves = a.t2_target;
   if (a.variant >= 0) o.tiling.variant = a.variant;

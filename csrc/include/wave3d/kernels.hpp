@@ -72,7 +72,7 @@ void launch_leapfrog2(const Layout& l, const Coeffs& c, const double* prev, cons
 // marching in x, one workgroup per CU). Reads u^{n−1}, u^n; writes u^{n+S−1} into out1 and u^{n+S} into out2: 32/S
 // compulsory bytes per node-step. Same preconditions as launch_leapfrog2 with S−1 stage-1 planes beyond the box.
 // Error check of u^{n+k} when bit k−1 of `check_mask` is set (ct[k−1] = its time factor); stage k's partials go to
-// partials + (k−1)·leapfrog_tb_partials(). analytic_start: the pass starts at n = 1 from u⁰ = φ and u¹ computed in
+// partials + (k−1)·level_stride (0: leapfrog_tb_partials(), the launch's block count). analytic_start: the pass starts at n = 1 from u⁰ = φ and u¹ computed in
 // the kernel (init_first's formulas, bit-identical), prev/cur are not read: it writes u^S, u^{S+1} with no HBM reads.
 struct LeapfrogTbTiling {
   int stages = 4;         // 2, 3 or 4 steps per pass
@@ -87,7 +87,7 @@ int leapfrog_tb_partials(const Layout& l, const LBox& box, const LeapfrogTbTilin
 void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
                         double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
                         Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, i64 sx0 = 1, i64 sx1 = 0,
-                        bool analytic_start = false);
+                        bool analytic_start = false, int level_stride = 0);
 
 // Error of a stored field vs φ·ct over `box` (step 1 / standalone check). Writes leapfrog-compatible partials and
 // returns how many.

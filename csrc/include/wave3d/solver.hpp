@@ -40,7 +40,8 @@ struct SolverOptions {
   LeapfrogTiling tiling;
   // Temporal blocking: up to `temporal` (2..4) steps per HBM pass wherever no halo exchange intervenes. One rank:
   // k_leapfrog_tb passes (all levels in LDS, error checks at any level), the steps split into passes by measured
-  // per-step cost; slab ranks: two-step k_leapfrog2 passes with 2-deep halos. 1 = one step per pass everywhere.
+  // per-step cost; slab ranks: the same LDS passes with `temporal`-deep x halos (one exchange per pass; tb = false:
+  // two-step k_leapfrog2 passes with 2-deep halos). 1 = one step per pass everywhere.
   int temporal = 4;
   bool tb = true;  // one rank: LDS kernel (false: k_leapfrog2 pairs, only where the intermediate step has no check)
   Leapfrog2Tiling tiling2;
@@ -49,6 +50,9 @@ struct SolverOptions {
   bool init2 = true;
   // Slab ranks use the deep-halo fused schedule only from this many owned x-planes up (below, single steps are faster).
   int deep_min_planes = 96;
+  // Slab ranks use the LDS multi-step passes (deep-tb) when every rank owns at least this many x-planes (and at least
+  // 2·temporal: each pass first computes the `steps` planes next to each neighbour, the shells that are sent).
+  int tb_min_planes = 16;
 };
 
 // Summed device time per phase of the last run() (SolverOptions::timers). compute = interior / whole-box / fused
@@ -112,7 +116,8 @@ class GpuSolver {
   LBox interior_box() const { return interior_; }
   std::vector<int> check_steps() const;
   size_t device_bytes() const;
-  // "single-step" | "fused-single" (temporal blocking, one rank) | "deep-halo" (temporal blocking, slab ranks)
+  // "single-step" | "fused-single" (temporal blocking, one rank) | "deep-tb" (LDS multi-step passes, slab ranks)
+  // | "deep-halo" (two-step passes, slab ranks)
   std::string mode() const;
 
  private:
@@ -122,7 +127,7 @@ class GpuSolver {
   void gather_errors(RunResult& r);
   // Schedule: a solve is phase_init() followed by units; a unit advances one step (in place over u^{n−1}) or 2..4
   // (a fused pass into the two free buffers). Multi-rank units run shell -> exchange -> interior.
-  enum class Mode { kSingleStep, kFusedSingle, kDeep };
+  enum class Mode { kSingleStep, kFusedSingle, kDeep, kDeepTb };
   struct Unit {
     int n;      // current level u^n before the unit
     int steps;  // 1: in-place single step; >= 2: one fused pass writing u^{n+steps−1}, u^{n+steps}
@@ -141,12 +146,15 @@ class GpuSolver {
   bool needs_exchange(int i) const;
   hipStream_t xstream() const;
   bool pairable() const;
+  bool analytic_ok() const;  // the first unit can be an analytic-start LDS pass
   void build_units();
   void build_msgs(int i);
   void phase_init();
   void unit_shell(int i);
   void unit_exchange_rccl(int i);
   void unit_interior(int i);
+  void tb_pass(const Unit& u, const LBox& box, int phase);  // one k_leapfrog_tb launch of unit u over box
+  LBox tb_interior(int i) const;                            // deep-tb: the box left after unit i's shells
   void lb_pack(int i);
   void lb_pull(int i, const std::vector<GpuSolver*>& ranks);
   void lb_fence(int i, const std::vector<GpuSolver*>& ranks);
@@ -188,6 +196,9 @@ class GpuSolver {
   hipEvent_t ev_shell_ = nullptr, ev_halo_ = nullptr, ev_packed_ = nullptr;
   int n_full_ = 0, n_shell_ = 0, n_int_ = 0, n_fused_ = 0;  // error partials of each launch kind
   int n_tb_ = 0;                                            // ... per level of a k_leapfrog_tb pass
+  // deep-tb: per level, the partials of this unit's launches (shell lo, shell hi, interior) follow each other
+  int tb_slots_ = 0;                                        // launches of the current unit with partials so far
+  bool nb_lo_ = false, nb_hi_ = false;                      // x neighbours (slab ranks)
   int cur_ = 1, old_ = 0;                     // buffer roles during enqueue
   int start_n_ = 1;                           // first leapfrog step after the init kernel
   bool analytic_ = false;                     // the first unit computes u⁰, u¹ itself (no init kernel)

@@ -359,6 +359,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("temporal", &SolverOptions::temporal)
       .def_readwrite("init2", &SolverOptions::init2)
       .def_readwrite("deep_min_planes", &SolverOptions::deep_min_planes)
+      .def_readwrite("tb_min_planes", &SolverOptions::tb_min_planes)
       .def_readwrite("tiling2", &SolverOptions::tiling2)
       .def_readwrite("tb", &SolverOptions::tb)
       .def_readwrite("tiling_tb", &SolverOptions::tiling_tb)

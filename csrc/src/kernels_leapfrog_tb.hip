@@ -51,7 +51,7 @@ struct TbParams {
   double* out1;        // u^{n+S−1}
   double* out2;        // u^{n+S}
   const double* s;     // sin table, global index −1..N+1
-  Partial* partials;   // [S][nblocks]; stage k's block at (k−1)·nblocks (checked stages only)
+  Partial* partials;   // stage k's block of nblocks partials at (k−1)·lstride (checked stages only)
   i64 plane, pitch, zs;
   int x0, x1;          // output x range (local)
   int sx0, sx1;        // x range where stage outputs are real (outside: Dirichlet 0)
@@ -62,6 +62,7 @@ struct TbParams {
   double ct[4];        // time factor of u^{n+k} (k = 1..S) for the check
   int check_mask;      // bit k−1: check u^{n+k}
   int nty, ntz, nblocks, xcd_remap;
+  int lstride;         // partials between consecutive levels (≥ nblocks; larger when several launches share a level)
   int bby, bbz;        // > 0: each XCD's tiles form a bby × bbz block of the tile grid (else two-row strips)
 };
 
@@ -377,7 +378,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         mm = red_m[w] > mm ? red_m[w] : mm;
         ss += red_s[w];
       }
-      p.partials[k * p.nblocks + static_cast<int>(blockIdx.x)] = make_double2(mm, ss);
+      p.partials[k * p.lstride + static_cast<int>(blockIdx.x)] = make_double2(mm, ss);
     }
   }
 }
@@ -535,14 +536,14 @@ size_t leapfrog_tb_lds_bytes(int stages) {
 }
 
 int leapfrog_tb_partials(const Layout& l, const LBox& box, const LeapfrogTbTiling& t) {
-  const LBox full = compute_box(l);
-  return make_plan_tb(l, box, t, full.x0, full.x1).nblocks;
+  // the block count depends on the (y,z) tiling only: a stage range wide enough for any box passes the halo checks
+  return make_plan_tb(l, box, t, box.x0 - (t.stages - 1), box.x1 + (t.stages - 1)).nblocks;
 }
 
 void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
                         double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
                         Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, i64 sx0, i64 sx1,
-                        bool analytic_start) {
+                        bool analytic_start, int level_stride) {
   W3D_REQUIRE(out1 != out2 && (analytic_start || (prev != out1 && prev != out2 && cur != out1 && cur != out2)),
               "leapfrog_tb needs four distinct buffers");
   if (sx0 > sx1) {
@@ -566,6 +567,8 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
   p.half_tau2 = c.half_tau2;
   p.check_mask = partials != nullptr ? (check_mask & ((1 << t.stages) - 1)) : 0;
   p.partials = p.check_mask != 0 ? partials : nullptr;
+  W3D_REQUIRE(level_stride == 0 || level_stride >= pl.nblocks, "leapfrog_tb: level stride below the block count");
+  p.lstride = level_stride > 0 ? level_stride : pl.nblocks;
   for (int k = 0; k < 4; ++k) p.ct[k] = (ct != nullptr && k < t.stages) ? ct[k] : 0.0;
   switch (t.stages) {
     case 2: launch_s<2>(p, pl.nblocks, t, analytic_start, stream); break;

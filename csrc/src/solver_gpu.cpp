@@ -92,17 +92,24 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   const Box box = rank_box(prob_, dims_, rank);
   W3D_REQUIRE(box.nx() >= 1 && box.ny() >= 1 && box.nz() >= 1,
               "decomposition leaves a rank without nodes; use fewer ranks or a larger N");
-  // schedule mode: temporal blocking on one rank, or on a 1-D slab decomposition with 2-deep x halos
+  // schedule mode: temporal blocking on one rank, or on a 1-D slab decomposition with `temporal`-deep x halos (LDS
+  // passes) or 2-deep ones (two-step passes). Decided from the SMALLEST rank box so every rank picks the same mode.
   mode_ = Mode::kSingleStep;
   W3D_REQUIRE(opt_.temporal >= 1 && opt_.temporal <= 4, "temporal must be 1..4");
   if (opt_.temporal >= 2 && world == 1) mode_ = Mode::kFusedSingle;
-  // (measured with --fake-rank on 512³: the fused pass wins from ~128 local planes up, but at 64 planes the two
-  // 2-plane shell passes and the per-chunk stage-1 recompute cost more than the saved traffic)
-  if (opt_.temporal >= 2 && world > 1 && dims_.py == 1 && dims_.pz == 1 && box.nx() >= opt_.deep_min_planes &&
-      box.nx() >= 3 && pairable())
-    mode_ = Mode::kDeep;
+  if (opt_.temporal >= 2 && world > 1 && dims_.py == 1 && dims_.pz == 1) {
+    i64 min_nx = box.nx();
+    for (int r = 0; r < world; ++r) min_nx = imin(min_nx, rank_box(prob_, dims_, r).nx());
+    const int rem = prob_.K - (analytic_ok() ? 1 : 2);  // steps left to the passes (each takes 2..temporal)
+    if (opt_.tb && opt_.init2 && rem >= 2 && min_nx >= imax(opt_.tb_min_planes, 2 * opt_.temporal))
+      mode_ = Mode::kDeepTb;
+    // (two-step passes, measured with --fake-rank on 512³: they win from ~128 local planes up, but at 64 planes the
+    // two 2-plane shell passes and the per-chunk stage-1 recompute cost more than the saved traffic)
+    else if (min_nx >= opt_.deep_min_planes && min_nx >= 3 && pairable())
+      mode_ = Mode::kDeep;
+  }
   for (int attempt = 0; attempt < 2; ++attempt) {
-    lay_ = make_layout(prob_, box, 16, mode_ == Mode::kDeep ? 2 : 1);
+    lay_ = make_layout(prob_, box, 16, mode_ == Mode::kDeep ? 2 : mode_ == Mode::kDeepTb ? opt_.temporal : 1);
     // memory plan: temporal blocking needs four field buffers; fall back to the two-buffer in-place scheme when four
     // do not fit next to the other allocations (2049³ fp64 is 68.8 GB per buffer)
     size_t free_b = 0, total_b = 0;
@@ -163,6 +170,14 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
     sx0_ = full_.x0 - (nb[0][0] ? 1 : 0);
     sx1_ = full_.x1 + (nb[0][1] ? 1 : 0);
   }
+  // deep-tb slab: stage values are real up to temporal − 1 planes beyond each neighbour face (recomputed from the
+  // temporal-deep halo); the shell/interior split depends on the next pass's depth and is made per unit
+  nb_lo_ = nb[0][0];
+  nb_hi_ = nb[0][1];
+  if (mode_ == Mode::kDeepTb) {
+    sx0_ = full_.x0 - (nb_lo_ ? opt_.temporal - 1 : 0);
+    sx1_ = full_.x1 + (nb_hi_ ? opt_.temporal - 1 : 0);
+  }
 
   // device memory
   W3D_HIP(hipStreamCreateWithFlags(&s0_, hipStreamNonBlocking));
@@ -192,9 +207,9 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   n_shell_ = leapfrog_blocks(lay_, shell_.data(), static_cast<int>(shell_.size()), opt_.tiling);
   n_int_ = leapfrog_blocks(lay_, &interior_, 1, opt_.tiling);
   n_fused_ = (mode_ == Mode::kFusedSingle && !full_.empty()) ? leapfrog2_partials(lay_, full_, opt_.tiling2) : 0;
-  if (mode_ == Mode::kFusedSingle && opt_.tb && !full_.empty()) {
+  if ((mode_ == Mode::kFusedSingle || mode_ == Mode::kDeepTb) && opt_.tb && !full_.empty()) {
     LeapfrogTbTiling t = opt_.tiling_tb;
-    t.stages = 4;  // partials per level do not depend on the stage count
+    t.stages = opt_.temporal;  // partials per level do not depend on the stage count
     n_tb_ = leapfrog_tb_partials(lay_, full_, t);
     leapfrog_tb_prepare();
   }
@@ -205,7 +220,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   }
   n_dint_ = dint_.empty() ? 0 : leapfrog2_partials(lay_, dint_, opt_.tiling2);
   n_deep += n_dint_;
-  n_partials_ = std::max({n_full_, n_shell_ + n_int_, error_blocks(lay_, full_), n_fused_, n_deep, 4 * n_tb_,
+  n_partials_ = std::max({n_full_, n_shell_ + n_int_, error_blocks(lay_, full_), n_fused_, n_deep, 4 * 3 * n_tb_,
                           opt_.init2 ? init_two_partials(lay_) : 0, 1});
   W3D_HIP(hipMalloc(&partials_, static_cast<size_t>(n_partials_) * sizeof(Partial)));
   W3D_HIP(hipMalloc(&errlog_, static_cast<size_t>(prob_.K + 1) * sizeof(Partial)));
@@ -247,6 +262,7 @@ std::string GpuSolver::mode() const {
   switch (mode_) {
     case Mode::kFusedSingle: return "fused-single";
     case Mode::kDeep: return "deep-halo";
+    case Mode::kDeepTb: return "deep-tb";
     default: return "single-step";
   }
 }
@@ -255,7 +271,7 @@ std::string GpuSolver::mode() const {
 // schedule
 // ------------------------------------------------------------------------------------------------------------------
 bool GpuSolver::split() const { return opt_.overlap && plan_.any(); }
-bool GpuSolver::post_exchange() const { return mode_ == Mode::kDeep || split(); }
+bool GpuSolver::post_exchange() const { return mode_ == Mode::kDeep || mode_ == Mode::kDeepTb || split(); }
 
 bool GpuSolver::needs_exchange(int i) const {
   if (!plan_.any()) return false;
@@ -274,22 +290,30 @@ bool GpuSolver::pairable() const {
   return true;
 }
 
+bool GpuSolver::analytic_ok() const {
+  if (!opt_.tb || !opt_.init2 || opt_.temporal < 2 || prob_.K < 3) return false;
+  for (int n : check_steps())
+    if (n == 1) return false;  // u¹ is the pass's input level: it cannot carry a check
+  return true;
+}
+
 void GpuSolver::build_units() {
   units_.clear();
   const int K = prob_.K;
   int n = start_n_;
-  if (mode_ == Mode::kFusedSingle && opt_.tb) {
+  if ((mode_ == Mode::kFusedSingle && opt_.tb) || mode_ == Mode::kDeepTb) {
     // split the K − n remaining steps into passes of 1..temporal steps minimising the summed cost: µs per step of a
     // pass of s steps with every 2nd level checked, measured at 512³ (tools/tune_leapfrog.py --tb); the analytic
-    // first pass reads nothing but computes u⁰, u¹ (compute-bound)
+    // first pass reads nothing but computes u⁰, u¹ (compute-bound). Slab ranks (deep-tb) take passes of ≥ 2 steps
+    // only: every pass writes the two levels the next one reads, so each exchange is one message pair per face.
     static const double kStepCost[5] = {0.0, 610.0, 451.0, 310.0, 283.0};
     static const double kAnalyticCost[5] = {0.0, 1e9, 380.0, 328.0, 306.0};
-    const int rem = K - n, smax = opt_.temporal;
+    const int rem = K - n, smax = opt_.temporal, smin = mode_ == Mode::kDeepTb ? 2 : 1;
     std::vector<double> best(static_cast<size_t>(rem + 1), 1e300);
     std::vector<int> take(static_cast<size_t>(rem + 1), 1);
     best[0] = 0.0;
     for (int r = 1; r <= rem; ++r)
-      for (int st = 1; st <= std::min(smax, r); ++st) {
+      for (int st = smin; st <= std::min(smax, r); ++st) {
         const double c = best[static_cast<size_t>(r - st)] + st * kStepCost[st];
         if (c < best[static_cast<size_t>(r)]) {
           best[static_cast<size_t>(r)] = c;
@@ -310,6 +334,7 @@ void GpuSolver::build_units() {
       units_.push_back(Unit{n, bf, true});
       n += bf;
     }
+    W3D_REQUIRE(best[static_cast<size_t>(K - n)] < 1e299, "no pass schedule for the remaining steps");
     for (int r = K - n; r > 0; r -= take[static_cast<size_t>(r)]) {
       units_.push_back(Unit{n, take[static_cast<size_t>(r)]});
       n += take[static_cast<size_t>(r)];
@@ -329,6 +354,20 @@ void GpuSolver::build_units() {
 
 void GpuSolver::build_msgs(int i) {
   msgs_.clear();
+  if (mode_ == Mode::kDeepTb) {
+    // the next pass of s steps reads u^{n+S} (this pass's out2) on s ghost planes and u^{n+S−1} (out1) on s − 1
+    const i64 s = units_[static_cast<size_t>(i) + 1].steps, P = lay_.plane, nx = lay_.nx;
+    double* out1 = u_[uf_[0]];
+    double* out2 = u_[uf_[1]];
+    for (const Face& f : plan_.faces) {
+      W3D_REQUIRE(f.axis == 0, "deep-tb mode is slab-only");
+      const i64 s2 = f.side == 0 ? 0 : nx - s, s1 = f.side == 0 ? 0 : nx - (s - 1);
+      const i64 r2 = f.side == 0 ? -s : nx, r1 = f.side == 0 ? -(s - 1) : nx;
+      msgs_.push_back(Msg{f.peer, 0, out2 + lay_.plane_off(s2), out2 + lay_.plane_off(r2), s * P});
+      msgs_.push_back(Msg{f.peer, 1, out1 + lay_.plane_off(s1), out1 + lay_.plane_off(r1), (s - 1) * P});
+    }
+    return;
+  }
   if (mode_ == Mode::kDeep) {
     // after a fused pass the next one needs u^{n+2} on 2 ghost planes and u^{n+1} on 1 (x faces of a slab rank)
     double* out1 = u_[uf_[0]];
@@ -388,7 +427,7 @@ void GpuSolver::phase_init() {
   marks_.clear();
   W3D_HIP(hipMemsetAsync(errlog_, 0, static_cast<size_t>(K + 1) * sizeof(Partial), s0_));
   // one rank on the LDS kernel: the first pass starts from the analytic u⁰, u¹ itself (no init kernel, no reads)
-  analytic_ = mode_ == Mode::kFusedSingle && opt_.tb && opt_.init2 && opt_.temporal >= 2 && K >= 3 && !is_check_[1];
+  analytic_ = (mode_ == Mode::kFusedSingle || mode_ == Mode::kDeepTb) && analytic_ok();
   if (analytic_) {
     start_n_ = 1;
   } else if (opt_.init2 && K >= 2) {
@@ -437,6 +476,16 @@ void GpuSolver::unit_shell(int i) {
       });
       off += n_dshell_[k];
     }
+  } else if (mode_ == Mode::kDeepTb) {
+    // the planes the neighbours receive first: as many as the next pass is deep, next to each neighbour face
+    tb_slots_ = 0;
+    if (needs_exchange(i)) {
+      const i64 w = units_[static_cast<size_t>(i) + 1].steps;
+      if (nb_lo_) tb_pass(u, LBox{full_.x0, imin(full_.x0 + w, full_.x1), full_.y0, full_.y1, full_.z0, full_.z1},
+                          kPhaseShell);
+      if (nb_hi_) tb_pass(u, LBox{imax(full_.x1 - w, full_.x0), full_.x1, full_.y0, full_.y1, full_.z0, full_.z1},
+                          kPhaseShell);
+    }
   } else if (mode_ == Mode::kSingleStep && split()) {
     timed(kPhaseShell, s0_, [&] {
       launch_leapfrog(lay_, coef_, u_[cur_], u_[old_], shell_.data(), static_cast<int>(shell_.size()), d_s_ + 1,
@@ -474,6 +523,38 @@ void GpuSolver::unit_exchange_rccl(int i) {
   if (xs != s0_) W3D_HIP(hipEventRecord(ev_halo_, xs));
 }
 
+// One LDS S-step pass of unit u over `box`. Its checked levels' partials go to slot tb_slots_ of each level: one slot
+// per level on one rank, three on slab ranks (shell lo, shell hi, interior), reduced together after the interior.
+void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase) {
+  LeapfrogTbTiling t = opt_.tiling_tb;
+  t.stages = u.steps;
+  double cts[4] = {0, 0, 0, 0};
+  int mask = 0;
+  for (int k = 1; k <= u.steps; ++k) {
+    cts[k - 1] = ct_[static_cast<size_t>(u.n + k)];
+    if (is_check_[static_cast<size_t>(u.n + k)]) mask |= 1 << (k - 1);
+  }
+  const int slots = mode_ == Mode::kDeepTb ? 3 : 1;
+  W3D_REQUIRE(tb_slots_ < slots, "leapfrog_tb: too many launches in one unit");
+  Partial* part = mask ? partials_ + tb_slots_ * n_tb_ : nullptr;
+  const i64 sx0 = mode_ == Mode::kDeepTb ? sx0_ : 1, sx1 = mode_ == Mode::kDeepTb ? sx1_ : 0;
+  timed(phase, s0_, [&] {
+    launch_leapfrog_tb(lay_, coef_, u_[old_], u_[cur_], u_[uf_[0]], u_[uf_[1]], box, d_s_ + 1, cts, mask, part, t,
+                       s0_, sx0, sx1, u.analytic, slots * n_tb_);
+  });
+  if (mask) ++tb_slots_;
+}
+
+LBox GpuSolver::tb_interior(int i) const {
+  LBox b = full_;
+  if (needs_exchange(i)) {
+    const i64 w = units_[static_cast<size_t>(i) + 1].steps;
+    if (nb_lo_) b.x0 = imin(b.x0 + w, b.x1);
+    if (nb_hi_) b.x1 = imax(b.x1 - w, b.x0);
+  }
+  return b;
+}
+
 void GpuSolver::unit_interior(int i) {
   const Unit& u = units_[static_cast<size_t>(i)];
   const int nc = u.n + u.steps;
@@ -492,25 +573,18 @@ void GpuSolver::unit_interior(int i) {
       });
     }
     np = off + n_dint_;
-  } else if (mode_ == Mode::kFusedSingle && opt_.tb && u.fused()) {
-    // S steps in one LDS pass; every checked level has its own block of partials
-    LeapfrogTbTiling t = opt_.tiling_tb;
-    t.stages = u.steps;
-    double cts[4] = {0, 0, 0, 0};
-    int mask = 0;
-    for (int k = 1; k <= u.steps; ++k) {
-      cts[k - 1] = ct_[static_cast<size_t>(u.n + k)];
-      if (is_check_[static_cast<size_t>(u.n + k)]) mask |= 1 << (k - 1);
-    }
-    timed(kPhaseCompute, s0_, [&] {
-      launch_leapfrog_tb(lay_, coef_, u_[old_], u_[cur_], u_[uf_[0]], u_[uf_[1]], full_, s, cts, mask,
-                         mask ? partials_ : nullptr, t, s0_, 1, 0, u.analytic);
-    });
-    if (mask) {
+  } else if ((mode_ == Mode::kFusedSingle && opt_.tb && u.fused()) || mode_ == Mode::kDeepTb) {
+    // S steps in one LDS pass (on slab ranks: the interior left between this unit's shells); every checked level
+    // has its own block of partials
+    if (mode_ != Mode::kDeepTb) tb_slots_ = 0;
+    const LBox b = mode_ == Mode::kDeepTb ? tb_interior(i) : full_;
+    if (!b.empty()) tb_pass(u, b, kPhaseCompute);
+    const int slots = mode_ == Mode::kDeepTb ? 3 : 1;
+    if (tb_slots_ > 0) {
       timed(kPhaseCheck, s0_, [&] {
         for (int k = 1; k <= u.steps; ++k)
-          if (mask >> (k - 1) & 1)
-            launch_reduce(partials_ + (k - 1) * n_tb_, n_tb_, errlog_ + u.n + k, s0_);
+          if (is_check_[static_cast<size_t>(u.n + k)])
+            launch_reduce(partials_ + (k - 1) * slots * n_tb_, tb_slots_ * n_tb_, errlog_ + u.n + k, s0_);
       });
     }
   } else if (mode_ == Mode::kFusedSingle) {

@@ -75,7 +75,8 @@ class Solver:
                  comm=None, group=None, stage_via_host: bool = False, force: bool = False, temporal: int = 4,
                  tiling2: dict | None = None, init2: bool = True, timers: bool = False, tb: bool = True,
                  tiling_tb: dict | None = None,
-                 debug_sync: bool = False, poison_ghosts: bool = False, deep_min_planes: int | None = None):
+                 debug_sync: bool = False, poison_ghosts: bool = False, deep_min_planes: int | None = None,
+                 tb_min_planes: int | None = None):
         import torch.distributed as dist
 
         if not spec.cfl_ok and not force:
@@ -105,6 +106,8 @@ class Solver:
             opts.timers, opts.debug_sync, opts.poison_ghosts = timers, debug_sync, poison_ghosts
             if deep_min_planes is not None:
                 opts.deep_min_planes = deep_min_planes
+            if tb_min_planes is not None:
+                opts.tb_min_planes = tb_min_planes
             self._impl = C.GpuGroup(spec.native(), opts, world)
             self.dims = self._impl.dims().as_tuple()
         elif self.backend == "hip" and self.transport == "rccl":
@@ -114,6 +117,8 @@ class Solver:
             opts.timers, opts.debug_sync, opts.poison_ghosts = timers, debug_sync, poison_ghosts
             if deep_min_planes is not None:
                 opts.deep_min_planes = deep_min_planes
+            if tb_min_planes is not None:
+                opts.tb_min_planes = tb_min_planes
             if comm is None and world > 1:
                 comm = make_comm(rank, world, group)
             self.comm = comm

@@ -133,7 +133,7 @@ def test_deep_halo_temporal_blocking_bitexact(gpu, single_even, world, overlap):
     bit-identical to one GPU, also with NaN-poisoned ghosts."""
     spec, r1, f0, f1 = single_even
     g = Solver(spec, backend="hip", transport="loopback", world=world, rank=0, decomp="slab", overlap=overlap,
-               device=0, poison_ghosts=True, deep_min_planes=3)
+               device=0, poison_ghosts=True, deep_min_planes=3, tb=False)
     assert g.native.mode() == "deep-halo"
     r = g.run()
     assert r.steps == r1.steps and r.max_err == r1.max_err
@@ -141,6 +141,30 @@ def test_deep_halo_temporal_blocking_bitexact(gpu, single_even, world, overlap):
         assert math.isclose(a, b, rel_tol=1e-12)
     assert torch.equal(g.global_field(0), f0)
     assert torch.equal(g.global_field(1), f1)
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+@pytest.mark.parametrize("K,check_every,temporal", [(10, 2, 4), (20, 2, 4), (9, 1, 4), (12, 3, 3), (11, 2, 2)])
+def test_deep_tb_bitexact(gpu, world, overlap, K, check_every, temporal):
+    """Slab ranks on the LDS S-step kernel with S-deep x halos: each pass computes the planes its neighbours need
+    first (shells), sends S planes of u^{n+S} and S−1 of u^{n+S−1} per face on the side stream while the interior
+    pass runs. Bit-identical to one GPU, with NaN-poisoned ghosts; odd-level checks and a checked step 1 (no
+    analytic start) included."""
+    spec = ProblemSpec(N=66, tau=1e-3, K=K, check_every=check_every)
+    ref = Solver(spec, backend="hip", device=0, temporal=1)
+    r1 = ref.run()
+    f0, f1 = ref.global_field(0), ref.global_field(1)
+    g = Solver(spec, backend="hip", transport="loopback", world=world, rank=0, decomp="slab", overlap=overlap,
+               device=0, poison_ghosts=True, tb_min_planes=2 * temporal, temporal=temporal)
+    assert g.native.mode() == "deep-tb"
+    for _ in range(2):
+        r = g.run()
+        assert r.finite and r.steps == r1.steps and r.max_err == r1.max_err
+        for a, b in zip(r.rms_err, r1.rms_err):
+            assert math.isclose(a, b, rel_tol=1e-12)
+        assert torch.equal(g.global_field(0), f0)
+        assert torch.equal(g.global_field(1), f1)
 
 
 def test_schedule_modes(gpu):
@@ -151,8 +175,14 @@ def test_schedule_modes(gpu):
     assert Solver(even, backend="hip", transport="loopback", world=4, rank=0, decomp="2x2x1",
                   device=0).native.mode() == "single-step"
     assert Solver(odd_check, backend="hip", transport="loopback", world=2, rank=0, decomp="slab",
-                  device=0, deep_min_planes=3).native.mode() == "single-step"
+                  device=0, deep_min_planes=3, tb=False).native.mode() == "single-step"  # odd checks: no pairs
+    assert Solver(odd_check, backend="hip", transport="loopback", world=2, rank=0, decomp="slab",
+                  device=0).native.mode() == "deep-tb"  # the LDS passes check any level
     assert Solver(even, backend="hip", transport="loopback", world=2, rank=0, decomp="slab",
-                  device=0, deep_min_planes=3).native.mode() == "deep-halo"
+                  device=0, deep_min_planes=3, tb=False).native.mode() == "deep-halo"
     assert Solver(even, backend="hip", transport="loopback", world=2, rank=0, decomp="slab",
-                  device=0).native.mode() == "single-step"  # 20 planes per rank < default 96
+                  device=0, tb=False).native.mode() == "single-step"  # 20 planes per rank < default 96
+    assert Solver(even, backend="hip", transport="loopback", world=2, rank=0, decomp="slab",
+                  device=0).native.mode() == "deep-tb"  # 20 planes per rank >= default 16
+    assert Solver(even, backend="hip", transport="loopback", world=4, rank=0, decomp="slab",
+                  device=0).native.mode() == "single-step"  # 10 planes per rank < 16

@@ -56,7 +56,7 @@ struct Args {
   int variant = -1;
   int target_blocks = 0;
   int nt_store = -1;
-  std::string json, dump;
+  std::string json, dump, trace;
   bool quiet = false;
 };
 
@@ -91,6 +91,7 @@ struct Args {
                "  --target-blocks B  x-chunking target (waves for v1, workgroups for v0)\n"
                "  --nt-store 0/1     non-temporal stores of u^{n+1} (default 1)\n"
                "  --json PATH        machine-readable summary (rank 0)\n"
+               "  --trace PATH       per-unit device times as JSON lines (PATH[.rankR] per rank; implies --timers)\n"
                "  --dump PREFIX      write u^K: PREFIX[.rankR].bin (fp64, C order, owned nodes) + .json\n"
                "  --force            run even if the CFL condition is violated\n"
                "  --quiet            only the summary\n");
@@ -138,6 +139,10 @@ Args parse(int argc, char** argv) {
     else if (s == "--target-blocks") a.target_blocks = std::stoi(next());
     else if (s == "--nt-store") a.nt_store = std::stoi(next());
     else if (s == "--json") a.json = next();
+    else if (s == "--trace") {
+      a.trace = next();
+      a.timers = true;
+    }
     else if (s == "--dump") a.dump = next();
     else if (s == "--force") a.force = true;
     else if (s == "--quiet") a.quiet = true;
@@ -392,6 +397,15 @@ int run_gpu(const Args& a) {
         j << (i ? ", " : "") << "[" << r.steps[i] << ", " << r.max_err[i] << ", " << r.rms_err[i] << "]";
       j << "]}\n";
     }
+  }
+  if (!a.trace.empty()) {  // per-unit device times of the last run, one JSON object per line
+    const std::string path = world > 1 ? a.trace + ".rank" + std::to_string(rank) : a.trace;
+    std::ofstream t(path);
+    t.precision(6);
+    for (const UnitTrace& u : r.trace)
+      t << "{\"rank\": " << rank << ", \"unit\": " << u.unit << ", \"n\": " << u.n << ", \"steps\": " << u.steps
+        << ", \"schedule\": \"" << s.mode() << "\", \"shell_ms\": " << u.shell_ms << ", \"comm_ms\": " << u.comm_ms
+        << ", \"compute_ms\": " << u.compute_ms << ", \"check_ms\": " << u.check_ms << "}\n";
   }
   if (!a.dump.empty()) write_dump(a.dump, a.prob, s.layout(), s.download(0), rank, world, d);
   (void)free_b;

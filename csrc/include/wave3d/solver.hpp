@@ -61,12 +61,20 @@ struct PhaseTimes {
   double init_ms = 0, shell_ms = 0, interior_ms = 0, comm_ms = 0, check_ms = 0, gather_ms = 0;
 };
 
+// Device time of one schedule unit (SolverOptions::timers; --trace): shell = the boundary part computed first,
+// comm = its exchange (side stream, overlapping compute), compute = the rest, check = error reductions.
+struct UnitTrace {
+  int unit = 0, n = 0, steps = 0;
+  double shell_ms = 0, comm_ms = 0, compute_ms = 0, check_ms = 0;
+};
+
 struct RunResult {
   std::vector<int> steps;         // checked steps
   std::vector<double> max_err;    // L∞ (global)
   std::vector<double> rms_err;    // sqrt(Σe² / (N−1)³) (global)
   double solve_s = 0.0;           // host wall time of run(): field init → last error gathered
   PhaseTimes phases;              // only with SolverOptions::timers
+  std::vector<UnitTrace> trace;   // per unit, only with SolverOptions::timers
   bool finite = true;
 };
 
@@ -208,9 +216,10 @@ class GpuSolver {
   // per-phase timers
   enum { kPhaseInit = 0, kPhaseShell, kPhaseCompute, kPhaseComm, kPhaseCheck, kNumPhases };
   struct Mark {
-    int phase;
+    int phase, unit;  // unit −1: init
     hipEvent_t b, e;
   };
+  int cur_unit_ = -1;
   std::vector<hipEvent_t> ev_pool_;
   size_t ev_next_ = 0;
   std::vector<Mark> marks_;

@@ -50,6 +50,19 @@ py::dict result_dict(const RunResult& r) {
   ph["check_ms"] = r.phases.check_ms;
   ph["gather_ms"] = r.phases.gather_ms;
   d["phases"] = ph;
+  py::list tr;
+  for (const UnitTrace& t : r.trace) {
+    py::dict u;
+    u["unit"] = t.unit;
+    u["n"] = t.n;
+    u["steps"] = t.steps;
+    u["shell_ms"] = t.shell_ms;
+    u["comm_ms"] = t.comm_ms;
+    u["compute_ms"] = t.compute_ms;
+    u["check_ms"] = t.check_ms;
+    tr.append(u);
+  }
+  d["trace"] = tr;
   return d;
 }
 

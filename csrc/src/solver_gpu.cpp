@@ -2,6 +2,7 @@
 #include "wave3d/solver.hpp"
 
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <chrono>
@@ -394,15 +395,21 @@ void GpuSolver::build_msgs(int i) {
 }
 
 // Per-phase device timers (SolverOptions::timers, eager launches only): every timed launch group is bracketed by two
-// events on its stream; after the solve the intervals are summed per phase. The reference reports its GPU time as
-// compute / H2D-D2H copies / MPI exchange (report.pdf p.16 §4.4); here: init, compute (shell + interior / fused),
-// exchange (pack + RCCL + unpack, overlapped with compute on the side stream) and error check (reductions).
+// events on its stream; after the solve the intervals are summed per phase (and per unit for --trace). The reference
+// reports its GPU time as compute / H2D-D2H copies / MPI exchange (report.pdf p.16 §4.4); here: init, compute (shell
+// + interior / fused), exchange (pack + RCCL + unpack, overlapped with compute on the side stream) and error check
+// (reductions). Each group is also a roctx range ("w3d:<phase>:u<unit>"), so rocprofv3 --marker-trace timelines
+// show the schedule.
 template <class F>
 void GpuSolver::timed(int phase, hipStream_t st, F&& f) {
   if (!opt_.timers) {
     f();
     return;
   }
+  static const char* const kNames[kNumPhases] = {"init", "shell", "compute", "exchange", "check"};
+  char label[48];
+  std::snprintf(label, sizeof label, "w3d:%s:u%d", kNames[phase], cur_unit_);
+  roctxRangePushA(label);
   auto take = [&]() {
     if (ev_next_ == ev_pool_.size()) {
       hipEvent_t e;
@@ -415,7 +422,8 @@ void GpuSolver::timed(int phase, hipStream_t st, F&& f) {
   W3D_HIP(hipEventRecord(a, st));
   f();
   W3D_HIP(hipEventRecord(b, st));
-  marks_.push_back({phase, a, b});
+  roctxRangePop();
+  marks_.push_back({phase, cur_unit_, a, b});
 }
 
 void GpuSolver::phase_init() {
@@ -423,6 +431,7 @@ void GpuSolver::phase_init() {
   const double* s = d_s_ + 1;
   is_check_.assign(static_cast<size_t>(K + 1), 0);
   for (int n : check_steps()) is_check_[static_cast<size_t>(n)] = 1;
+  cur_unit_ = -1;
   ev_next_ = 0;
   marks_.clear();
   W3D_HIP(hipMemsetAsync(errlog_, 0, static_cast<size_t>(K + 1) * sizeof(Partial), s0_));
@@ -459,6 +468,7 @@ void GpuSolver::phase_init() {
 }
 
 void GpuSolver::unit_shell(int i) {
+  cur_unit_ = i;
   const Unit& u = units_[static_cast<size_t>(i)];
   if (u.fused()) {
     int k = 0;
@@ -644,10 +654,20 @@ void GpuSolver::poison(hipStream_t st) {
 void GpuSolver::collect_phases(RunResult& r) {
   if (!opt_.timers) return;
   double acc[kNumPhases] = {0, 0, 0, 0, 0};
+  r.trace.assign(units_.size(), UnitTrace{});
+  for (size_t i = 0; i < units_.size(); ++i) {
+    r.trace[i].unit = static_cast<int>(i);
+    r.trace[i].n = units_[i].n;
+    r.trace[i].steps = units_[i].steps;
+  }
   for (const auto& m : marks_) {
     float ms = 0.0f;
     W3D_HIP(hipEventElapsedTime(&ms, m.b, m.e));
     acc[m.phase] += ms;
+    if (m.unit < 0 || m.unit >= static_cast<int>(r.trace.size())) continue;
+    UnitTrace& t = r.trace[static_cast<size_t>(m.unit)];
+    (m.phase == kPhaseShell ? t.shell_ms : m.phase == kPhaseComm ? t.comm_ms : m.phase == kPhaseCheck ? t.check_ms
+                                                                                                 : t.compute_ms) += ms;
   }
   r.phases.init_ms = acc[kPhaseInit];
   r.phases.shell_ms = acc[kPhaseShell];

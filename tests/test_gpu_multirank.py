@@ -116,6 +116,25 @@ def test_phase_timers(gpu, tb):
     assert (ph["init_ms"] == 0) if tb else (ph["init_ms"] > 0)
     ref = Solver(spec, backend="hip", device=0, tb=tb).run()
     assert r.max_err == ref.max_err
+    # per-unit trace: the units cover every step after the init, and their compute sums to the phase total
+    tr = r.extra["trace"]
+    assert tr and tr[-1]["n"] + tr[-1]["steps"] == spec.K
+    assert all(a["n"] + a["steps"] == b["n"] for a, b in zip(tr, tr[1:]))
+    assert math.isclose(sum(u["compute_ms"] for u in tr), ph["compute_ms"], rel_tol=1e-6)
+
+
+def test_cli_trace_deep_tb(gpu, tmp_path):
+    """--trace on a fake slab rank (deep-tb schedule): one JSON line per pass with shell, exchange and compute."""
+    import json
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "trace.jsonl"
+    subprocess.run([os.path.join(root, "bin", "wave3d"), "128", "0.001", "20", "1", "--fake-rank", "1/3",
+                    "--trace", str(out), "--quiet"], check=True, timeout=120)
+    rows = [json.loads(x) for x in (tmp_path / "trace.jsonl.rank1").read_text().splitlines()]  # per-rank file
+    assert rows and all(r["schedule"] == "deep-tb" for r in rows)
+    assert rows[0]["n"] == 1 and rows[-1]["n"] + rows[-1]["steps"] == 20
+    assert all(r["shell_ms"] > 0 for r in rows[:-1]) and rows[-1]["shell_ms"] == 0  # no exchange after the last
 
 
 @pytest.fixture(scope="module")

@@ -94,7 +94,7 @@ def _link(objs: list[Path], out: Path, shared: bool, verbose: bool) -> None:
     out.parent.mkdir(parents=True, exist_ok=True)
     rocm_lib = ROCM / "lib"
     cmd = [HIPCC, f"--offload-arch={ARCH}", *map(str, objs), "-o", str(out) + ".tmp",
-           f"-L{rocm_lib}", "-lrccl", "-lamdhip64", "-lgomp", "-lpthread", f"-Wl,-rpath,{rocm_lib}"]
+           f"-L{rocm_lib}", "-lrccl", "-lrocprofiler-sdk-roctx", "-lamdhip64", "-lgomp", "-lpthread", f"-Wl,-rpath,{rocm_lib}"]
     if shared:
         cmd.insert(1, "-shared")
     if verbose:

@@ -276,13 +276,15 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     };
 
     // stage k at plane xp; D = (xp − i0) & 3 (static), parity of xp = D & 1
-    auto stage = [&](auto kc, auto dc, int xp) {
+    // BK (bulk): plane xp is real and owned for every stage (the x tests are compile-time true)
+    auto stage = [&](auto kc, auto dc, auto bkc, int xp) {
       constexpr int k = decltype(kc)::value, D = decltype(dc)::value;
+      constexpr bool BK = decltype(bkc)::value;
       constexpr int sm = (D + 3) & 3, s0 = D, sp = (D + 1) & 3;
       const double* nb = lds_plane(k - 1, D & 1);
       double* dst = lds_plane(k < S ? k : 0, D & 1);
-      const bool xreal = xp >= p.sx0 && xp < p.sx1 && inside(p.gx0 + xp);
-      const bool xown = xp >= x0 && xp < x1;
+      const bool xreal = BK || (xp >= p.sx0 && xp < p.sx1 && inside(p.gx0 + xp));
+      const bool xown = BK || (xp >= x0 && xp < x1);
       constexpr bool kChk = (CM >> (k - 1)) & 1;
       const bool chk = kChk && ((p.check_mask >> (k - 1)) & 1);
       double* outp = (k == S ? p.out2 : p.out1) + static_cast<i64>(xp + 1) * P;
@@ -322,8 +324,9 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     };
 
     // iteration i with phase F = (i − i0) & 3
-    auto iteration = [&](auto fc, int i) {
+    auto iteration = [&](auto fc, auto bkc, int i) {
       constexpr int F = decltype(fc)::value;
+      constexpr bool BK = decltype(bkc)::value;
       __syncthreads();  // every read of the slots overwritten below (iteration i−1) is done; i−1's writes visible
       commit_cur(std::integral_constant<int, (F + 1) & 3>{}, std::integral_constant<int, (F + 1) & 1>{},
                  (F + 1) & 1);  // u^n plane i+1 → LDS (loaded one iteration ago)
@@ -332,8 +335,8 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
 #define W3D_TB_STAGE(K)                                                                                          \
   if constexpr (K <= S) {                                                                                        \
     const int xp = i - (K - 1);                                                                                  \
-    if (xp >= x0 - (S - K) && xp < x1 + (S - K))                                                                 \
-      stage(std::integral_constant<int, K>{}, std::integral_constant<int, (F - (K - 1) + 8) & 3>{}, xp);         \
+    if (BK || (xp >= x0 - (S - K) && xp < x1 + (S - K)))                                                         \
+      stage(std::integral_constant<int, K>{}, std::integral_constant<int, (F - (K - 1) + 8) & 3>{}, bkc, xp);    \
   }
       W3D_TB_STAGE(1)
       W3D_TB_STAGE(2)
@@ -348,14 +351,49 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     commit_cur(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0);
     load_cur(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, i0 + 1);
     load_prev(std::integral_constant<int, 0>{}, i0);
-    for (int ib = i0; ib <= i1; ib += 4) {
-      iteration(std::integral_constant<int, 0>{}, ib);
-      if (ib + 1 > i1) break;
-      iteration(std::integral_constant<int, 1>{}, ib + 1);
-      if (ib + 2 > i1) break;
-      iteration(std::integral_constant<int, 2>{}, ib + 2);
-      if (ib + 3 > i1) break;
-      iteration(std::integral_constant<int, 3>{}, ib + 3);
+    // bulk iterations: every stage's plane i − (k−1) lies in [blo, bhi) (owned, real, inside the global interior),
+    // so the per-stage x tests vanish; measured: the scalar unit (exec masks, compares, address math) was as busy as
+    // the vector unit. Blocks of 4 iterations keep the register-queue slots static.
+    using Gen = std::false_type;
+    using Bulk = std::true_type;
+    if constexpr (INIT) {
+      // the analytic-start pass runs general blocks only: its register footprint leaves no room for a second copy
+      for (int ib = i0; ib <= i1; ib += 4) {
+        iteration(std::integral_constant<int, 0>{}, Gen{}, ib);
+        if (ib + 1 > i1) break;
+        iteration(std::integral_constant<int, 1>{}, Gen{}, ib + 1);
+        if (ib + 2 > i1) break;
+        iteration(std::integral_constant<int, 2>{}, Gen{}, ib + 2);
+        if (ib + 3 > i1) break;
+        iteration(std::integral_constant<int, 3>{}, Gen{}, ib + 3);
+      }
+    } else {
+      // head blocks (general) until the first block inside the bulk range, bulk blocks, then the general tail
+      const int blo = imax(imax(x0, p.sx0), 1 - p.gx0) + (S - 1);
+      const int bhi = imin(imin(x1, p.sx1), N - p.gx0);
+      int ib = i0;
+      const int nhead = blo > i0 ? (blo - i0 + 3) / 4 : 0;
+      for (int b = 0; b < nhead && ib + 3 <= i1; ++b, ib += 4) {
+        iteration(std::integral_constant<int, 0>{}, Gen{}, ib);
+        iteration(std::integral_constant<int, 1>{}, Gen{}, ib + 1);
+        iteration(std::integral_constant<int, 2>{}, Gen{}, ib + 2);
+        iteration(std::integral_constant<int, 3>{}, Gen{}, ib + 3);
+      }
+      for (; ib + 3 < bhi; ib += 4) {
+        iteration(std::integral_constant<int, 0>{}, Bulk{}, ib);
+        iteration(std::integral_constant<int, 1>{}, Bulk{}, ib + 1);
+        iteration(std::integral_constant<int, 2>{}, Bulk{}, ib + 2);
+        iteration(std::integral_constant<int, 3>{}, Bulk{}, ib + 3);
+      }
+      for (; ib <= i1; ib += 4) {
+        iteration(std::integral_constant<int, 0>{}, Gen{}, ib);
+        if (ib + 1 > i1) break;
+        iteration(std::integral_constant<int, 1>{}, Gen{}, ib + 1);
+        if (ib + 2 > i1) break;
+        iteration(std::integral_constant<int, 2>{}, Gen{}, ib + 2);
+        if (ib + 3 > i1) break;
+        iteration(std::integral_constant<int, 3>{}, Gen{}, ib + 3);
+      }
     }
   }
 

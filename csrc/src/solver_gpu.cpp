@@ -307,8 +307,8 @@ void GpuSolver::build_units() {
     // pass of s steps with every 2nd level checked, measured at 512³ (tools/tune_leapfrog.py --tb); the analytic
     // first pass reads nothing but computes u⁰, u¹ (compute-bound). Slab ranks (deep-tb) take passes of ≥ 2 steps
     // only: every pass writes the two levels the next one reads, so each exchange is one message pair per face.
-    static const double kStepCost[5] = {0.0, 610.0, 451.0, 310.0, 283.0};
-    static const double kAnalyticCost[5] = {0.0, 1e9, 380.0, 328.0, 306.0};
+    static const double kStepCost[5] = {0.0, 610.0, 495.0, 327.0, 272.0};
+    static const double kAnalyticCost[5] = {0.0, 1e9, 382.0, 326.0, 300.0};
     const int rem = K - n, smax = opt_.temporal, smin = mode_ == Mode::kDeepTb ? 2 : 1;
     std::vector<double> best(static_cast<size_t>(rem + 1), 1e300);
     std::vector<int> take(static_cast<size_t>(rem + 1), 1);

@@ -18,12 +18,14 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <memory>
 #include <sstream>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "wave3d/cpu.hpp"
+#include "wave3d/cpu_dist.hpp"
 #include "wave3d/solver.hpp"
 
 using namespace wave3d;
@@ -67,7 +69,8 @@ struct Args {
                "  N        intervals per axis ((N+1)^3 nodes)      tau   time step\n"
                "  K        number of steps                          L     cube edge (default 1)\n"
                "options:\n"
-               "  --np P             spawn P ranks on this node (one GPU each)\n"
+               "  --np P             spawn P ranks on this node (one GPU each; with --cpu: P CPU processes, the\n"
+               "                     reference's MPI / MPI+OpenMP programs, halos through shared memory)\n"
                "  --decomp D         slab | block | PxQxR (default slab)\n"
                "  --check-every C    error check cadence (default 2, as the reference)\n"
                "  --cpu [--threads T] sequential/OpenMP CPU path\n"
@@ -293,6 +296,47 @@ int run_cpu(const Args& a) {
   return r.finite ? 0 : 3;
 }
 
+// One rank of the multi-process CPU path (--cpu --np P): the reference's MPI / MPI+OpenMP programs.
+int run_cpu_rank(const Args& a, ShmGroup& g) {
+  const int rank = std::atoi(std::getenv("RANK"));
+  try {
+    CpuRankSolver s(a.prob, g, rank, a.check_every, a.threads);
+    // fault injection: W3D_FAULT_RANK=r makes rank r fail before its first exchange
+    if (const char* fr = std::getenv("W3D_FAULT_RANK"); fr && std::atoi(fr) == rank) fail("injected fault");
+    CpuResult r;
+    double best = 1e30, sum = 0, exch = 0;
+    for (int i = 0; i < a.warmup + a.repeat; ++i) {
+      r = s.run();
+      if (i >= a.warmup) {
+        if (r.solve_s < best) exch = s.exchange_s();
+        best = std::min(best, r.solve_s);
+        sum += r.solve_s;
+      }
+    }
+    const Dims d = g.dims();
+    if (rank == 0) {
+      if (!a.quiet) print_errors(r.steps, r.max_err, r.rms_err, a.prob.tau);
+      const double gcell = a.prob.cell_updates() / best / 1e9;
+      std::printf("Total time: %.6f s (max over %d ranks, decomp %dx%dx%d; exchange %.6f s), threads %d per rank, "
+                  "%.3f GCell/s\n", best, g.world(), d.px, d.py, d.pz, exch, cpu_max_threads(), gcell);
+      if (!a.json.empty()) {
+        std::ofstream j(a.json);
+        j << "{\"backend\": \"cpu\", \"ranks\": " << g.world() << ", \"dims\": [" << d.px << ", " << d.py << ", "
+          << d.pz << "], \"N\": " << a.prob.N << ", \"tau\": " << a.prob.tau << ", \"K\": " << a.prob.K
+          << ", \"L\": " << a.prob.L << ", \"threads\": " << cpu_max_threads() << ", \"solve_s\": " << best
+          << ", \"mean_s\": " << sum / a.repeat << ", \"exchange_s\": " << exch << ", \"gcell_per_s\": " << gcell
+          << ", \"final_max_err\": " << (r.max_err.empty() ? 0.0 : r.max_err.back())
+          << ", \"final_rms_err\": " << (r.rms_err.empty() ? 0.0 : r.rms_err.back()) << "}\n";
+      }
+    }
+    if (!a.dump.empty()) write_dump(a.dump, a.prob, s.layout(), s.field(0), rank, g.world(), d);
+    return r.finite ? 0 : 3;
+  } catch (...) {
+    g.abort();  // the other ranks leave their barriers with an error instead of waiting for the timeout
+    throw;
+  }
+}
+
 int run_gpu(const Args& a) {
   static const char* const kRank[] = {"RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID", nullptr};
   static const char* const kSize[] = {"WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "SLURM_NTASKS", nullptr};
@@ -427,11 +471,15 @@ int main(int argc, char** argv) {
                    a.force ? " Continuing (--force)." : " Use a smaller tau, or --force.");
       if (!a.force) return 2;
     }
+    // multi-process CPU path: the shared segment is mapped before the fork so every rank inherits it
+    std::unique_ptr<ShmGroup> group;
+    if (a.cpu && a.np > 1 && !std::getenv("W3D_SPAWNED"))
+      group = std::make_unique<ShmGroup>(a.prob, parse_dims(a.decomp, a.np, a.prob.N), a.np);
     if (a.np > 1 && !std::getenv("W3D_SPAWNED")) {
       const int rc = spawn(a.np, argv);
       if (rc >= 0) return rc;  // parent
     }
-    const int rc = a.cpu ? run_cpu(a) : run_gpu(a);
+    const int rc = a.cpu ? (group ? run_cpu_rank(a, *group) : run_cpu(a)) : run_gpu(a);
     if (rc == 3) std::fprintf(stderr, "wave3d: solution blew up (non-finite error)\n");
     return rc;
   } catch (const std::exception& e) {

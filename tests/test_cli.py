@@ -65,3 +65,37 @@ def test_json_and_dump(tmp_path):
 
     _, uk, _ = torch_reference_solve(ProblemSpec(N=24, tau=1e-3, K=4), return_fields=True)
     assert np.array_equal(u, uk.numpy())
+
+
+@pytest.mark.parametrize("np_,decomp", [(2, "slab"), (3, "slab"), (4, "block"), (6, "1x2x3"), (8, "2x2x2")])
+def test_cpu_multiprocess_bitexact(tmp_path, np_, decomp):
+    """`--cpu --np P`: the reference's MPI / MPI+OpenMP programs (one process per rank, OpenMP inside, halos through a
+    shared-memory segment). Same log as the sequential program and, assembled from the per-rank dumps, the same field
+    bit for bit (the reference's rank-count invariance, report.pdf p.7-11)."""
+    seq = run(30, 0.001, 8, "--cpu", "--threads", 1, "--dump", tmp_path / "seq")
+    par = run(30, 0.001, 8, "--cpu", "--np", np_, "--decomp", decomp, "--threads", 1, "--dump", tmp_path / "par")
+    lines = lambda o: [l for l in o.stdout.splitlines() if l.startswith("Step ")]  # noqa: E731
+    assert lines(par) == lines(seq) and len(lines(seq)) == 4
+    assert f"max over {np_} ranks" in par.stdout
+    meta = json.loads((tmp_path / "seq.json").read_text())
+    full = np.fromfile(tmp_path / "seq.bin", dtype=np.float64).reshape(meta["shape"])
+    got = np.full_like(full, np.nan)
+    for r in range(np_):
+        m = json.loads((tmp_path / f"par.rank{r}.json").read_text())
+        (x0, y0, z0), (nx, ny, nz) = m["offset"], m["shape"]
+        got[x0:x0 + nx, y0:y0 + ny, z0:z0 + nz] = np.fromfile(tmp_path / f"par.rank{r}.bin",
+                                                              dtype=np.float64).reshape(nx, ny, nz)
+    assert np.array_equal(got, full)
+
+
+def test_cpu_multiprocess_rank_failure_is_an_error():
+    """Fault injection: one rank fails before its first exchange; the others leave their barriers with an error at
+    once (shared failure flag) instead of waiting for the barrier timeout, and the run exits non-zero."""
+    import time
+
+    t0 = time.time()
+    r = subprocess.run([CLI, "40", "0.001", "6", "--cpu", "--np", "4", "--threads", "1"], capture_output=True,
+                       text=True, timeout=120, env=dict(os.environ, W3D_FAULT_RANK="2"))
+    assert r.returncode != 0
+    assert "injected fault" in r.stderr and "another rank failed" in r.stderr
+    assert time.time() - t0 < 30

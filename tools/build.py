@@ -48,6 +48,7 @@ LIB_SOURCES = [
     ("src/solver_gpu.cpp", "hip"),
     ("src/cpu_kernels.cpp", "cpu"),
     ("src/cpu_solver.cpp", "cpu"),
+    ("src/cpu_dist.cpp", "cpu"),
 ]
 EXT_SOURCES = [("src/bindings.cpp", "hip")]
 CLI_SOURCES = [("app/wave3d_main.cpp", "hip")]

@@ -90,7 +90,7 @@ def main() -> int:
     solver, r, err = None, None, ""
     try:
         solver = make(transport)
-        r = solver.run()  # first warmup: graph capture + RCCL connection setup
+        r = solver.run()  # first warmup: graph capture (one rank) or RCCL connection setup (several)
         ok = 1
     except Exception as e:  # noqa: BLE001
         ok, err = 0, f"{type(e).__name__}: {e}"
@@ -115,7 +115,9 @@ def main() -> int:
         if not a.cpu:
             torch.cuda.synchronize()
 
-    for _ in range(max(0, a.warmup - 1)):
+    # RCCL ranks capture their hipGraph on the second solve (the first sets up the peer connections eagerly), so a
+    # multi-rank job always runs at least two untimed solves
+    for _ in range(max(0, a.warmup - 1, 1 if world > 1 else 0)):
         r = solver.run()
     barrier_sync()
     t0 = time.perf_counter()

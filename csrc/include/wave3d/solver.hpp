@@ -212,6 +212,7 @@ class GpuSolver {
   bool analytic_ = false;                     // the first unit computes u⁰, u¹ itself (no init kernel)
   std::vector<char> is_check_;
   hipGraphExec_t graph_exec_ = nullptr;
+  int runs_ = 0;  // completed run() calls (RCCL ranks capture the graph only after one eager solve)
   int final_buf_ = 0;            // buffer index holding u^K after a solve
   // per-phase timers
   enum { kPhaseInit = 0, kPhaseShell, kPhaseCompute, kPhaseComm, kPhaseCheck, kNumPhases };

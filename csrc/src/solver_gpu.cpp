@@ -750,7 +750,10 @@ void GpuSolver::gather_errors(RunResult& r) {
 
 RunResult GpuSolver::run() {
   RunResult r;
-  if (opt_.graph && !graph_exec_) {
+  // RCCL ranks run their first solve eagerly: the peer connections (and RCCL's proxy threads) are set up at the
+  // first send/recv, which must not happen inside a stream capture; the capture follows on the second run
+  const bool capture_ok = !(world_ > 1 && comm_) || runs_ >= 1;
+  if (opt_.graph && !graph_exec_ && capture_ok) {
     // capture once (outside the timed region of later runs); fall back to eager launches if capture is refused
     hipGraph_t g = nullptr;
     bool ok = hipStreamBeginCapture(s0_, hipStreamCaptureModeThreadLocal) == hipSuccess;
@@ -781,6 +784,7 @@ RunResult GpuSolver::run() {
   r.solve_s = now_s() - t0;
   collect_phases(r);
   r.phases.gather_ms = (now_s() - tg) * 1e3;  // host: waits for the device, then all-gathers the error log
+  ++runs_;
   return r;
 }
 

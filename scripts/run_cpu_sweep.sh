@@ -1,29 +1,40 @@
 #!/bin/bash
-# Reference-style CPU sweeps (report.pdf p.7-11, p.20-26): grids {128,256,512} x OpenMP threads (sequential/OpenMP
-# programs) and x ranks over torch.distributed gloo (MPI / MPI+OpenMP programs). Writes JSON lines to $OUT.
-#   scripts/run_cpu_sweep.sh [OUT=cpu_sweep.jsonl] [GRIDS="128 256"] [THREADS="1 2 4 8"] [RANKS="1 2 4"]
+# Reference-style CPU sweeps (report.pdf p.7-11, p.20-26): grids x OpenMP threads (the sequential / OpenMP programs)
+# and x processes (the MPI program: native `wave3d --cpu --np P`, one process per rank over shared memory; MPI+OpenMP:
+# P processes x T threads). Best of REPEAT solves per point. Writes JSON lines to $OUT, prints the tables, draws the
+# speedup / efficiency figure next to it.
+#   scripts/run_cpu_sweep.sh [OUT=cpu_sweep.jsonl] [GRIDS="128 256"] [THREADS="1 2 4 8"] [RANKS="1 2 4 8"]
+#                            [HYBRID="2x2 2x4 4x2"] [REPEAT=3]
 set -euo pipefail
 cd "$(dirname "$0")/.."
-OUT=${1:-cpu_sweep.jsonl}; GRIDS=${GRIDS:-"128 256"}; THREADS=${THREADS:-"1 2 4 8"}; RANKS=${RANKS:-"1 2 4"}
+OUT=${1:-cpu_sweep.jsonl}; GRIDS=${GRIDS:-"128 256"}; THREADS=${THREADS:-"1 2 4 8"}; RANKS=${RANKS:-"1 2 4 8"}
+HYBRID=${HYBRID:-"2x2 2x4 4x2"}; REPEAT=${REPEAT:-3}
 [ -x bin/wave3d ] || python tools/build.py
 : > "$OUT"
+tag() {  # tag <json> <mode> <workers>: add the sweep coordinates to one result line
+  python - "$@" >> "$OUT" <<'PY'
+import json, sys
+d = json.load(open(sys.argv[1])); d["mode"] = sys.argv[2]; d["workers"] = int(sys.argv[3]); print(json.dumps(d))
+PY
+}
 for g in $GRIDS; do
   echo "Running test with grid size ${g}^3"
   for t in $THREADS; do
-    bin/wave3d "$g" 0.001 20 --cpu --threads "$t" --quiet --json /tmp/w3d_cpu.json > /dev/null
-    python - "$t" >> "$OUT" <<'PY'
-import json, sys
-d = json.load(open("/tmp/w3d_cpu.json")); d["mode"] = "openmp"; d["workers"] = int(sys.argv[1]); print(json.dumps(d))
-PY
+    bin/wave3d "$g" 0.001 20 --cpu --threads "$t" --repeat "$REPEAT" --quiet --json /tmp/w3d_cpu.json > /dev/null
+    tag /tmp/w3d_cpu.json openmp "$t"
   done
   for p in $RANKS; do
-    OMP_NUM_THREADS=1 python -m torch.distributed.run --nproc-per-node "$p" --master-addr 127.0.0.1 \
-      --master-port $((29700 + p)) -m mpi_cuda_amd "$g" 0.001 20 --backend cpu --transport torch --threads 1 \
-      --quiet --json /tmp/w3d_mpi.json > /dev/null
-    python - "$p" >> "$OUT" <<'PY'
-import json, sys
-d = json.load(open("/tmp/w3d_mpi.json")); d["mode"] = "ranks"; d["workers"] = int(sys.argv[1]); print(json.dumps(d))
-PY
+    if [ "$p" = 1 ]; then
+      bin/wave3d "$g" 0.001 20 --cpu --threads 1 --repeat "$REPEAT" --quiet --json /tmp/w3d_mpi.json > /dev/null
+    else
+      bin/wave3d "$g" 0.001 20 --cpu --np "$p" --threads 1 --repeat "$REPEAT" --quiet --json /tmp/w3d_mpi.json > /dev/null
+    fi
+    tag /tmp/w3d_mpi.json mpi "$p"
+  done
+  for h in $HYBRID; do
+    p=${h%x*}; t=${h#*x}
+    bin/wave3d "$g" 0.001 20 --cpu --np "$p" --threads "$t" --repeat "$REPEAT" --quiet --json /tmp/w3d_hyb.json > /dev/null
+    tag /tmp/w3d_hyb.json "mpi+openmp(${p}x${t})" $((p * t))
   done
 done
-python tools/scaling_report.py "$OUT"
+python tools/scaling_report.py "$OUT" --plot "${OUT%.jsonl}.png"

@@ -4,6 +4,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 from mpi_cuda_amd.utils.report import error_line, gcell_per_s, parse_error_line, speedup_table
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -31,3 +33,19 @@ def test_scaling_report_table(tmp_path):
     out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scaling_report.py"), str(p)], check=True,
                          capture_output=True, text=True).stdout
     assert "| 2 | 0.00500 |" in out and "1.80" in out and "101.0x" in out
+
+
+def test_scaling_report_plot(tmp_path):
+    """--plot writes the reference-style speedup / efficiency figure (iamge1.png analogue) for both row kinds."""
+    pytest.importorskip("matplotlib")
+    g = tmp_path / "g.jsonl"
+    g.write_text("\n".join(json.dumps(r) for r in [{"n_gpus": 1, "ms_per_step": 5.3, "value": 506.0},
+                                                     {"n_gpus": 2, "ms_per_step": 3.1, "value": 866.0}]) + "\n")
+    c = tmp_path / "c.jsonl"
+    c.write_text("\n".join(json.dumps({"mode": m, "N": 128, "workers": w, "solve_s": 1.0 / w ** 0.9,
+                                       "gcell_per_s": 0.1 * w}) for m in ("openmp", "mpi") for w in (1, 2, 4)) + "\n")
+    for src in (g, c):
+        png = tmp_path / (src.stem + ".png")
+        out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scaling_report.py"), str(src), "--plot",
+                              str(png)], check=True, capture_output=True, text=True).stdout
+        assert "figure:" in out and png.stat().st_size > 1000

@@ -58,6 +58,9 @@ def main() -> int:
     ap.add_argument("--variant", type=int, default=1, help="leapfrog kernel (1 = register-queue, 0 = LDS tile)")
     ap.add_argument("--tile-rows", type=int, default=0, help="rows per wave (v1) / per workgroup (v0); 0 = default")
     ap.add_argument("--cpu", action="store_true", help="CPU backend (contract test without a GPU)")
+    ap.add_argument("--autotune", action="store_true", help="time the candidate schedules even on one rank")
+    ap.add_argument("--no-autotune", action="store_true",
+                    help="multi-rank: use --decomp/--temporal as given instead of timing the candidate schedules")
     ap.add_argument("--out", default="", help="also append the JSON line to this file")
     a = ap.parse_args()
 
@@ -78,34 +81,95 @@ def main() -> int:
     transport = ("torch" if world > 1 else "native") if a.cpu else a.transport
     os.environ.setdefault("W3D_TIMEOUT_S", "180")
 
-    def make(transport, group=None):
-        return Solver(spec, backend=backend, transport=transport, decomp=a.decomp, rank=rank, world=world,
+    def make(transport, group=None, comm=None, decomp=None, temporal=None):
+        return Solver(spec, backend=backend, transport=transport, decomp=decomp or a.decomp, rank=rank, world=world,
                       device=None if a.cpu else local, overlap=not a.no_overlap, graph=not a.no_graph,
-                      tiling=_tiling(a), group=group, temporal=1 if a.no_temporal else a.temporal,
-                      tb=not a.no_tb)
+                      tiling=_tiling(a), group=group, comm=comm,
+                      temporal=temporal or (1 if a.no_temporal else a.temporal), tb=not a.no_tb)
 
+    def agree(ok: int) -> int:  # every rank takes the same branch
+        if world > 1:
+            f = torch.tensor([ok], dtype=torch.int64)
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)
+            ok = int(f.item())
+        return ok
+
+    def timed_solve_max(s, n: int) -> float:  # best of n solves, max over ranks (seconds)
+        best = float("inf")
+        for _ in range(n):
+            t0 = time.perf_counter()
+            s.run()
+            best = min(best, time.perf_counter() - t0)
+        t = torch.tensor([best], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    # Multi-rank schedule autotune (part of the warmup, untimed): the halo volume of the deep-halo passes (S + S−1
+    # planes per face per S steps) against the per-step exchanges of the single-step schedule is a trade of xGMI
+    # bandwidth against HBM traffic that depends on the node, so each candidate runs a few solves on the real
+    # interconnect and every rank adopts the one whose slowest rank was fastest. One RCCL communicator serves all.
+    # (CPU multi-process runs take the same path over the torch.distributed transport: contract tests of this logic)
+    # (--autotune forces it on one rank too: a GPU-box rehearsal of this path)
+    autotune = (world > 1 or a.autotune) and not a.no_autotune and (
+        transport == "rccl" or (a.cpu and transport in ("torch", "native")))
+    cands = [("slab-S4", "slab", 4), ("slab-S2", "slab", 2), ("slab-S1", "slab", 1)]
+    if world >= 4:  # 2x2x1 / 2x2x2 blocks: smaller faces on more links (at 2 ranks "block" is the slab)
+        cands.append(("block-S1", "block", 1))
+    tuned = {}
+    solver, r, err, sched = None, None, "", f"{a.decomp}-S{1 if a.no_temporal else a.temporal}"
+    if autotune:
+        from mpi_cuda_amd.parallel.rccl import make_comm
+
+        comm, best_t, ok = None, float("inf"), 1
+        if transport == "rccl":
+            try:
+                comm = make_comm(rank, world)
+            except Exception as e:  # noqa: BLE001
+                ok, err = 0, f"{type(e).__name__}: {e}"
+        if agree(ok):
+            for name, dec, temp in cands:
+                s, t = None, float("inf")
+                try:
+                    s = make(transport, comm=comm, decomp=dec, temporal=temp)
+                    s.run()  # eager: RCCL peer connections
+                    s.run()  # graph capture
+                    t, ok = timed_solve_max(s, 3), 1
+                except Exception as e:  # noqa: BLE001
+                    ok, err = 0, f"{type(e).__name__}: {e}"
+                    print(f"[bench rank {rank}] autotune candidate {name} failed: {err}", file=sys.stderr, flush=True)
+                if not agree(ok):
+                    break  # a failed RCCL exchange may leave the communicator unusable: stop here
+                tuned[name] = round(t * 1e3, 4)
+                if t < best_t:
+                    solver, best_t, sched = s, t, name
+                else:
+                    del s
+        if solver is not None:  # the winner must still work (a failed candidate may have hurt the communicator)
+            try:
+                r, ok = solver.run(), 1
+            except Exception as e:  # noqa: BLE001
+                ok, err = 0, f"{type(e).__name__}: {e}"
+            if not agree(ok):
+                solver, sched, tuned = None, f"{a.decomp}-S{1 if a.no_temporal else a.temporal}", {}
     # The native RCCL runtime is the production path. If it fails on some rank (it throws; stuck exchanges time out),
     # every rank switches together to the torch.distributed transport (RCCL through ProcessGroupNCCL) so the scaling
     # run still measures the same kernels; the JSON line says which transport ran.
-    solver, r, err = None, None, ""
-    try:
-        solver = make(transport)
-        r = solver.run()  # first warmup: graph capture (one rank) or RCCL connection setup (several)
-        ok = 1
-    except Exception as e:  # noqa: BLE001
-        ok, err = 0, f"{type(e).__name__}: {e}"
-        print(f"[bench rank {rank}] {transport} path failed: {err}", file=sys.stderr, flush=True)
-    if world > 1:
-        flag = torch.tensor([ok], dtype=torch.int64)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        ok = int(flag.item())
-    if not ok:
-        if a.cpu or transport != "rccl":
-            raise SystemExit(f"bench: {transport} transport failed: {err}")
-        group = dist.new_group(backend="nccl") if world > 1 else None
-        transport = "torch"
-        solver = make(transport, group)
-        r = solver.run()
+    if solver is None:
+        try:
+            solver = make(transport)
+            r = solver.run()  # first warmup: graph capture (one rank) or RCCL connection setup (several)
+            ok = 1
+        except Exception as e:  # noqa: BLE001
+            ok, err = 0, f"{type(e).__name__}: {e}"
+            print(f"[bench rank {rank}] {transport} path failed: {err}", file=sys.stderr, flush=True)
+        if not agree(ok):
+            if a.cpu or transport != "rccl":
+                raise SystemExit(f"bench: {transport} transport failed: {err}")
+            group = dist.new_group(backend="nccl") if world > 1 else None
+            transport = "torch"
+            solver = make(transport, group)
+            r = solver.run()
 
     def barrier_sync():
         if not a.cpu:
@@ -139,7 +203,7 @@ def main() -> int:
     correct = bool(r is not None and r.finite and (a.N != 512 or a.K != 20 or a.tau != 1e-3 or a.L != 1.0
                                                    or abs(final_linf / REF_FINAL_LINF - 1) < 1e-5))
     if rank == 0:
-        par = f"{a.decomp}{world}" if world > 1 else "single"
+        par = f"{sched.split('-')[0]}{world}" if world > 1 else "single"
         dims = "x".join(str(d) for d in solver.dims)
         line = {
             "metric": f"gcell_updates_per_s_{a.N}cube_K{a.K}",
@@ -161,7 +225,10 @@ def main() -> int:
                 "parallelism": par,
                 "grid": f"{a.N}^3", "N": a.N, "tau": a.tau, "K": a.K, "L": a.L,
                 "decomp": dims, "transport": transport, "graph": bool(not a.no_graph),
-                "overlap": bool(not a.no_overlap), "temporal_blocking": bool(not a.no_temporal and world == 1),
+                "overlap": bool(not a.no_overlap),
+                "temporal_blocking": bool(not a.no_temporal and (world == 1 or not sched.endswith("S1"))),
+                "schedule": sched if (world > 1 or tuned) else f"fused-single-S{1 if a.no_temporal else a.temporal}",
+                "autotune_ms": tuned or None,
             },
             "wall_clock_s": round(ms / 1e3, 6),
             "best_solve_s": round(best, 6),

@@ -73,3 +73,7 @@ def test_bench_contract_cpu_two_ranks(tmp_path):
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1 and d["correct"]
     for k in ("model", "global_batch", "seq_len", "parallelism"):
         assert k in d["config"]
+    # the multi-rank schedule autotune ran (over the torch transport here) and picked one of its candidates
+    assert set(d["config"]["autotune_ms"]) == {"slab-S4", "slab-S2", "slab-S1"}
+    assert d["config"]["schedule"] in d["config"]["autotune_ms"]
+    assert d["config"]["schedule"] == min(d["config"]["autotune_ms"], key=d["config"]["autotune_ms"].get)

@@ -493,24 +493,33 @@ TbPlan make_plan_tb(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, i
 
 template <int NT>
 constexpr size_t max_dyn_lds() {
-  return 160 * 1024 - 2 * (NT / 64) * sizeof(double);  // minus the static reduction arrays
+  return 160 * 1024 - 2 * (NT / 64) * sizeof(double) - 64;  // minus the static reduction arrays (+ alignment)
 }
 
-// allow the dynamic LDS size once per instantiation (outside any stream capture: see leapfrog_tb_prepare)
+// allow the dynamic LDS size once per instantiation (outside any stream capture: see leapfrog_tb_prepare): the CU's
+// 160 KiB minus the kernel's static LDS (the reduction arrays as the compiler laid them out, alignment included);
+// returns that limit
 template <int S, int NT, int CM, bool INIT>
-void prepare_cfg() {
+size_t prepare_cfg() {
   static_assert(tb_lds_bytes<S, kTile, NT>() <= max_dyn_lds<NT>(), "leapfrog_tb tile does not fit in LDS");
-  static const hipError_t attr =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(k_leapfrog_tb<S, kTile, NT, CM, INIT>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(max_dyn_lds<NT>()));
-  if (attr != hipSuccess) fail(std::string("leapfrog_tb LDS attribute: ") + hipGetErrorString(attr));
+  static const size_t limit = [] {
+    const void* fn = reinterpret_cast<const void*>(k_leapfrog_tb<S, kTile, NT, CM, INIT>);
+    hipFuncAttributes fa{};
+    hipError_t e = hipFuncGetAttributes(&fa, fn);
+    if (e != hipSuccess) fail(std::string("leapfrog_tb attributes: ") + hipGetErrorString(e));
+    const size_t lim = 160 * 1024 - fa.sharedSizeBytes;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lim));
+    if (e != hipSuccess) fail(std::string("leapfrog_tb LDS attribute: ") + hipGetErrorString(e));
+    return lim;
+  }();
+  return limit;
 }
 
 template <int S, int NT, int CM, bool INIT>
 void launch_cfg(const TbParams& p, int nblocks, hipStream_t st) {
-  prepare_cfg<S, NT, CM, INIT>();
+  const size_t limit = prepare_cfg<S, NT, CM, INIT>();
   const size_t shmem = tb_lds_bytes<S, kTile, NT>((p.check_mask || INIT) ? tb_nx_table<S>(p.x1 - p.x0) : 0);
-  W3D_REQUIRE(shmem <= max_dyn_lds<NT>(), "leapfrog_tb: too many planes for the LDS sin table");
+  W3D_REQUIRE(shmem <= limit, "leapfrog_tb: too many planes for the LDS sin table");
   hipLaunchKernelGGL((k_leapfrog_tb<S, kTile, NT, CM, INIT>), dim3(nblocks), dim3(NT), shmem, st, p);
 }
 

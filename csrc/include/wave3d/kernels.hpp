@@ -97,6 +97,13 @@ void launch_error(const Layout& l, const double* u, const LBox& box, const doubl
 
 // out[0] = (max_i partials[i].x, Σ_i partials[i].y), in a fixed order.
 void launch_reduce(const Partial* partials, int n, Partial* out, hipStream_t stream);
+// Several independent reductions in one launch (one workgroup each, k_reduce's order: bit-identical results).
+struct ReduceJob {
+  const Partial* in;
+  int n;
+  Partial* out;
+};
+void launch_reduce_batch(const ReduceJob* jobs, int njobs, hipStream_t stream);
 
 // Pack all strided faces of `plan` from `u` into `buf`, or unpack `buf` into the ghost layers of `u`.
 void launch_pack(const Layout& l, const HaloPlan& plan, const double* u, double* buf, hipStream_t stream);

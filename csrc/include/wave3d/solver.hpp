@@ -206,6 +206,13 @@ class GpuSolver {
   int n_tb_ = 0;                                            // ... per level of a k_leapfrog_tb pass
   // deep-tb: per level, the partials of this unit's launches (shell lo, shell hi, interior) follow each other
   int tb_slots_ = 0;                                        // launches of the current unit with partials so far
+  // LDS passes: each unit's partials go to region tb_region_ of kTbRegions; their reductions are queued and issued as
+  // one batched launch when the regions wrap and at the end of the solve (one launch instead of one per checked step)
+  static constexpr int kTbRegions = 8;
+  Partial* tb_partials_ = nullptr;
+  int tb_region_ = 0;
+  std::vector<ReduceJob> pending_;
+  void flush_reduces();
   bool nb_lo_ = false, nb_hi_ = false;                      // x neighbours (slab ranks)
   int cur_ = 1, old_ = 0;                     // buffer roles during enqueue
   int start_n_ = 1;                           // first leapfrog step after the init kernel

@@ -618,7 +618,23 @@ __global__ __launch_bounds__(256) void k_error(const ErrParams p) {
 // ---------------------------------------------------------------------------------------------------------------
 // fixed-order reduction of partials
 // ---------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void reduce_block(const Partial* __restrict__ in, int n, Partial* out);
+
 __global__ __launch_bounds__(1024) void k_reduce(const Partial* __restrict__ in, int n, Partial* out) {
+  reduce_block(in, n, out);
+}
+
+constexpr int kReduceBatch = 64;  // jobs per launch (kernel-argument struct: 64 × 24 B)
+struct ReduceBatch {
+  ReduceJob job[kReduceBatch];
+};
+
+__global__ __launch_bounds__(1024) void k_reduce_batch(const ReduceBatch b) {
+  const ReduceJob j = b.job[blockIdx.x];
+  reduce_block(j.in, j.n, j.out);
+}
+
+__device__ __forceinline__ void reduce_block(const Partial* __restrict__ in, int n, Partial* out) {
   __shared__ double sm[16], ss[16];
   double m = 0.0, s = 0.0;
   for (int i = threadIdx.x; i < n; i += 1024) {
@@ -753,6 +769,16 @@ void launch_error(const Layout& l, const double* u, const LBox& b, const double*
 void launch_reduce(const Partial* partials, int n, Partial* out, hipStream_t stream) {
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, stream, partials, n, out);
   W3D_HIP_CHECK(hipGetLastError());
+}
+
+void launch_reduce_batch(const ReduceJob* jobs, int njobs, hipStream_t stream) {
+  for (int j0 = 0; j0 < njobs; j0 += kReduceBatch) {
+    ReduceBatch b{};
+    const int nb = njobs - j0 < kReduceBatch ? njobs - j0 : kReduceBatch;
+    for (int j = 0; j < nb; ++j) b.job[j] = jobs[j0 + j];
+    hipLaunchKernelGGL(k_reduce_batch, dim3(nb), dim3(1024), 0, stream, b);
+    W3D_HIP_CHECK(hipGetLastError());
+  }
 }
 
 }  // namespace wave3d

@@ -221,9 +221,13 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   }
   n_dint_ = dint_.empty() ? 0 : leapfrog2_partials(lay_, dint_, opt_.tiling2);
   n_deep += n_dint_;
-  n_partials_ = std::max({n_full_, n_shell_ + n_int_, error_blocks(lay_, full_), n_fused_, n_deep, 4 * 3 * n_tb_,
+  n_partials_ = std::max({n_full_, n_shell_ + n_int_, error_blocks(lay_, full_), n_fused_, n_deep,
                           opt_.init2 ? init_two_partials(lay_) : 0, 1});
   W3D_HIP(hipMalloc(&partials_, static_cast<size_t>(n_partials_) * sizeof(Partial)));
+  // the LDS passes' partials live apart: their reductions are deferred, so the immediate users of partials_ (init,
+  // single steps between passes) must not overwrite them
+  if (n_tb_ > 0)
+    W3D_HIP(hipMalloc(&tb_partials_, static_cast<size_t>(kTbRegions) * 4 * 3 * n_tb_ * sizeof(Partial)));
   W3D_HIP(hipMalloc(&errlog_, static_cast<size_t>(prob_.K + 1) * sizeof(Partial)));
   W3D_HIP(hipMalloc(&errall_, static_cast<size_t>(world_) * (prob_.K + 1) * sizeof(Partial)));
   ct_.resize(static_cast<size_t>(prob_.K + 1));
@@ -236,6 +240,7 @@ GpuSolver::~GpuSolver() {
   for (double* p : {u_[0], u_[1], u_[2], u_[3], d_s_, send_buf_, recv_buf_})
     if (p) hipFree(p);
   if (partials_) hipFree(partials_);
+  if (tb_partials_) hipFree(tb_partials_);
   if (errlog_) hipFree(errlog_);
   if (errall_) hipFree(errall_);
   for (hipEvent_t e : ev_pool_) hipEventDestroy(e);
@@ -248,7 +253,8 @@ GpuSolver::~GpuSolver() {
 
 size_t GpuSolver::device_bytes() const {
   return static_cast<size_t>(nbuf_) * static_cast<size_t>(lay_.bytes()) + 2 * static_cast<size_t>(plan_.packed_doubles) * sizeof(double) +
-         static_cast<size_t>(n_partials_) * sizeof(Partial) + static_cast<size_t>(prob_.N + 3) * sizeof(double);
+         static_cast<size_t>(n_partials_) * sizeof(Partial) + static_cast<size_t>(prob_.N + 3) * sizeof(double) +
+         static_cast<size_t>(kTbRegions) * 4 * 3 * static_cast<size_t>(n_tb_) * sizeof(Partial);
 }
 
 std::vector<int> GpuSolver::check_steps() const {
@@ -546,7 +552,7 @@ void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase) {
   }
   const int slots = mode_ == Mode::kDeepTb ? 3 : 1;
   W3D_REQUIRE(tb_slots_ < slots, "leapfrog_tb: too many launches in one unit");
-  Partial* part = mask ? partials_ + tb_slots_ * n_tb_ : nullptr;
+  Partial* part = mask ? tb_partials_ + tb_region_ * (4 * slots * n_tb_) + tb_slots_ * n_tb_ : nullptr;
   const i64 sx0 = mode_ == Mode::kDeepTb ? sx0_ : 1, sx1 = mode_ == Mode::kDeepTb ? sx1_ : 0;
   timed(phase, s0_, [&] {
     launch_leapfrog_tb(lay_, coef_, u_[old_], u_[cur_], u_[uf_[0]], u_[uf_[1]], box, d_s_ + 1, cts, mask, part, t,
@@ -591,11 +597,12 @@ void GpuSolver::unit_interior(int i) {
     if (!b.empty()) tb_pass(u, b, kPhaseCompute);
     const int slots = mode_ == Mode::kDeepTb ? 3 : 1;
     if (tb_slots_ > 0) {
-      timed(kPhaseCheck, s0_, [&] {
-        for (int k = 1; k <= u.steps; ++k)
-          if (is_check_[static_cast<size_t>(u.n + k)])
-            launch_reduce(partials_ + (k - 1) * slots * n_tb_, tb_slots_ * n_tb_, errlog_ + u.n + k, s0_);
-      });
+      Partial* region = tb_partials_ + tb_region_ * (4 * slots * n_tb_);
+      for (int k = 1; k <= u.steps; ++k)
+        if (is_check_[static_cast<size_t>(u.n + k)])
+          pending_.push_back(ReduceJob{region + (k - 1) * slots * n_tb_, tb_slots_ * n_tb_, errlog_ + u.n + k});
+      tb_region_ = (tb_region_ + 1) % kTbRegions;
+      if (tb_region_ == 0 || opt_.timers) flush_reduces();  // the next unit reuses region 0 / per-unit check time
     }
   } else if (mode_ == Mode::kFusedSingle) {
     timed(kPhaseCompute, s0_, [&] {
@@ -633,13 +640,22 @@ void GpuSolver::unit_interior(int i) {
   prev_buf_ = old_;
 }
 
+void GpuSolver::flush_reduces() {
+  if (pending_.empty()) return;
+  timed(kPhaseCheck, s0_, [&] { launch_reduce_batch(pending_.data(), static_cast<int>(pending_.size()), s0_); });
+  pending_.clear();
+}
+
 void GpuSolver::enqueue_solve() {
   phase_init();
+  tb_region_ = 0;
+  pending_.clear();
   for (int i = 0; i < static_cast<int>(units_.size()); ++i) {
     unit_shell(i);
     unit_exchange_rccl(i);
     unit_interior(i);
   }
+  flush_reduces();
   final_buf_ = cur_;
   prev_buf_ = old_;
 }
@@ -831,7 +847,11 @@ RunResult GpuGroup::run() {
   for (auto& p : ranks_) rs.push_back(p.get());
   const int K = rs[0]->prob_.K;
   const double t0 = now_s();
-  for (auto* s : rs) s->phase_init();
+  for (auto* s : rs) {
+    s->phase_init();
+    s->tb_region_ = 0;
+    s->pending_.clear();
+  }
   const int nu = static_cast<int>(rs[0]->units_.size());
   for (int i = 0; i < nu; ++i) {
     for (auto* s : rs) s->unit_shell(i);
@@ -840,6 +860,7 @@ RunResult GpuGroup::run() {
     for (auto* s : rs) s->lb_fence(i, rs);
     for (auto* s : rs) s->unit_interior(i);
   }
+  for (auto* s : rs) s->flush_reduces();
   // combine the per-rank error logs in rank order (what the RCCL all-gather does across processes)
   const size_t per = static_cast<size_t>(K + 1);
   std::vector<Partial> all(per * rs.size());

@@ -78,15 +78,17 @@ struct TbGeom {
   static constexpr int PLP = PL + 2 * W0 + 2;
   static constexpr int DUMMY = PL + W0 + 1;
   static constexpr int QR = (NR + NT - 1) / NT;
-  static constexpr int lds_doubles() { return S * 2 * PLP; }  // levels 0..S−1 × 2 parity slots
+  // levels 0..S−1 × 2 parity slots; the analytic start adds a φ level (two parity slots) after them
+  static constexpr int lds_doubles(bool init = false) { return (S + (init ? 1 : 0)) * 2 * PLP; }
 };
 
 // + sin tables (error check, analytic start): y and z over the u^n region ± 1, x over the planes the pass touches ± 1.
 // In LDS because a global load of the per-plane x factor would be a vector load (the table may alias the outputs, so
 // no scalar load) whose wait drains the prefetch queue. nxo = tb_nx_table(x1 − x0) or 0 (no table needed).
-template <int S, int T, int NT>
+template <int S, int T, int NT, bool INIT = false>
 constexpr size_t tb_lds_bytes(int nxo = 0) {
-  return (static_cast<size_t>(TbGeom<S, T, NT>::lds_doubles()) + 2 * (T + 2 * S + 2) + static_cast<size_t>(nxo)) *
+  return (static_cast<size_t>(TbGeom<S, T, NT>::lds_doubles(INIT)) + 2 * (T + 2 * S + 2) +
+          static_cast<size_t>(nxo)) *
          sizeof(double);
 }
 template <int S>
@@ -188,7 +190,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     // sin tables: syw[j] = s[y] for y = ty0 − S − 1 + j (the u^n region ± 1), szw likewise, sxw[i] = s[x] for
     // x = x0 − S − 1 + i; indices clamped into −1..N+1 (only nodes of the interior, and their neighbours, use them)
     constexpr int NYW = T + 2 * S + 2;
-    double* syw = lds + G::lds_doubles();
+    double* syw = lds + G::lds_doubles(INIT);
     double* szw = syw + NYW;
     double* sxw = szw + NYW;
     if (p.check_mask || INIT) {
@@ -275,6 +277,68 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       for (int r = 0; r < QR; ++r) d[lrid[r]] = Rg[r][rs];
     };
 
+    // ---- analytic start, φ stage: φ = (s_x·s_y)·s_z is computed once per node and plane (2 products with the
+    // node's y/z factors held in registers) into a φ plane of LDS (two parity slots after the S levels); u¹ of the
+    // owned positions is then first_step(φ, Δ_h φ) with the y/z neighbours from that plane and the x neighbours from
+    // the thread's own entries of both φ slots. Every neighbour value is the product u1_at forms for it, so u¹ is
+    // bit-identical to k_init_first's; 2 products + 4 LDS reads instead of 12 products + 9 table reads per node.
+    // The halo ring (no φ neighbours beyond it in LDS) keeps u1_at.
+    double fy[Q], fz[Q], fyr[QR], fzr[QR];
+    if constexpr (INIT) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        fy[q] = syw[ytab(lid[q])];
+        fz[q] = szw[ztab(lid[q])];
+      }
+#pragma unroll
+      for (int r = 0; r < QR; ++r) {
+        fyr[r] = syw[ytab(lrid[r])];
+        fzr[r] = szw[ztab(lrid[r])];
+      }
+    }
+    auto lds_phi = [&](int par) { return lds + (S * 2 + par) * PLP; };
+    // φ of plane x (owned positions and ring) into φ slot `par`
+    auto phi_plane = [&](int x, int par) {
+      double* d = lds_phi(par);
+      const double sx = sxw[x + xtab0];
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (wsm[q]) d[lid[q]] = (sx * fy[q]) * fz[q];
+#pragma unroll
+      for (int r = 0; r < QR; ++r)
+        if (wbase_r + r * NT < G::NR) d[lrid[r]] = (sx * fyr[r]) * fzr[r];
+    };
+    // iteration i of the analytic pass (F = (i − i0) & 3): u¹ of plane i+2 into L[0] slot (F+2)&3 / Rg slot (F+2)&1,
+    // u⁰ = φ of plane i+1 into Lm slot (F+1)&1; φ of plane i+3 into its slot. φ slot (i+2)&1 was completed in the
+    // previous iteration (behind this iteration's barrier); slot (i+3)&1 still holds this thread's φ(i+1) entries,
+    // read before they are overwritten.
+    auto init_iter = [&](auto fc, int i) {
+      constexpr int F = decltype(fc)::value;
+      double* p3 = lds_phi((F + 3) & 1);
+      const double* p2 = lds_phi((F + 2) & 1);
+      const double sx3 = sxw[i + 3 + xtab0];
+      const bool xin = inside(p.gx0 + i + 2);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        if (!wsm[q]) continue;  // wave-uniform
+        const int li = lid[q];
+        const double f1 = p3[li];                    // φ(i+1), own entry
+        const double f3 = (sx3 * fy[q]) * fz[q];     // φ(i+3)
+        p3[li] = f3;
+        const double c = p2[li];                     // φ(i+2)
+        const double lap = lap7(c, f1, f3, p2[li - W0], p2[li + W0], p2[li - 1], p2[li + 1], ihx2, ihy2, ihz2);
+        L[0][q][(F + 2) & 3] = ((gof[q] & kReal) && xin) ? first_step(c, lap, p.half_tau2) : 0.0;
+        Lm[q][(F + 1) & 1] = f1;
+      }
+#pragma unroll
+      for (int r = 0; r < QR; ++r) {
+        if (wbase_r + r * NT < G::NR) {
+          p3[lrid[r]] = (sx3 * fyr[r]) * fzr[r];
+          Rg[r][(F + 2) & 1] = u1_at(i + 2, lrid[r], grof[r] & kReal);
+        }
+      }
+    };
+
     // stage k at plane xp; D = (xp − i0) & 3 (static), parity of xp = D & 1
     // BK (bulk): plane xp is real and owned for every stage (the x tests are compile-time true)
     auto stage = [&](auto kc, auto dc, auto bkc, int xp) {
@@ -330,8 +394,12 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       __syncthreads();  // every read of the slots overwritten below (iteration i−1) is done; i−1's writes visible
       commit_cur(std::integral_constant<int, (F + 1) & 3>{}, std::integral_constant<int, (F + 1) & 1>{},
                  (F + 1) & 1);  // u^n plane i+1 → LDS (loaded one iteration ago)
-      load_cur(std::integral_constant<int, (F + 2) & 3>{}, std::integral_constant<int, (F + 2) & 1>{}, i + 2);
-      load_prev(std::integral_constant<int, (F + 1) & 1>{}, i + 1);
+      if constexpr (INIT) {
+        init_iter(fc, i);
+      } else {
+        load_cur(std::integral_constant<int, (F + 2) & 3>{}, std::integral_constant<int, (F + 2) & 1>{}, i + 2);
+        load_prev(std::integral_constant<int, (F + 1) & 1>{}, i + 1);
+      }
 #define W3D_TB_STAGE(K)                                                                                          \
   if constexpr (K <= S) {                                                                                        \
     const int xp = i - (K - 1);                                                                                  \
@@ -351,6 +419,10 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     commit_cur(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0);
     load_cur(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, i0 + 1);
     load_prev(std::integral_constant<int, 0>{}, i0);
+    if constexpr (INIT) {  // φ planes i0+1 (slot 1: read back as the x neighbour at i0) and i0+2 (slot 0)
+      phi_plane(i0 + 1, 1);
+      phi_plane(i0 + 2, 0);
+    }
     // bulk iterations: every stage's plane i − (k−1) lies in [blo, bhi) (owned, real, inside the global interior),
     // so the per-stage x tests vanish; measured: the scalar unit (exec masks, compares, address math) was as busy as
     // the vector unit. Blocks of 4 iterations keep the register-queue slots static.
@@ -501,7 +573,7 @@ constexpr size_t max_dyn_lds() {
 // returns that limit
 template <int S, int NT, int CM, bool INIT>
 size_t prepare_cfg() {
-  static_assert(tb_lds_bytes<S, kTile, NT>() <= max_dyn_lds<NT>(), "leapfrog_tb tile does not fit in LDS");
+  static_assert(tb_lds_bytes<S, kTile, NT, INIT>() <= max_dyn_lds<NT>(), "leapfrog_tb tile does not fit in LDS");
   static const size_t limit = [] {
     const void* fn = reinterpret_cast<const void*>(k_leapfrog_tb<S, kTile, NT, CM, INIT>);
     hipFuncAttributes fa{};
@@ -518,7 +590,7 @@ size_t prepare_cfg() {
 template <int S, int NT, int CM, bool INIT>
 void launch_cfg(const TbParams& p, int nblocks, hipStream_t st) {
   const size_t limit = prepare_cfg<S, NT, CM, INIT>();
-  const size_t shmem = tb_lds_bytes<S, kTile, NT>((p.check_mask || INIT) ? tb_nx_table<S>(p.x1 - p.x0) : 0);
+  const size_t shmem = tb_lds_bytes<S, kTile, NT, INIT>((p.check_mask || INIT) ? tb_nx_table<S>(p.x1 - p.x0) : 0);
   W3D_REQUIRE(shmem <= limit, "leapfrog_tb: too many planes for the LDS sin table");
   hipLaunchKernelGGL((k_leapfrog_tb<S, kTile, NT, CM, INIT>), dim3(nblocks), dim3(NT), shmem, st, p);
 }

@@ -87,7 +87,7 @@ struct TbGeom {
 // no scalar load) whose wait drains the prefetch queue. nxo = tb_nx_table(x1 − x0) or 0 (no table needed).
 template <int S, int T, int NT, bool INIT = false>
 constexpr size_t tb_lds_bytes(int nxo = 0) {
-  return (static_cast<size_t>(TbGeom<S, T, NT>::lds_doubles(INIT)) + 2 * (T + 2 * S + 2) +
+  return (static_cast<size_t>(TbGeom<S, T, NT>::lds_doubles(INIT)) + (2 + 2 * S) * (T + 2 * S + 2) +
           static_cast<size_t>(nxo)) *
          sizeof(double);
 }
@@ -192,7 +192,8 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     constexpr int NYW = T + 2 * S + 2;
     double* syw = lds + G::lds_doubles(INIT);
     double* szw = syw + NYW;
-    double* sxw = szw + NYW;
+    double* rowt = szw + NYW;  // per checked level, two plane-parity slots of NYW row factors s_x·s_y
+    double* sxw = rowt + 2 * S * NYW;
     if (p.check_mask || INIT) {
       auto sc = [&](int g) { return p.s[g < -1 ? -1 : g > N + 1 ? N + 1 : g]; };
       for (int t = tid; t < NYW; t += NT) {
@@ -352,7 +353,9 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       constexpr bool kChk = (CM >> (k - 1)) & 1;
       const bool chk = kChk && ((p.check_mask >> (k - 1)) & 1);
       double* outp = (k == S ? p.out2 : p.out1) + static_cast<i64>(xp + 1) * P;
-      const double sxc = (chk && xown) ? sxw[xp + xtab0] : 0.0;
+      // the check's (s_x·s_y) row factor of plane xp, tabulated one iteration ahead (row_tables), slot F & 1
+      const double* rowk = rowt + ((k - 1) * 2 + ((D + k - 1) & 1)) * NYW;
+      (void)xown;
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         if (!((wsm[q] >> (k - 1)) & 1)) continue;  // wave-uniform
@@ -379,10 +382,24 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         }
         if constexpr (kChk) {
           if (chk && own && xreal) {
-            const double e = fabs(v - ((sxc * syw[ytab(li)]) * szw[ztab(li)]) * p.ct[k - 1]);
-            emax[k - 1] = e > emax[k - 1] ? e : emax[k - 1];
+            const double e = fabs(v - (rowk[ytab(li)] * szw[ztab(li)]) * p.ct[k - 1]);
+            emax[k - 1] = fmax(e, emax[k - 1]);  // = (e > m ? e : m) for every non-NaN e; a NaN shows in the sum
             esum[k - 1] += e * e;
           }
+        }
+      }
+    };
+
+    // check row factors: rowt[k][slot][j] = s_x(plane of stage k) · s_y(j), the first product of the check's
+    // ((s_x·s_y)·s_z)·ct (same operands and order: bit-identical), tabulated once per plane by the first NYW threads
+    // instead of once per node; iteration i fills slot ((i − i0) + 1) & 1 for the planes its successor checks
+    auto row_tables = [&](int i, int slot) {
+      if constexpr (CM != 0) {
+        if (p.check_mask && tid < NYW) {
+#pragma unroll
+          for (int k = 1; k <= S; ++k)
+            if (((CM & p.check_mask) >> (k - 1)) & 1)
+              rowt[((k - 1) * 2 + slot) * NYW + tid] = sxw[imax(i - (k - 1) + xtab0, 0)] * syw[tid];
         }
       }
     };
@@ -392,6 +409,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       constexpr int F = decltype(fc)::value;
       constexpr bool BK = decltype(bkc)::value;
       __syncthreads();  // every read of the slots overwritten below (iteration i−1) is done; i−1's writes visible
+      row_tables(i + 1, (F + 1) & 1);
       commit_cur(std::integral_constant<int, (F + 1) & 3>{}, std::integral_constant<int, (F + 1) & 1>{},
                  (F + 1) & 1);  // u^n plane i+1 → LDS (loaded one iteration ago)
       if constexpr (INIT) {
@@ -419,6 +437,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     commit_cur(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0);
     load_cur(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, i0 + 1);
     load_prev(std::integral_constant<int, 0>{}, i0);
+    row_tables(i0, 0);
     if constexpr (INIT) {  // φ planes i0+1 (slot 1: read back as the x neighbour at i0) and i0+2 (slot 0)
       phi_plane(i0 + 1, 1);
       phi_plane(i0 + 2, 0);

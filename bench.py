@@ -113,7 +113,7 @@ def main() -> int:
     # (--autotune forces it on one rank too: a GPU-box rehearsal of this path)
     autotune = (world > 1 or a.autotune) and not a.no_autotune and (
         transport == "rccl" or (a.cpu and transport in ("torch", "native")))
-    cands = [("slab-S4", "slab", 4), ("slab-S2", "slab", 2), ("slab-S1", "slab", 1)]
+    cands = [("slab-S4", "slab", 4), ("slab-S3", "slab", 3), ("slab-S2", "slab", 2), ("slab-S1", "slab", 1)]
     if world >= 4:  # 2x2x1 / 2x2x2 blocks: smaller faces on more links (at 2 ranks "block" is the slab)
         cands.append(("block-S1", "block", 1))
     tuned = {}

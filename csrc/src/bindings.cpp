@@ -349,6 +349,12 @@ PYBIND11_MODULE(_C, m) {
                         std::uintptr_t partials, std::uintptr_t stream) {
     launch_error(l, dptr<const double>(u), b, dptr<const double>(s) + 1, ct, dptr<Partial>(partials), sptr(stream));
   });
+  m.def("gpu_reduce_batch", [](const std::vector<std::tuple<std::uintptr_t, int, std::uintptr_t>>& jobs,
+                               std::uintptr_t stream) {
+    std::vector<ReduceJob> js;
+    for (const auto& [in, n, out] : jobs) js.push_back(ReduceJob{dptr<const Partial>(in), n, dptr<Partial>(out)});
+    launch_reduce_batch(js.data(), static_cast<int>(js.size()), sptr(stream));
+  });
   m.def("gpu_reduce", [](std::uintptr_t partials, int n, std::uintptr_t out, std::uintptr_t stream) {
     launch_reduce(dptr<const Partial>(partials), n, dptr<Partial>(out), sptr(stream));
   });

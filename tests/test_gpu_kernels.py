@@ -268,3 +268,21 @@ def test_init_two_equals_init_plus_step(gpu, N, world, rank, decomp, check):
         e = ops.error(lay, b.cpu(), C.compute_box(lay), s, ct2)
         o = out.cpu()
         assert float(o[0]) == e[0] and math.isclose(float(o[1]), e[1], rel_tol=1e-12)
+
+
+def test_reduce_batch_matches_single_reductions(gpu):
+    """k_reduce_batch (one workgroup per job, the deferred reductions of the LDS passes) == k_reduce per job, bit for
+    bit, for job counts across the 64-job launch split and lengths around the 1024-thread stride."""
+    C = gpu
+    torch.manual_seed(7)
+    st = torch.cuda.current_stream().cuda_stream
+    lens = [1, 5, 256, 1023, 1024, 1025, 3000] * 10  # 70 jobs: two launches
+    parts = [torch.rand((n, 2), dtype=torch.float64, device="cuda") for n in lens]
+    a = torch.zeros((len(lens), 2), dtype=torch.float64, device="cuda")
+    b = torch.zeros_like(a)
+    for j, p in enumerate(parts):
+        C.gpu_reduce(p.data_ptr(), p.shape[0], a[j].data_ptr(), st)
+    C.gpu_reduce_batch([(p.data_ptr(), p.shape[0], b[j].data_ptr()) for j, p in enumerate(parts)], st)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert torch.equal(b[:, 0], torch.stack([p[:, 0].max() for p in parts]))

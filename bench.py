@@ -81,9 +81,10 @@ def main() -> int:
     transport = ("torch" if world > 1 else "native") if a.cpu else a.transport
     os.environ.setdefault("W3D_TIMEOUT_S", "180")
 
-    def make(transport, group=None, comm=None, decomp=None, temporal=None):
+    def make(transport, group=None, comm=None, decomp=None, temporal=None, overlap=None):
         return Solver(spec, backend=backend, transport=transport, decomp=decomp or a.decomp, rank=rank, world=world,
-                      device=None if a.cpu else local, overlap=not a.no_overlap, graph=not a.no_graph,
+                      device=None if a.cpu else local, overlap=(not a.no_overlap) if overlap is None else overlap,
+                      graph=not a.no_graph,
                       tiling=_tiling(a), group=group, comm=comm,
                       temporal=temporal or (1 if a.no_temporal else a.temporal), tb=not a.no_tb)
 
@@ -113,9 +114,12 @@ def main() -> int:
     # (--autotune forces it on one rank too: a GPU-box rehearsal of this path)
     autotune = (world > 1 or a.autotune) and not a.no_autotune and (
         transport == "rccl" or (a.cpu and transport in ("torch", "native")))
-    cands = [("slab-S4", "slab", 4), ("slab-S3", "slab", 3), ("slab-S2", "slab", 2), ("slab-S1", "slab", 1)]
+    # "-seq": no overlap — each pass runs whole and its faces go out after it (no shell launches: cheaper compute,
+    # exposed exchange; wins when the links are fast against the ≈ 0.1 ms of shell passes per solve at 8 ranks)
+    cands = [("slab-S4", "slab", 4, True), ("slab-S4-seq", "slab", 4, False), ("slab-S3", "slab", 3, True),
+             ("slab-S2", "slab", 2, True), ("slab-S1", "slab", 1, True)]
     if world >= 4:  # 2x2x1 / 2x2x2 blocks: smaller faces on more links (at 2 ranks "block" is the slab)
-        cands.append(("block-S1", "block", 1))
+        cands.append(("block-S1", "block", 1, True))
     tuned = {}
     solver, r, err, sched = None, None, "", f"{a.decomp}-S{1 if a.no_temporal else a.temporal}"
     if autotune:
@@ -128,10 +132,10 @@ def main() -> int:
             except Exception as e:  # noqa: BLE001
                 ok, err = 0, f"{type(e).__name__}: {e}"
         if agree(ok):
-            for name, dec, temp in cands:
+            for name, dec, temp, ovl in cands:
                 s, t = None, float("inf")
                 try:
-                    s = make(transport, comm=comm, decomp=dec, temporal=temp)
+                    s = make(transport, comm=comm, decomp=dec, temporal=temp, overlap=ovl)
                     s.run()  # eager: RCCL peer connections
                     s.run()  # graph capture
                     t, ok = timed_solve_max(s, 3), 1
@@ -225,7 +229,7 @@ def main() -> int:
                 "parallelism": par,
                 "grid": f"{a.N}^3", "N": a.N, "tau": a.tau, "K": a.K, "L": a.L,
                 "decomp": dims, "transport": transport, "graph": bool(not a.no_graph),
-                "overlap": bool(not a.no_overlap),
+                "overlap": bool(not a.no_overlap) and not sched.endswith("-seq"),
                 "temporal_blocking": bool(not a.no_temporal and (world == 1 or not sched.endswith("S1"))),
                 "schedule": sched if (world > 1 or tuned) else f"fused-single-S{1 if a.no_temporal else a.temporal}",
                 "autotune_ms": tuned or None,

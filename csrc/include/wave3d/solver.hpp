@@ -151,6 +151,8 @@ class GpuSolver {
   };
   bool split() const;
   bool post_exchange() const;  // the unit's NEW field is exchanged after its shell (else: current field, before)
+  // deep-tb without overlap: no shell launches; each pass runs whole and its faces are exchanged after it (on s0)
+  bool late_exchange() const;
   bool needs_exchange(int i) const;
   hipStream_t xstream() const;
   bool pairable() const;

@@ -280,6 +280,8 @@ std::string GpuSolver::mode() const {
 bool GpuSolver::split() const { return opt_.overlap && plan_.any(); }
 bool GpuSolver::post_exchange() const { return mode_ == Mode::kDeep || mode_ == Mode::kDeepTb || split(); }
 
+bool GpuSolver::late_exchange() const { return mode_ == Mode::kDeepTb && !opt_.overlap; }
+
 bool GpuSolver::needs_exchange(int i) const {
   if (!plan_.any()) return false;
   return post_exchange() ? i + 1 < static_cast<int>(units_.size()) : i > 0;
@@ -496,7 +498,7 @@ void GpuSolver::unit_shell(int i) {
   } else if (mode_ == Mode::kDeepTb) {
     // the planes the neighbours receive first: as many as the next pass is deep, next to each neighbour face
     tb_slots_ = 0;
-    if (needs_exchange(i)) {
+    if (needs_exchange(i) && !late_exchange()) {
       const i64 w = units_[static_cast<size_t>(i) + 1].steps;
       if (nb_lo_) tb_pass(u, LBox{full_.x0, imin(full_.x0 + w, full_.x1), full_.y0, full_.y1, full_.z0, full_.z1},
                           kPhaseShell);
@@ -564,7 +566,7 @@ void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase) {
 
 LBox GpuSolver::tb_interior(int i) const {
   LBox b = full_;
-  if (needs_exchange(i)) {
+  if (needs_exchange(i) && !late_exchange()) {
     const i64 w = units_[static_cast<size_t>(i) + 1].steps;
     if (nb_lo_) b.x0 = imin(b.x0 + w, b.x1);
     if (nb_hi_) b.x1 = imax(b.x1 - w, b.x0);
@@ -651,10 +653,12 @@ void GpuSolver::enqueue_solve() {
   phase_init();
   tb_region_ = 0;
   pending_.clear();
+  const bool late = late_exchange();
   for (int i = 0; i < static_cast<int>(units_.size()); ++i) {
     unit_shell(i);
-    unit_exchange_rccl(i);
+    if (!late) unit_exchange_rccl(i);
     unit_interior(i);
+    if (late) unit_exchange_rccl(i);
   }
   flush_reduces();
   final_buf_ = cur_;
@@ -854,12 +858,16 @@ RunResult GpuGroup::run() {
     s->pending_.clear();
   }
   const int nu = static_cast<int>(rs[0]->units_.size());
+  const bool late = rs[0]->late_exchange();
   for (int i = 0; i < nu; ++i) {
     for (auto* s : rs) s->unit_shell(i);
+    if (late)
+      for (auto* s : rs) s->unit_interior(i);
     for (auto* s : rs) s->lb_pack(i);
     for (auto* s : rs) s->lb_pull(i, rs);
     for (auto* s : rs) s->lb_fence(i, rs);
-    for (auto* s : rs) s->unit_interior(i);
+    if (!late)
+      for (auto* s : rs) s->unit_interior(i);
   }
   for (auto* s : rs) s->flush_reduces();
   // combine the per-rank error logs in rank order (what the RCCL all-gather does across processes)

@@ -74,6 +74,6 @@ def test_bench_contract_cpu_two_ranks(tmp_path):
     for k in ("model", "global_batch", "seq_len", "parallelism"):
         assert k in d["config"]
     # the multi-rank schedule autotune ran (over the torch transport here) and picked one of its candidates
-    assert set(d["config"]["autotune_ms"]) == {"slab-S4", "slab-S3", "slab-S2", "slab-S1"}
+    assert set(d["config"]["autotune_ms"]) == {"slab-S4", "slab-S4-seq", "slab-S3", "slab-S2", "slab-S1"}
     assert d["config"]["schedule"] in d["config"]["autotune_ms"]
     assert d["config"]["schedule"] == min(d["config"]["autotune_ms"], key=d["config"]["autotune_ms"].get)

@@ -13,6 +13,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <cctype>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -60,6 +61,26 @@ struct Args {
   int nt_store = -1;
   std::string json, dump, trace;
   bool quiet = false;
+  std::string program = "wave3d";  // reference program personality (argv[0])
+};
+
+// The reference's five programs (readme.md:33-62, report.pdf p.11-15, p.20-26) by executable name, so
+// symlinks to this binary accept their command lines unchanged:
+//   wave N tau K                 sequential          openmpwave / wave3dOMP N tau K T   OpenMP, T threads
+//   [mpirun -np P] onlyMPI|mpi N tau K              MPI: one CPU process per rank
+//   [mpirun -np P] mpiomp N tau K T                 MPI+OpenMP: P processes × T threads
+//   [mpirun -np P] mpigpu-1 N tau K L               MPI+CUDA → one MI355X per rank (the 4th argument is L)
+// (ranks under an external launcher come from its environment; `--np P` spawns them here instead)
+struct Personality {
+  const char* name;
+  bool cpu;
+  bool pos4_threads;  // 4th positional = OpenMP threads (else L)
+  int threads;        // default threads (0: OpenMP default)
+};
+constexpr Personality kPersonalities[] = {
+    {"wave", true, false, 1},      {"openmpwave", true, true, 0}, {"wave3dOMP", true, true, 0},
+    {"onlyMPI", true, false, 1},   {"mpi", true, false, 1},       {"mpiomp", true, true, 0},
+    {"mpigpu-1", false, false, 0},
 };
 
 [[noreturn]] void usage(const char* msg = nullptr) {
@@ -103,6 +124,19 @@ struct Args {
 
 Args parse(int argc, char** argv) {
   Args a;
+  const Personality* pers = nullptr;
+  {
+    std::string prog = argv[0];
+    const size_t sl = prog.find_last_of('/');
+    if (sl != std::string::npos) prog = prog.substr(sl + 1);
+    for (const Personality& q : kPersonalities)
+      if (prog == q.name) pers = &q;
+    if (pers) {
+      a.program = pers->name;
+      a.cpu = pers->cpu;
+      a.threads = pers->threads;
+    }
+  }
   std::vector<std::string> pos;
   for (int i = 1; i < argc; ++i) {
     std::string s = argv[i];
@@ -159,11 +193,33 @@ Args parse(int argc, char** argv) {
   a.prob.tau = std::stod(pos[1]);
   a.prob.K = std::stoi(pos[2]);
   if (pos.size() == 4) {
-    a.prob.L = std::stod(pos[3]);
-    a.have_L = true;
+    if (pers && pers->pos4_threads) {
+      a.threads = std::stoi(pos[3]);
+    } else {
+      a.prob.L = std::stod(pos[3]);
+      a.have_L = true;
+    }
   }
   if (a.repeat < 1) a.repeat = 1;
   return a;
+}
+
+const char* const kRankEnv[] = {"RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID", nullptr};
+const char* const kSizeEnv[] = {"WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "SLURM_NTASKS", nullptr};
+
+// Name of the shared segment of the CPU ranks of one launcher job: W3D_JOB_ID, else the launcher's job id
+// (torchrun TORCHELASTIC_RUN_ID, SLURM_JOB_ID, PMIx namespace), else MASTER_PORT, else the parent pid (the ranks of
+// one node are children of the same launcher process).
+std::string job_segment_name() {
+  static const char* const kJob[] = {"W3D_JOB_ID", "TORCHELASTIC_RUN_ID", "SLURM_JOB_ID", "PMIX_NAMESPACE",
+                                     "OMPI_MCA_orte_ess_jobid", "MASTER_PORT", nullptr};
+  std::string id;
+  for (const char* const* n = kJob; *n && id.empty(); ++n)
+    if (const char* v = std::getenv(*n); v && *v) id = v;
+  if (id.empty()) id = std::to_string(static_cast<long long>(getppid()));
+  std::string name = "/wave3d-cpu-";
+  for (char c : id) name += std::isalnum(static_cast<unsigned char>(c)) ? c : '_';
+  return name;
 }
 
 int env_int(const char* const* names, int dflt) {
@@ -297,8 +353,7 @@ int run_cpu(const Args& a) {
 }
 
 // One rank of the multi-process CPU path (--cpu --np P): the reference's MPI / MPI+OpenMP programs.
-int run_cpu_rank(const Args& a, ShmGroup& g) {
-  const int rank = std::atoi(std::getenv("RANK"));
+int run_cpu_rank(const Args& a, ShmGroup& g, int rank) {
   try {
     CpuRankSolver s(a.prob, g, rank, a.check_every, a.threads);
     // fault injection: W3D_FAULT_RANK=r makes rank r fail before its first exchange
@@ -471,15 +526,24 @@ int main(int argc, char** argv) {
                    a.force ? " Continuing (--force)." : " Use a smaller tau, or --force.");
       if (!a.force) return 2;
     }
-    // multi-process CPU path: the shared segment is mapped before the fork so every rank inherits it
+    // multi-process CPU path: the shared segment is mapped before the fork so every rank inherits it (--np), or, for
+    // ranks started by an external launcher, a named segment keyed by the job
     std::unique_ptr<ShmGroup> group;
+    int cpu_rank = 0;
     if (a.cpu && a.np > 1 && !std::getenv("W3D_SPAWNED"))
       group = std::make_unique<ShmGroup>(a.prob, parse_dims(a.decomp, a.np, a.prob.N), a.np);
     if (a.np > 1 && !std::getenv("W3D_SPAWNED")) {
       const int rc = spawn(a.np, argv);
       if (rc >= 0) return rc;  // parent
     }
-    const int rc = a.cpu ? (group ? run_cpu_rank(a, *group) : run_cpu(a)) : run_gpu(a);
+    if (group) cpu_rank = env_int(kRankEnv, 0);
+    const int lworld = env_int(kSizeEnv, 1);
+    if (a.cpu && !group && a.np <= 1 && lworld > 1 && a.fake_rank < 0) {
+      cpu_rank = env_int(kRankEnv, 0);
+      group = std::make_unique<ShmGroup>(a.prob, parse_dims(a.decomp, lworld, a.prob.N), lworld, job_segment_name(),
+                                         cpu_rank);
+    }
+    const int rc = a.cpu ? (group ? run_cpu_rank(a, *group, cpu_rank) : run_cpu(a)) : run_gpu(a);
     if (rc == 3) std::fprintf(stderr, "wave3d: solution blew up (non-finite error)\n");
     return rc;
   } catch (const std::exception& e) {

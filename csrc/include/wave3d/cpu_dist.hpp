@@ -11,6 +11,7 @@
 
 #include <atomic>
 #include <cstddef>
+#include <string>
 #include <vector>
 
 #include "wave3d/cpu.hpp"
@@ -22,6 +23,10 @@ class ShmGroup {
  public:
   // Map the segment (anonymous, MAP_SHARED) in the parent BEFORE forking the ranks; every child inherits it.
   ShmGroup(const Problem& p, const Dims& d, int world);
+  // Ranks started by an external launcher (`mpirun -np P ./onlyMPI …`, `torchrun --no-python …`, srun): a named POSIX
+  // segment (shm_open), created and initialised by rank 0 and attached by the others once it is marked ready; rank 0
+  // unlinks the name when it is done. Fails after `timeout_s` if rank 0 never shows up.
+  ShmGroup(const Problem& p, const Dims& d, int world, const std::string& name, int rank, double timeout_s = 120.0);
   ~ShmGroup();
   ShmGroup(const ShmGroup&) = delete;
   ShmGroup& operator=(const ShmGroup&) = delete;
@@ -42,7 +47,9 @@ class ShmGroup {
     std::atomic<int> count;
     std::atomic<int> sense;
     std::atomic<int> failed;
+    std::atomic<int> ready;  // named segments: set by rank 0 after initialisation
   };
+  void layout(const Problem& p);  // face and slot offsets, bytes_
   int world_;
   Dims dims_;
   size_t bytes_ = 0, slot_doubles_ = 0;
@@ -52,6 +59,8 @@ class ShmGroup {
   size_t slot_off_ = 0;
   double* data() const;
   int local_sense_ = 0;  // per process (each rank is its own process)
+  std::string name_;     // named segment (empty: anonymous)
+  bool owner_ = false;   // this process unlinks the name
 };
 
 // One rank's block, OpenMP inside the rank. run(): init (analytic, ghosts included) → K−1 steps of {exchange the

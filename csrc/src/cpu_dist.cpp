@@ -1,8 +1,14 @@
 // Native multi-process CPU solver over a shared-memory segment. See wave3d/cpu_dist.hpp.
 #include "wave3d/cpu_dist.hpp"
 
+#include <fcntl.h>
 #include <sched.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <thread>
 
 #include <algorithm>
 #include <chrono>
@@ -24,9 +30,11 @@ size_t round_up_sz(size_t a, size_t b) { return (a + b - 1) / b * b; }
 
 }  // namespace
 
-ShmGroup::ShmGroup(const Problem& p, const Dims& d, int world) : world_(world), dims_(d) {
-  W3D_REQUIRE(world >= 1 && d.size() == world, "ShmGroup: dims do not match the world size");
+void ShmGroup::layout(const Problem& p) {
+  W3D_REQUIRE(world_ >= 1 && dims_.size() == world_, "ShmGroup: dims do not match the world size");
   static_assert(std::atomic<int>::is_always_lock_free, "process-shared atomics must be lock-free");
+  const Dims& d = dims_;
+  const int world = world_;
   size_t off = 0;
   face_off_.resize(static_cast<size_t>(world));
   for (int r = 0; r < world; ++r) {
@@ -42,6 +50,10 @@ ShmGroup::ShmGroup(const Problem& p, const Dims& d, int world) : world_(world), 
   slot_off_ = off;
   off += slot_doubles_ * static_cast<size_t>(world);
   bytes_ = 4096 + off * sizeof(double);
+}
+
+ShmGroup::ShmGroup(const Problem& p, const Dims& d, int world) : world_(world), dims_(d) {
+  layout(p);
   base_ = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
   if (base_ == MAP_FAILED) {
     base_ = nullptr;
@@ -51,10 +63,62 @@ ShmGroup::ShmGroup(const Problem& p, const Dims& d, int world) : world_(world), 
   hdr_->count.store(0);
   hdr_->sense.store(0);
   hdr_->failed.store(0);
+  hdr_->ready.store(1);
+}
+
+ShmGroup::ShmGroup(const Problem& p, const Dims& d, int world, const std::string& name, int rank, double timeout_s)
+    : world_(world), dims_(d), name_(name), owner_(rank == 0) {
+  layout(p);
+  W3D_REQUIRE(!name.empty() && name[0] == '/', "ShmGroup: segment names start with '/'");
+  const double t0 = now_s();
+  int fd = -1;
+  if (owner_) {
+    shm_unlink(name.c_str());  // a stale segment of an aborted run with the same job id
+    fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd < 0) fail("ShmGroup: shm_open(" + name + ") failed: " + std::strerror(errno));
+    if (ftruncate(fd, static_cast<off_t>(bytes_)) != 0) {
+      close(fd);
+      shm_unlink(name.c_str());
+      fail("ShmGroup: ftruncate failed");
+    }
+  } else {
+    for (;;) {  // rank 0 creates the segment: wait for it with its full size
+      fd = shm_open(name.c_str(), O_RDWR, 0600);
+      if (fd >= 0) {
+        struct stat st {};
+        if (fstat(fd, &st) == 0 && static_cast<size_t>(st.st_size) >= bytes_) break;
+        close(fd);
+        fd = -1;
+      }
+      if (now_s() - t0 > timeout_s) fail("ShmGroup: rank 0 did not create " + name + " in time");
+      std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    }
+  }
+  base_ = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (base_ == MAP_FAILED) {
+    base_ = nullptr;
+    if (owner_) shm_unlink(name.c_str());
+    fail("ShmGroup: mmap of " + name + " failed");
+  }
+  hdr_ = static_cast<Header*>(base_);
+  if (owner_) {
+    new (base_) Header;
+    hdr_->count.store(0);
+    hdr_->sense.store(0);
+    hdr_->failed.store(0);
+    hdr_->ready.store(1, std::memory_order_release);
+  } else {
+    while (hdr_->ready.load(std::memory_order_acquire) != 1) {
+      if (now_s() - t0 > timeout_s) fail("ShmGroup: " + name + " never became ready");
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+  }
 }
 
 ShmGroup::~ShmGroup() {
   if (base_) munmap(base_, bytes_);
+  if (owner_ && !name_.empty()) shm_unlink(name_.c_str());
 }
 
 double* ShmGroup::data() const { return reinterpret_cast<double*>(static_cast<char*>(base_) + 4096); }

@@ -99,3 +99,38 @@ def test_cpu_multiprocess_rank_failure_is_an_error():
     assert r.returncode != 0
     assert "injected fault" in r.stderr and "another rank failed" in r.stderr
     assert time.time() - t0 < 30
+
+
+def test_reference_program_personalities():
+    """The build links the reference's program names to the CLI (tools/build.py); argv[0] picks the behaviour:
+    `wave N tau K` sequential, `wave3dOMP N tau K T` / `mpiomp N tau K T` take OpenMP threads as the 4th argument,
+    `mpigpu-1 N tau K L` takes L (report.pdf p.12-15, p.20-24)."""
+    seq = run(40, 0.001, 6, "--cpu", "--threads", 1)
+    b = os.path.join(ROOT, "bin")
+    for prog, extra, threads in (("wave", [], 1), ("wave3dOMP", [3], 3), ("openmpwave", [2], 2), ("mpiomp", [2], 2)):
+        out = subprocess.run([os.path.join(b, prog), "40", "0.001", "6", *map(str, extra)], capture_output=True,
+                             text=True, check=True, timeout=120).stdout
+        assert [l for l in out.splitlines() if l.startswith("Step ")] == \
+            [l for l in seq.stdout.splitlines() if l.startswith("Step ")]
+        assert f"threads {threads}" in out, (prog, out)
+
+
+def test_mpi_program_under_external_launcher():
+    """`mpirun -np P ./onlyMPI N tau K` semantics: P independently started processes with the launcher's rank env find
+    each other through a named shared-memory segment (keyed by the job id) and print the sequential program's log."""
+    import uuid
+
+    seq = run(36, 0.001, 6, "--cpu", "--threads", 1)
+    job = uuid.uuid4().hex[:12]
+    prog = os.path.join(ROOT, "bin", "onlyMPI")
+    procs = []
+    for r in range(3):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="3", LOCAL_RANK=str(r), W3D_JOB_ID=job)
+        procs.append(subprocess.Popen([prog, "36", "0.001", "6"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                      text=True, env=env))
+    outs = [p.communicate(timeout=120) for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    lines = [l for l in outs[0][0].splitlines() if l.startswith("Step ")]
+    assert lines == [l for l in seq.stdout.splitlines() if l.startswith("Step ")] and len(lines) == 3
+    assert "max over 3 ranks" in outs[0][0]
+    assert not os.path.exists(f"/dev/shm/wave3d-cpu-{job}")  # rank 0 unlinked the segment

@@ -52,6 +52,7 @@ LIB_SOURCES = [
 ]
 EXT_SOURCES = [("src/bindings.cpp", "hip")]
 CLI_SOURCES = [("app/wave3d_main.cpp", "hip")]
+PERSONALITIES = ["wave", "openmpwave", "wave3dOMP", "onlyMPI", "mpi", "mpiomp", "mpigpu-1"]
 
 
 def _pybind_includes() -> list[str]:
@@ -133,6 +134,12 @@ def build(jobs: int = 8, force: bool = False, cli: bool = True, verbose: bool = 
     if cli:
         _link(lib_objs + [objs[s] for s, _ in CLI_SOURCES], cli_path(), shared=False, verbose=verbose)
         out["cli"] = str(cli_path())
+        # the reference's program names (the CLI picks its personality from argv[0]; csrc/app/wave3d_main.cpp)
+        for name in PERSONALITIES:
+            link = cli_path().parent / name
+            if link.is_symlink() or link.exists():
+                link.unlink()
+            link.symlink_to(cli_path().name)
     return out
 
 

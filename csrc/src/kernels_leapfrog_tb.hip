@@ -284,8 +284,14 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     // the thread's own entries of both φ slots. Every neighbour value is the product u1_at forms for it, so u¹ is
     // bit-identical to k_init_first's; 2 products + 4 LDS reads instead of 12 products + 9 table reads per node.
     // The halo ring (no φ neighbours beyond it in LDS) keeps u1_at.
+    // (S = 4: the queues leave no room for them — the factors are re-read from the LDS tables per use instead)
+    constexpr bool kFacReg = S < 4;
     double fy[Q], fz[Q], fyr[QR], fzr[QR];
-    if constexpr (INIT) {
+    auto fyq = [&](int q) { return kFacReg ? fy[q] : syw[ytab(lid[q])]; };
+    auto fzq = [&](int q) { return kFacReg ? fz[q] : szw[ztab(lid[q])]; };
+    auto fyrr = [&](int r) { return kFacReg ? fyr[r] : syw[ytab(lrid[r])]; };
+    auto fzrr = [&](int r) { return kFacReg ? fzr[r] : szw[ztab(lrid[r])]; };
+    if constexpr (INIT && kFacReg) {
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         fy[q] = syw[ytab(lid[q])];
@@ -304,10 +310,10 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       const double sx = sxw[x + xtab0];
 #pragma unroll
       for (int q = 0; q < Q; ++q)
-        if (wsm[q]) d[lid[q]] = (sx * fy[q]) * fz[q];
+        if (wsm[q]) d[lid[q]] = (sx * fyq(q)) * fzq(q);
 #pragma unroll
       for (int r = 0; r < QR; ++r)
-        if (wbase_r + r * NT < G::NR) d[lrid[r]] = (sx * fyr[r]) * fzr[r];
+        if (wbase_r + r * NT < G::NR) d[lrid[r]] = (sx * fyrr(r)) * fzrr(r);
     };
     // iteration i of the analytic pass (F = (i − i0) & 3): u¹ of plane i+2 into L[0] slot (F+2)&3 / Rg slot (F+2)&1,
     // u⁰ = φ of plane i+1 into Lm slot (F+1)&1; φ of plane i+3 into its slot. φ slot (i+2)&1 was completed in the
@@ -324,7 +330,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         if (!wsm[q]) continue;  // wave-uniform
         const int li = lid[q];
         const double f1 = p3[li];                    // φ(i+1), own entry
-        const double f3 = (sx3 * fy[q]) * fz[q];     // φ(i+3)
+        const double f3 = (sx3 * fyq(q)) * fzq(q);   // φ(i+3)
         p3[li] = f3;
         const double c = p2[li];                     // φ(i+2)
         const double lap = lap7(c, f1, f3, p2[li - W0], p2[li + W0], p2[li - 1], p2[li + 1], ihx2, ihy2, ihz2);
@@ -334,7 +340,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
 #pragma unroll
       for (int r = 0; r < QR; ++r) {
         if (wbase_r + r * NT < G::NR) {
-          p3[lrid[r]] = (sx3 * fyr[r]) * fzr[r];
+          p3[lrid[r]] = (sx3 * fyrr(r)) * fzrr(r);
           Rg[r][(F + 2) & 1] = u1_at(i + 2, lrid[r], grof[r] & kReal);
         }
       }

@@ -316,8 +316,8 @@ void GpuSolver::build_units() {
     // first pass reads nothing but computes u⁰, u¹ (compute-bound). Slab ranks (deep-tb) take passes of ≥ 2 steps
     // only: every pass writes the two levels the next one reads, so each exchange is one message pair per face.
     static const double kStepCost[5] = {0.0, 610.0, 495.0, 327.0, 272.0};
-    // (analytic: φ-stage start, re-measured; its 4-step variant spills)
-    static const double kAnalyticCost[5] = {0.0, 1e9, 346.0, 300.0, 449.0};
+    // (analytic: φ-stage start, re-measured)
+    static const double kAnalyticCost[5] = {0.0, 1e9, 346.0, 300.0, 318.0};
     const int rem = K - n, smax = opt_.temporal, smin = mode_ == Mode::kDeepTb ? 2 : 1;
     std::vector<double> best(static_cast<size_t>(rem + 1), 1e300);
     std::vector<int> take(static_cast<size_t>(rem + 1), 1);

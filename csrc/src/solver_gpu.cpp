@@ -315,7 +315,7 @@ void GpuSolver::build_units() {
     // pass of s steps with every 2nd level checked, measured at 512³ (tools/tune_leapfrog.py --tb); the analytic
     // first pass reads nothing but computes u⁰, u¹ (compute-bound). Slab ranks (deep-tb) take passes of ≥ 2 steps
     // only: every pass writes the two levels the next one reads, so each exchange is one message pair per face.
-    static const double kStepCost[5] = {0.0, 610.0, 495.0, 327.0, 272.0};
+    static const double kStepCost[5] = {0.0, 610.0, 437.0, 302.0, 258.0};
     // (analytic: φ-stage start, re-measured)
     static const double kAnalyticCost[5] = {0.0, 1e9, 346.0, 300.0, 318.0};
     const int rem = K - n, smax = opt_.temporal, smin = mode_ == Mode::kDeepTb ? 2 : 1;

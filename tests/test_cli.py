@@ -13,7 +13,7 @@ CLI = os.path.join(ROOT, "bin", "wave3d")
 
 @pytest.fixture(scope="module", autouse=True)
 def cli_built():
-    if not os.path.exists(CLI):
+    if not os.path.exists(CLI) or not os.path.lexists(os.path.join(ROOT, "bin", "mpiomp")):
         from mpi_cuda_amd._native import load
 
         load()

@@ -287,6 +287,10 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     // (S = 4: the queues leave no room for them — the factors are re-read from the LDS tables per use instead)
     constexpr bool kFacReg = S < 4;
     double fy[Q], fz[Q], fyr[QR], fzr[QR];
+    // checked passes: each position's z factor of the analytic solution (loop-invariant) in a register
+    double czs[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) czs[q] = (CM != 0 && p.check_mask) ? szw[ztab(lid[q])] : 0.0;
     auto fyq = [&](int q) { return kFacReg ? fy[q] : syw[ytab(lid[q])]; };
     auto fzq = [&](int q) { return kFacReg ? fz[q] : szw[ztab(lid[q])]; };
     auto fyrr = [&](int r) { return kFacReg ? fyr[r] : syw[ytab(lrid[r])]; };
@@ -388,7 +392,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         }
         if constexpr (kChk) {
           if (chk && own && xreal) {
-            const double e = fabs(v - (rowk[ytab(li)] * szw[ztab(li)]) * p.ct[k - 1]);
+            const double e = fabs(v - (rowk[ytab(li)] * czs[q]) * p.ct[k - 1]);
             emax[k - 1] = fmax(e, emax[k - 1]);  // = (e > m ? e : m) for every non-NaN e; a NaN shows in the sum
             esum[k - 1] += e * e;
           }

@@ -152,8 +152,9 @@ def laplacian_torch(u: torch.Tensor, h: float) -> torch.Tensor:
     ih2 = 1.0 / (h * h)
     c = u[1:-1, 1:-1, 1:-1]
     c2 = 2.0 * c
-    return ((u[2:, 1:-1, 1:-1] - c2 + u[:-2, 1:-1, 1:-1]) * ih2 + (u[1:-1, 2:, 1:-1] - c2 + u[1:-1, :-2, 1:-1]) * ih2
-            + (u[1:-1, 1:-1, 2:] - c2 + u[1:-1, 1:-1, :-2]) * ih2)
+    # one 1/h² factor for the three second differences (uniform h), like stencil.hpp::lap7
+    return ((u[2:, 1:-1, 1:-1] - c2 + u[:-2, 1:-1, 1:-1]) + (u[1:-1, 2:, 1:-1] - c2 + u[1:-1, :-2, 1:-1])
+            + (u[1:-1, 1:-1, 2:] - c2 + u[1:-1, 1:-1, :-2])) * ih2
 
 
 def torch_reference_solve(spec: ProblemSpec, device="cpu", return_fields: bool = False):

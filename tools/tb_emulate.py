@@ -23,8 +23,8 @@ class Geom:
 
 
 def lap7(c, xm, xp, ym, yp, zm, zp, ihx2, ihy2, ihz2):
-    c2 = 2.0 * c
-    return (xp - c2 + xm) * ihx2 + (yp - c2 + ym) * ihy2 + (zp - c2 + zm) * ihz2
+    c2 = 2.0 * c  # uniform h: one 1/h² factor, as stencil.hpp::lap7
+    return ((xp - c2 + xm) + (yp - c2 + ym) + (zp - c2 + zm)) * ihx2
 
 
 def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2: np.ndarray, box, s_ext: np.ndarray,

@@ -46,6 +46,8 @@ struct Coeffs {
   double ihx2, ihy2, ihz2;  // 1/h_d²
   double tau2;              // τ²
   double half_tau2;         // τ²/2
+  double lam;               // τ²/h²: the update coefficient of d2sum (stencil.hpp)
+  double half_lam;          // (τ²/2)/h²
 
   static Coeffs from(const Problem& p) {
     Coeffs c;
@@ -55,6 +57,8 @@ struct Coeffs {
     c.ihz2 = c.ihx2;
     c.tau2 = p.tau * p.tau;
     c.half_tau2 = 0.5 * c.tau2;
+    c.lam = c.tau2 * c.ihx2;
+    c.half_lam = c.half_tau2 * c.ihx2;
     return c;
   }
 };

@@ -103,7 +103,9 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("ihy2", &Coeffs::ihy2)
       .def_readonly("ihz2", &Coeffs::ihz2)
       .def_readonly("tau2", &Coeffs::tau2)
-      .def_readonly("half_tau2", &Coeffs::half_tau2);
+      .def_readonly("half_tau2", &Coeffs::half_tau2)
+      .def_readonly("lam", &Coeffs::lam)
+      .def_readonly("half_lam", &Coeffs::half_lam);
 
   m.def("sin_table_ext", [](const Problem& p) {
     auto v = sin_table_ext(p);

@@ -40,10 +40,9 @@ void cpu_init_first(const Layout& l, const Coeffs& c, const double* s, double* u
         u0[o] = v;
         const bool interior = gx > 0 && gx < N && gy > 0 && gy < N && gz > 0 && gz < N;
         if (interior) {
-          const double lap = lap7(v, phi(s, gx - 1, gy, gz), phi(s, gx + 1, gy, gz), phi(s, gx, gy - 1, gz),
-                                  phi(s, gx, gy + 1, gz), phi(s, gx, gy, gz - 1), phi(s, gx, gy, gz + 1), c.ihx2,
-                                  c.ihy2, c.ihz2);
-          u1[o] = first_step(v, lap, c.half_tau2);
+          const double lap = d2sum(v, phi(s, gx - 1, gy, gz), phi(s, gx + 1, gy, gz), phi(s, gx, gy - 1, gz),
+                                  phi(s, gx, gy + 1, gz), phi(s, gx, gy, gz - 1), phi(s, gx, gy, gz + 1));
+          u1[o] = first_step(v, lap, c.half_lam);
         } else {
           u1[o] = 0.0;
         }
@@ -72,8 +71,8 @@ void leapfrog_impl(const Layout& l, const Coeffs& c, const double* cur, double* 
       for (i64 iz = b.z0; iz < b.z1; ++iz) {
         const double u = cr[iz];
         const double lap =
-            lap7(u, cr[iz - P], cr[iz + P], cr[iz - R], cr[iz + R], cr[iz - 1], cr[iz + 1], c.ihx2, c.ihy2, c.ihz2);
-        const double v = leapfrog(u, orow[iz], lap, c.tau2);
+            d2sum(u, cr[iz - P], cr[iz + P], cr[iz - R], cr[iz + R], cr[iz - 1], cr[iz + 1]);
+        const double v = leapfrog(u, orow[iz], lap, c.lam);
         orow[iz] = v;
         if (CHECK) {
           const double e = std::fabs(v - (sxy * s[l.gz0 + iz]) * ct);

@@ -96,7 +96,6 @@ __global__ __launch_bounds__(64 * kWaves) void k_init_two(const Init2Params p) {
     const i64 g = p.gy0 + yt - 1 + j;
     yi[j] = g > 0 && g < N;
   }
-  const double ihx2 = p.ihx2, ihy2 = p.ihy2, ihz2 = p.ihz2;
 
   // u¹ of plane x (global gx) for all J rows, both elements
   auto u1_plane = [&](i64 lx, v2d* out) {
@@ -111,8 +110,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_init_two(const Init2Params p) {
       for (int e = 0; e < 2; ++e) {
         const double zc = Z[e + 1];
         const double v = (xc * yc) * zc;
-        const double lap = lap7(v, (xm * yc) * zc, (xp * yc) * zc, (xc * ym) * zc, (xc * yp) * zc, (xc * yc) * Z[e],
-                                (xc * yc) * Z[e + 2], ihx2, ihy2, ihz2);
+        const double lap = d2sum(v, (xm * yc) * zc, (xp * yc) * zc, (xc * ym) * zc, (xc * yp) * zc, (xc * yc) * Z[e],
+                                (xc * yc) * Z[e + 2]);
         const bool in = xi && yi[j] && (e == 0 ? zi0 : zi1);
         r[e] = in ? first_step(v, lap, p.half_tau2) : 0.0;
       }
@@ -140,8 +139,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_init_two(const Init2Params p) {
       const double zm = __shfl_up(uc[j].y, 1, 64);
       const double zp = __shfl_down(uc[j].x, 1, 64);
       v2d u2v;
-      const double l0 = lap7(uc[j].x, um[j].x, up[j].x, uc[j - 1].x, uc[j + 1].x, zm, uc[j].y, ihx2, ihy2, ihz2);
-      const double l1 = lap7(uc[j].y, um[j].y, up[j].y, uc[j - 1].y, uc[j + 1].y, uc[j].x, zp, ihx2, ihy2, ihz2);
+      const double l0 = d2sum(uc[j].x, um[j].x, up[j].x, uc[j - 1].x, uc[j + 1].x, zm, uc[j].y);
+      const double l1 = d2sum(uc[j].y, um[j].y, up[j].y, uc[j - 1].y, uc[j + 1].y, uc[j].x, zp);
       const double yc = Y[j + 1];
       const double u00 = (xc * yc) * Z[1], u01 = (xc * yc) * Z[2];  // u⁰ = φ
       const bool in = xi && yi[j];
@@ -216,8 +215,8 @@ Init2Params make_params(const Layout& l, const Coeffs& c) {
   p.ihx2 = c.ihx2;
   p.ihy2 = c.ihy2;
   p.ihz2 = c.ihz2;
-  p.half_tau2 = c.half_tau2;
-  p.tau2 = c.tau2;
+  p.half_tau2 = c.half_lam;  // (the update coefficients of d2sum: τ²/(2h²), τ²/h²)
+  p.tau2 = c.lam;
   const i64 nxb = p.x1 - p.x0, nyb = p.y1 - p.y0;
   if (nxb <= 0 || nyb <= 0 || p.pz_end <= p.pz0) return p;  // nothing to write
   p.ntz = static_cast<int>(ceil_div(p.pz_end - p.pz0, kOutPairs));

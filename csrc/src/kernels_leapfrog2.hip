@@ -143,7 +143,7 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(OCC
       }
     }
   }
-  const double ihx2 = p.ihx2, ihy2 = p.ihy2, ihz2 = p.ihz2, tau2 = p.tau2;
+  const double tau2 = p.tau2;  // = τ²/h² (the coefficient of d2sum)
   double emax = 0.0, esum = 0.0;
   double sz0 = 0.0, sz1 = 0.0, sx = 0.0;
   double sy[R];
@@ -185,8 +185,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(OCC
       const v2d ym = c[e - 1], yp = c[e + 1];
       const double zm = __shfl_up(c[e].y, 1, 64);
       const double zp = __shfl_down(c[e].x, 1, 64);
-      const double l0 = lap7(c[e].x, m[e].x, q[e].x, ym.x, yp.x, zm, c[e].y, ihx2, ihy2, ihz2);
-      const double l1 = lap7(c[e].y, m[e].y, q[e].y, ym.y, yp.y, c[e].x, zp, ihx2, ihy2, ihz2);
+      const double l0 = d2sum(c[e].x, m[e].x, q[e].x, ym.x, yp.x, zm, c[e].y);
+      const double l1 = d2sum(c[e].y, m[e].y, q[e].y, ym.y, yp.y, c[e].x, zp);
       const bool keep = xin && ri[e];
       a[e].x = keep && in0 ? leapfrog(c[e].x, o[e].x, l0, tau2) : 0.0;
       a[e].y = keep && in1 ? leapfrog(c[e].y, o[e].y, l1, tau2) : 0.0;
@@ -208,8 +208,8 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(OCC
         const v2d ctr = w1[e];
         const double zm = __shfl_up(ctr.y, 1, 64);
         const double zp = __shfl_down(ctr.x, 1, 64);
-        const double l0 = lap7(ctr.x, w2[e].x, a[e].x, w1[e - 1].x, w1[e + 1].x, zm, ctr.y, ihx2, ihy2, ihz2);
-        const double l1 = lap7(ctr.y, w2[e].y, a[e].y, w1[e - 1].y, w1[e + 1].y, ctr.x, zp, ihx2, ihy2, ihz2);
+        const double l0 = d2sum(ctr.x, w2[e].x, a[e].x, w1[e - 1].x, w1[e + 1].x, zm, ctr.y);
+        const double l1 = d2sum(ctr.y, w2[e].y, a[e].y, w1[e - 1].y, w1[e + 1].y, ctr.x, zp);
         v2d v;
         v.x = leapfrog(ctr.x, m[e].x, l0, tau2);
         v.y = leapfrog(ctr.y, m[e].y, l1, tau2);
@@ -363,7 +363,7 @@ void launch_leapfrog2(const Layout& l, const Coeffs& c, const double* prev, cons
   p.ihx2 = c.ihx2;
   p.ihy2 = c.ihy2;
   p.ihz2 = c.ihz2;
-  p.tau2 = c.tau2;
+  p.tau2 = c.lam;  // τ²/h², the coefficient of d2sum
   p.ct2 = ct2;
   const bool check = partials != nullptr;
   switch (t.rows) {

@@ -122,7 +122,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
   const int N = p.N;
   const i64 P = p.plane;
   const int R = static_cast<int>(p.pitch), zs1 = static_cast<int>(p.zs) + 1;
-  const double ihx2 = p.ihx2, ihy2 = p.ihy2, ihz2 = p.ihz2, tau2 = p.tau2;
+  const double tau2 = p.tau2;  // = τ²/h² (the coefficient of d2sum)
   auto inside = [&](int g) { return static_cast<unsigned>(g - 1) < static_cast<unsigned>(N - 1); };
 
   double emax[S], esum[S];
@@ -217,8 +217,8 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       const double sxc = sxw[xi], sy = syw[ya], sz = szw[zb];
       const double cy = sxc * sy;
       const double c = cy * sz;
-      const double lap = lap7(c, (sxw[xi - 1] * sy) * sz, (sxw[xi + 1] * sy) * sz, (sxc * syw[ya - 1]) * sz,
-                              (sxc * syw[ya + 1]) * sz, cy * szw[zb - 1], cy * szw[zb + 1], ihx2, ihy2, ihz2);
+      const double lap = d2sum(c, (sxw[xi - 1] * sy) * sz, (sxw[xi + 1] * sy) * sz, (sxc * syw[ya - 1]) * sz,
+                              (sxc * syw[ya + 1]) * sz, cy * szw[zb - 1], cy * szw[zb + 1]);
       return (real_yz && inside(p.gx0 + x)) ? first_step(c, lap, p.half_tau2) : 0.0;
     };
 
@@ -337,7 +337,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         const double f3 = (sx3 * fyq(q)) * fzq(q);   // φ(i+3)
         p3[li] = f3;
         const double c = p2[li];                     // φ(i+2)
-        const double lap = lap7(c, f1, f3, p2[li - W0], p2[li + W0], p2[li - 1], p2[li + 1], ihx2, ihy2, ihz2);
+        const double lap = d2sum(c, f1, f3, p2[li - W0], p2[li + W0], p2[li - 1], p2[li + 1]);
         L[0][q][(F + 2) & 3] = ((gof[q] & kReal) && xin) ? first_step(c, lap, p.half_tau2) : 0.0;
         Lm[q][(F + 1) & 1] = f1;
       }
@@ -371,8 +371,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         if (!((wsm[q] >> (k - 1)) & 1)) continue;  // wave-uniform
         const int li = lid[q];
         const double c = L[k - 1][q][s0];
-        const double lap = lap7(c, L[k - 1][q][sm], L[k - 1][q][sp], nb[li - W0], nb[li + W0], nb[li - 1], nb[li + 1],
-                                ihx2, ihy2, ihz2);
+        const double lap = d2sum(c, L[k - 1][q][sm], L[k - 1][q][sp], nb[li - W0], nb[li + W0], nb[li - 1], nb[li + 1]);
         double o;
         if constexpr (k == 1)
           o = Lm[q][D & 1];
@@ -711,8 +710,8 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
   p.ihx2 = c.ihx2;
   p.ihy2 = c.ihy2;
   p.ihz2 = c.ihz2;
-  p.tau2 = c.tau2;
-  p.half_tau2 = c.half_tau2;
+  p.tau2 = c.lam;  // τ²/h² and τ²/(2h²): the coefficients of d2sum
+  p.half_tau2 = c.half_lam;
   p.check_mask = partials != nullptr ? (check_mask & ((1 << t.stages) - 1)) : 0;
   p.partials = p.check_mask != 0 ? partials : nullptr;
   W3D_REQUIRE(level_stride == 0 || level_stride >= pl.nblocks, "leapfrog_tb: level stride below the block count");

@@ -88,9 +88,8 @@ __global__ __launch_bounds__(256) void k_init_first(const InitParams p) {
       const i64 gz = p.gz0 + iz;
       v = phi(s, gx, gy, gz);
       if (xy_in && gz > 0 && gz < p.N) {
-        const double lap = lap7(v, phi(s, gx - 1, gy, gz), phi(s, gx + 1, gy, gz), phi(s, gx, gy - 1, gz),
-                                phi(s, gx, gy + 1, gz), phi(s, gx, gy, gz - 1), phi(s, gx, gy, gz + 1), p.ihx2, p.ihy2,
-                                p.ihz2);
+        const double lap = d2sum(v, phi(s, gx - 1, gy, gz), phi(s, gx + 1, gy, gz), phi(s, gx, gy - 1, gz),
+                                phi(s, gx, gy + 1, gz), phi(s, gx, gy, gz - 1), phi(s, gx, gy, gz + 1));
         w = first_step(v, lap, p.half_tau2);
       }
     }
@@ -204,7 +203,7 @@ __global__ __launch_bounds__(kLanes* TY) void k_leapfrog_lds(const LfParams p) {
   }
   if (hr >= 0) hv = ld2(cur + px + hoff);
 
-  const double ihx2 = p.ihx2, ihy2 = p.ihy2, ihz2 = p.ihz2, tau2 = p.tau2;
+  const double tau2 = p.tau2;  // = τ²/h² (the coefficient of d2sum)
   double emax = 0.0, esum = 0.0;
   double sxy = 0.0, sz0 = 0.0, sz1 = 0.0, sxp = CHECK ? p.s[p.gx0 + xs] : 0.0;
   if (CHECK && active) {
@@ -233,8 +232,8 @@ __global__ __launch_bounds__(kLanes* TY) void k_leapfrog_lds(const LfParams p) {
       const v2d yp = lds[buf][row + 2][lane + 1];
       const double zm = lds[buf][row + 1][lane].y;
       const double zp = lds[buf][row + 1][lane + 2].x;
-      const double l0 = lap7(uc.x, um.x, up.x, ym.x, yp.x, zm, uc.y, ihx2, ihy2, ihz2);
-      const double l1 = lap7(uc.y, um.y, up.y, ym.y, yp.y, uc.x, zp, ihx2, ihy2, ihz2);
+      const double l0 = d2sum(uc.x, um.x, up.x, ym.x, yp.x, zm, uc.y);
+      const double l1 = d2sum(uc.y, um.y, up.y, ym.y, yp.y, uc.x, zp);
       v2d r;
       r.x = leapfrog(uc.x, uo.x, l0, tau2);
       r.y = leapfrog(uc.y, uo.y, l1, tau2);
@@ -372,7 +371,7 @@ __global__ __launch_bounds__(64 * kWavesRq) __attribute__((amdgpu_waves_per_eu(R
     ht = ld2(cur + px + top);
     hb = ld2(cur + px + bot);
   }
-  const double ihx2 = p.ihx2, ihy2 = p.ihy2, ihz2 = p.ihz2, tau2 = p.tau2;
+  const double tau2 = p.tau2;  // = τ²/h² (the coefficient of d2sum)
   double emax = 0.0, esum = 0.0;
   // error-epilogue factors of φ are loaded up front / one plane ahead, like every other load: vector-memory
   // completion is in order, so a load consumed in the same iteration would drain the whole prefetch queue
@@ -421,8 +420,8 @@ __global__ __launch_bounds__(64 * kWavesRq) __attribute__((amdgpu_waves_per_eu(R
         const double hzs = npe == 1 ? __shfl_down(hz[r], 1, 64) : hz[r];
         const double zm = lane == 0 ? hz[r] : up_y;
         const double zp = lane == npe - 1 ? hzs : dn_x;
-        const double l0 = lap7(c[r].x, m[r].x, q[r].x, ym.x, yp.x, zm, c[r].y, ihx2, ihy2, ihz2);
-        const double l1 = lap7(c[r].y, m[r].y, q[r].y, ym.y, yp.y, c[r].x, zp, ihx2, ihy2, ihz2);
+        const double l0 = d2sum(c[r].x, m[r].x, q[r].x, ym.x, yp.x, zm, c[r].y);
+        const double l1 = d2sum(c[r].y, m[r].y, q[r].y, ym.y, yp.y, c[r].x, zp);
         v2d v;
         v.x = leapfrog(c[r].x, o[r].x, l0, tau2);
         v.y = leapfrog(c[r].y, o[r].y, l1, tau2);
@@ -687,7 +686,7 @@ InitParams init_params(const Layout& l, const Coeffs& c, const double* d_s, doub
   p.ihx2 = c.ihx2;
   p.ihy2 = c.ihy2;
   p.ihz2 = c.ihz2;
-  p.half_tau2 = c.half_tau2;
+  p.half_tau2 = c.half_lam;  // τ²/(2h²), the coefficient of d2sum
   return p;
 }
 }  // namespace
@@ -716,7 +715,7 @@ void launch_leapfrog(const Layout& l, const Coeffs& c, const double* cur, double
   p.ihx2 = c.ihx2;
   p.ihy2 = c.ihy2;
   p.ihz2 = c.ihz2;
-  p.tau2 = c.tau2;
+  p.tau2 = c.lam;  // τ²/h², the coefficient of d2sum
   p.ct = ct;
   const bool check = partials != nullptr;
   if (t.variant == 1) {

@@ -147,14 +147,18 @@ def oracle_errors(spec: ProblemSpec, steps: list[int] | None = None, dps: int = 
 # ----------------------------------------------------------------------------------------------------------------
 # independent PyTorch fp64 reference solver (second oracle; runs on CPU or GPU)
 # ----------------------------------------------------------------------------------------------------------------
-def laplacian_torch(u: torch.Tensor, h: float) -> torch.Tensor:
-    """7-point Δ_h on the interior of a full node grid (same operation order as the native kernels)."""
-    ih2 = 1.0 / (h * h)
+def d2sum_torch(u: torch.Tensor) -> torch.Tensor:
+    """h²·Δ_h on the interior of a full node grid: the sum of the three second differences (stencil.hpp::d2sum, same
+    operation order as the native kernels)."""
     c = u[1:-1, 1:-1, 1:-1]
     c2 = 2.0 * c
-    # one 1/h² factor for the three second differences (uniform h), like stencil.hpp::lap7
     return ((u[2:, 1:-1, 1:-1] - c2 + u[:-2, 1:-1, 1:-1]) + (u[1:-1, 2:, 1:-1] - c2 + u[1:-1, :-2, 1:-1])
-            + (u[1:-1, 1:-1, 2:] - c2 + u[1:-1, 1:-1, :-2])) * ih2
+            + (u[1:-1, 1:-1, 2:] - c2 + u[1:-1, 1:-1, :-2]))
+
+
+def laplacian_torch(u: torch.Tensor, h: float) -> torch.Tensor:
+    """7-point Δ_h on the interior of a full node grid."""
+    return d2sum_torch(u) * (1.0 / (h * h))
 
 
 def torch_reference_solve(spec: ProblemSpec, device="cpu", return_fields: bool = False):
@@ -165,7 +169,9 @@ def torch_reference_solve(spec: ProblemSpec, device="cpu", return_fields: bool =
     u0[:, 0], u0[:, -1] = 0.0, 0.0
     u0[:, :, 0], u0[:, :, -1] = 0.0, 0.0
     u1 = torch.zeros_like(u0)
-    u1[1:-1, 1:-1, 1:-1] = u0[1:-1, 1:-1, 1:-1] + (0.5 * tau2) * laplacian_torch(u0, spec.h)
+    ih2 = 1.0 / (spec.h * spec.h)
+    lam, half_lam = tau2 * ih2, (0.5 * tau2) * ih2  # problem.hpp::Coeffs: the coefficients of d2sum
+    u1[1:-1, 1:-1, 1:-1] = u0[1:-1, 1:-1, 1:-1] + half_lam * d2sum_torch(u0)
     denom = float(spec.N - 1) ** 3
     errs = {}
     checks = set(spec.check_steps())
@@ -180,7 +186,7 @@ def torch_reference_solve(spec: ProblemSpec, device="cpu", return_fields: bool =
     for n in range(1, spec.K):
         nxt = torch.zeros_like(cur)
         c = cur[1:-1, 1:-1, 1:-1]
-        nxt[1:-1, 1:-1, 1:-1] = (2.0 * c - prev[1:-1, 1:-1, 1:-1]) + tau2 * laplacian_torch(cur, spec.h)
+        nxt[1:-1, 1:-1, 1:-1] = (2.0 * c - prev[1:-1, 1:-1, 1:-1]) + lam * d2sum_torch(cur)
         prev, cur = cur, nxt
         if n + 1 in checks:
             errs[n + 1] = err(cur, n + 1)

@@ -185,9 +185,9 @@ def ref_leapfrog_grid(cur: torch.Tensor, old: torch.Tensor, ihx2: float, ihy2: f
     x0, x1, y0, y1, z0, z1 = (box.x0 + 1, box.x1 + 1, box.y0 + 1, box.y1 + 1, box.z0 + 1, box.z1 + 1)
     c = cur[x0:x1, y0:y1, z0:z1]
     c2 = 2.0 * c
-    assert ihx2 == ihy2 == ihz2, "uniform grid: one 1/h² factor (stencil.hpp::lap7)"
-    lap = ((cur[x0 + 1:x1 + 1, y0:y1, z0:z1] - c2 + cur[x0 - 1:x1 - 1, y0:y1, z0:z1])
-           + (cur[x0:x1, y0 + 1:y1 + 1, z0:z1] - c2 + cur[x0:x1, y0 - 1:y1 - 1, z0:z1])
-           + (cur[x0:x1, y0:y1, z0 + 1:z1 + 1] - c2 + cur[x0:x1, y0:y1, z0 - 1:z1 - 1])) * ihx2
-    out[x0:x1, y0:y1, z0:z1] = (2.0 * c - old[x0:x1, y0:y1, z0:z1]) + tau2 * lap
+    assert ihx2 == ihy2 == ihz2, "uniform grid: one 1/h² factor (stencil.hpp::d2sum)"
+    s = ((cur[x0 + 1:x1 + 1, y0:y1, z0:z1] - c2 + cur[x0 - 1:x1 - 1, y0:y1, z0:z1])
+         + (cur[x0:x1, y0 + 1:y1 + 1, z0:z1] - c2 + cur[x0:x1, y0 - 1:y1 - 1, z0:z1])
+         + (cur[x0:x1, y0:y1, z0 + 1:z1 + 1] - c2 + cur[x0:x1, y0:y1, z0 - 1:z1 - 1]))
+    out[x0:x1, y0:y1, z0:z1] = (2.0 * c - old[x0:x1, y0:y1, z0:z1]) + (tau2 * ihx2) * s
     return out

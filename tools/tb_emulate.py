@@ -23,8 +23,8 @@ class Geom:
 
 
 def lap7(c, xm, xp, ym, yp, zm, zp, ihx2, ihy2, ihz2):
-    c2 = 2.0 * c  # uniform h: one 1/h² factor, as stencil.hpp::lap7
-    return ((xp - c2 + xm) + (yp - c2 + ym) + (zp - c2 + zm)) * ihx2
+    c2 = 2.0 * c  # stencil.hpp::d2sum (h²·Δ_h; the update coefficients carry 1/h²)
+    return (xp - c2 + xm) + (yp - c2 + ym) + (zp - c2 + zm)
 
 
 def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2: np.ndarray, box, s_ext: np.ndarray,
@@ -42,7 +42,7 @@ def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2:
     x0, x1, y0, y1, z0, z1 = int(box.x0), int(box.x1), int(box.y0), int(box.y1), int(box.z0), int(box.z1)
     sx0, sx1 = sx  # the kernel's default is the rank's compute-box x range
     ax0, ax1 = -xg, int(lay.nx) + xg
-    ihx2, ihy2, ihz2, tau2 = co.ihx2, co.ihy2, co.ihz2, co.tau2
+    ihx2, ihy2, ihz2, tau2 = co.ihx2, co.ihy2, co.ihz2, co.lam  # tau2 here: τ²/h², the coefficient of d2sum
     ct = list(ct) if ct is not None else [0.0] * S
 
     def inside(g):
@@ -109,7 +109,7 @@ def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2:
                     lap = lap7(c, (sxw[xi - 1] * sy) * sz, (sxw[xi + 1] * sy) * sz, (sxc * syw[ya - 1]) * sz,
                                (sxc * syw[ya + 1]) * sz, cy * szw[zb - 1], cy * szw[zb + 1], co.ihx2, co.ihy2, co.ihz2)
                     real = inside(gy0 + y) & inside(gz0 + z) & (1 <= gx0 + x <= N - 1)
-                    return np.where(real, c + co.half_tau2 * lap, 0.0)
+                    return np.where(real, c + co.half_lam * lap, 0.0)
                 if ax0 <= x < ax1 and 1 <= gx0 + x <= N - 1:
                     m = inside(gy0 + y) & inside(gz0 + z)
                     v[m] = src[goff(x, y[m], z[m])]

@@ -18,8 +18,14 @@
 //     is 0 in every buffer on every init path (φ = 0 on it: sin-table boundary zero; the updates never write it), so
 //     no select follows a load and its wait is deferred to the first use; planes beyond the boundary only feed stage
 //     values outside the interior, which are forced to 0 like every stage output there;
-//   * any subset of the S new levels can carry the fused error check (per-stage partials).
-// Formulas and operation order are those of stencil.hpp: one pass is bit-identical to S single steps. The pass
+//   * any subset of the S new levels can carry the fused error check (per-stage partials); the check's s_x·s_y row
+//     factor is tabulated once per plane (row_tables) and each position's s_z factor sits in a register;
+//   * the analytic-start variant (INIT) reads nothing: a φ stage computes u⁰ = φ once per node and plane into an extra
+//     LDS level and u¹ = first_step(φ, d2sum φ) from its neighbours (bit-identical to k_init_first).
+// Formulas and operation order are those of stencil.hpp (d2sum with the folded coefficient λ = τ²/h²): one pass is
+// bit-identical to S single steps. Measured variants that lost (dense 768-thread layouts, 3-deep queues, 5-step
+// passes, deeper prefetch, half tiles, branch-free selects, a conflict-free position order) are documented with their
+// numbers in profiles/r1_tb_queue_experiments.md. The pass
 // semantics (which plane of which level each stage reads) are mirrored by tools/tb_emulate.py (CPU tests).
 #include <hip/hip_runtime.h>
 

@@ -99,3 +99,24 @@ def test_init2_identical(gpu, temporal, N, K, ce):
         assert math.isclose(x, y, rel_tol=1e-12)
     assert torch.equal(a.owned_field(0), b.owned_field(0))
     assert torch.equal(a.owned_field(1), b.owned_field(1))
+
+
+@pytest.mark.parametrize("N,L,tau,K,ce,temporal", [(64, 1.0, 1e-3, 1, 1, 4), (65, 1.0, 1e-3, 7, 3, 4),
+                                                   (100, math.pi, 1e-3, 20, 2, 4), (127, 1.0, 1e-3, 50, 2, 4),
+                                                   (129, 1.0, 1e-3, 33, 5, 2), (300, math.pi, 2e-3, 41, 4, 4)])
+def test_oracle_sweep(gpu, N, L, tau, K, ce, temporal):
+    """Odd/even N, L ∈ {1, π}, K up to 50 (more LDS passes than reduction regions), several check cadences and pass
+    depths: the printed errors match the closed-form oracle and the CPU solver's (tools/oracle_sweep.py
+    runs the full list)."""
+    from mpi_cuda_amd.models.wave3d import oracle_errors
+
+    spec = ProblemSpec(N=N, tau=tau, K=K, L=L, check_every=ce)
+    r = Solver(spec, backend="hip", device=0, temporal=temporal).run()
+    cpu = Solver(spec, backend="cpu").run()
+    ref = oracle_errors(spec)
+    assert r.steps == cpu.steps == [n for n in range(1, K + 1) if (ce and n % ce == 0) or n == K]
+    assert r.max_err == cpu.max_err
+    for n, m, e, ec in zip(r.steps, r.max_err, r.rms_err, cpu.rms_err):
+        om, oe = ref[n]
+        assert abs(m - om) <= 1e-5 * om and abs(e - oe) <= 1e-5 * oe
+        assert math.isclose(e, ec, rel_tol=1e-12)

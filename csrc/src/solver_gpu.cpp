@@ -37,8 +37,14 @@ Comm::Comm(int rank, int world, const std::string& unique_id) : rank_(rank), wor
   // self-test: one all-reduce of 1 per rank must give the world size. A communicator that cannot move data fails here
   // (with RCCL's error or the GPU-wait timeout) instead of inside a captured solve, so callers can fall back early.
   if (world > 1) {
-    const double n = comm_allreduce(*this, 1.0, false);
-    W3D_REQUIRE(n == static_cast<double>(world), "RCCL self-test: all-reduce of 1 per rank gave " + std::to_string(n));
+    try {
+      const double n = comm_allreduce(*this, 1.0, false);
+      W3D_REQUIRE(n == static_cast<double>(world), "RCCL self-test: all-reduce of 1 per rank gave " + std::to_string(n));
+    } catch (...) {
+      ncclCommAbort(c);  // the destructor does not run for a throwing constructor
+      comm_ = nullptr;
+      throw;
+    }
   }
 }
 

@@ -248,19 +248,20 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
 }
 
 GpuSolver::~GpuSolver() {
-  if (graph_exec_) hipGraphExecDestroy(graph_exec_);
+  // a destructor must not throw: release errors are dropped on purpose (the device may already be in an error state)
+  if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
   for (double* p : {u_[0], u_[1], u_[2], u_[3], d_s_, send_buf_, recv_buf_})
-    if (p) hipFree(p);
-  if (partials_) hipFree(partials_);
-  if (tb_partials_) hipFree(tb_partials_);
-  if (errlog_) hipFree(errlog_);
-  if (errall_) hipFree(errall_);
-  for (hipEvent_t e : ev_pool_) hipEventDestroy(e);
-  if (ev_shell_) hipEventDestroy(ev_shell_);
-  if (ev_halo_) hipEventDestroy(ev_halo_);
-  if (ev_packed_) hipEventDestroy(ev_packed_);
-  if (s0_) hipStreamDestroy(s0_);
-  if (s1_) hipStreamDestroy(s1_);
+    if (p) (void)hipFree(p);
+  if (partials_) (void)hipFree(partials_);
+  if (tb_partials_) (void)hipFree(tb_partials_);
+  if (errlog_) (void)hipFree(errlog_);
+  if (errall_) (void)hipFree(errall_);
+  for (hipEvent_t e : ev_pool_) (void)hipEventDestroy(e);
+  if (ev_shell_) (void)hipEventDestroy(ev_shell_);
+  if (ev_halo_) (void)hipEventDestroy(ev_halo_);
+  if (ev_packed_) (void)hipEventDestroy(ev_packed_);
+  if (s0_) (void)hipStreamDestroy(s0_);
+  if (s1_) (void)hipStreamDestroy(s1_);
 }
 
 size_t GpuSolver::device_bytes() const {
@@ -800,7 +801,7 @@ RunResult GpuSolver::run() {
       ok = ok && e == hipSuccess && g != nullptr;
     }
     if (ok) ok = hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0) == hipSuccess;
-    if (g) hipGraphDestroy(g);
+    if (g) (void)hipGraphDestroy(g);
     (void)hipGetLastError();
     if (!ok) {
       graph_exec_ = nullptr;

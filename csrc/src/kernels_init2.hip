@@ -235,7 +235,7 @@ Init2Params make_params(const Layout& l, const Coeffs& c) {
 }  // namespace
 
 int init_two_partials(const Layout& l) {
-  const Init2Params p = make_params(l, Coeffs{1, 1, 1, 1, 0.5});
+  const Init2Params p = make_params(l, Coeffs{1, 1, 1, 1, 0.5, 1, 0.5});  // only the geometry matters here
   return p.nblocks * kWaves;
 }
 

@@ -735,7 +735,7 @@ void launch_leapfrog(const Layout& l, const Coeffs& c, const double* cur, double
   W3D_HIP_CHECK(hipGetLastError());
 }
 
-int error_blocks(const Layout& l, const LBox& b) {
+int error_blocks(const Layout& /*l*/, const LBox& b) {
   if (b.empty()) return 0;
   return static_cast<int>(ceil_div((b.y1 - b.y0) * (b.z1 - b.z0), 256) * (b.x1 - b.x0));
 }

@@ -1,6 +1,5 @@
 """Decomposition / layout / halo-plan invariants (SURVEY.md §4.2 unit row): every node owned exactly once for many P,
 uneven splits, balanced interior work, aligned pairs, symmetric neighbour and face plans, 64-bit sizes."""
-import itertools
 
 import numpy as np
 import pytest

@@ -71,6 +71,8 @@ def main() -> int:
     from mpi_cuda_amd.solver import Solver
 
     rank, world, local = init_process_group("gloo")
+    if not a.cpu:  # one rank per GPU on a node; more ranks than GPUs (a one-GPU rehearsal) share them round-robin
+        local %= max(1, torch.cuda.device_count())
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit("bench.py --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
@@ -132,9 +134,15 @@ def main() -> int:
                 ok, err = 0, f"{type(e).__name__}: {e}"
         if agree(ok):
             for name, dec, temp, ovl in cands:
-                s, t = None, float("inf")
+                s, t, ok = None, float("inf"), 1
                 try:
                     s = make(transport, comm=comm, decomp=dec, temporal=temp, overlap=ovl)
+                except Exception as e:  # noqa: BLE001  (a schedule this decomposition cannot run: skip it everywhere)
+                    ok, err = 0, f"{type(e).__name__}: {e}"
+                    print(f"[bench rank {rank}] autotune candidate {name} rejected: {err}", file=sys.stderr, flush=True)
+                if not agree(ok):
+                    continue  # nothing was exchanged yet: the communicator is intact
+                try:
                     s.run()  # eager: RCCL peer connections
                     s.run()  # graph capture
                     t, ok = timed_solve_max(s, 3), 1
@@ -159,13 +167,20 @@ def main() -> int:
     # every rank switches together to the torch.distributed transport (RCCL through ProcessGroupNCCL) so the scaling
     # run still measures the same kernels; the JSON line says which transport ran.
     if solver is None:
+        # construction and the first solve are agreed on separately: a rank whose constructor failed must not leave
+        # the others blocked in the first solve's halo exchange
+        ok = 1
         try:
             solver = make(transport)
-            r = solver.run()  # first warmup: graph capture (one rank) or RCCL connection setup (several)
-            ok = 1
         except Exception as e:  # noqa: BLE001
             ok, err = 0, f"{type(e).__name__}: {e}"
-            print(f"[bench rank {rank}] {transport} path failed: {err}", file=sys.stderr, flush=True)
+            print(f"[bench rank {rank}] {transport} solver setup failed: {err}", file=sys.stderr, flush=True)
+        if agree(ok):
+            try:
+                r = solver.run()  # first warmup: graph capture (one rank) or RCCL connection setup (several)
+            except Exception as e:  # noqa: BLE001
+                ok, err = 0, f"{type(e).__name__}: {e}"
+                print(f"[bench rank {rank}] {transport} path failed: {err}", file=sys.stderr, flush=True)
         if not agree(ok):
             if a.cpu or transport != "rccl":
                 raise SystemExit(f"bench: {transport} transport failed: {err}")

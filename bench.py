@@ -223,6 +223,7 @@ def main() -> int:
     if rank == 0:
         par = f"{sched.split('-')[0]}{world}" if world > 1 else "single"
         dims = "x".join(str(d) for d in solver.dims)
+        py_loop = transport == "torch" and not a.cpu  # GPU fallback path (CPU runs keep the candidate names)
         line = {
             "metric": f"gcell_updates_per_s_{a.N}cube_K{a.K}",
             "value": round(value, 3),
@@ -236,16 +237,18 @@ def main() -> int:
             "vs_baseline": round(value / base, 3),
             "dtype": "fp64",
             "data": "analytic initial condition sin(pi x)sin(pi y)sin(pi z) (synthetic, as the reference)",
-            "config": {
+            "config": {  # the torch transport is the Python single-step loop (parallel/dist_solver.py)
                 "model": "wave3d leapfrog 7-point fp64 (AICCer1/MPI-CUDA mpigpu-1 config)",
                 "global_batch": 1,
                 "seq_len": a.N + 1,
                 "parallelism": par,
                 "grid": f"{a.N}^3", "N": a.N, "tau": a.tau, "K": a.K, "L": a.L,
-                "decomp": dims, "transport": transport, "graph": bool(not a.no_graph),
-                "overlap": bool(not a.no_overlap) and not sched.endswith("-seq"),
-                "temporal_blocking": bool(not a.no_temporal and (world == 1 or not sched.endswith("S1"))),
-                "schedule": sched if (world > 1 or tuned) else f"fused-single-S{1 if a.no_temporal else a.temporal}",
+                "decomp": dims, "transport": transport, "graph": bool(not a.no_graph) and not py_loop,
+                "overlap": bool(not a.no_overlap) and not sched.endswith("-seq") and not py_loop,
+                "temporal_blocking": bool(not a.no_temporal and (world == 1 or not sched.endswith("S1")))
+                and not py_loop,
+                "schedule": ("python-step-loop-S1" if py_loop else sched if (world > 1 or tuned)
+                             else f"fused-single-S{1 if a.no_temporal else a.temporal}"),
                 "autotune_ms": tuned or None,
             },
             "wall_clock_s": round(ms / 1e3, 6),

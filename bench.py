@@ -82,7 +82,11 @@ def main() -> int:
     transport = ("torch" if world > 1 else "native") if a.cpu else a.transport
     os.environ.setdefault("W3D_TIMEOUT_S", "180")
 
+    fail_rank = os.environ.get("W3D_BENCH_FAIL_SETUP_RANK")  # fault injection (tests): this rank cannot build solvers
+
     def make(transport, group=None, comm=None, decomp=None, temporal=None, overlap=None):
+        if fail_rank is not None and int(fail_rank) == rank:
+            raise RuntimeError(f"injected solver setup failure on rank {rank}")
         return Solver(spec, backend=backend, transport=transport, decomp=decomp or a.decomp, rank=rank, world=world,
                       device=None if a.cpu else local, overlap=(not a.no_overlap) if overlap is None else overlap,
                       graph=not a.no_graph,

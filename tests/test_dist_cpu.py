@@ -77,3 +77,15 @@ def test_bench_contract_cpu_two_ranks(tmp_path):
     assert set(d["config"]["autotune_ms"]) == {"slab-S4", "slab-S4-seq", "slab-S3", "slab-S2", "slab-S1"}
     assert d["config"]["schedule"] in d["config"]["autotune_ms"]
     assert d["config"]["schedule"] == min(d["config"]["autotune_ms"], key=d["config"]["autotune_ms"].get)
+
+
+def test_bench_setup_failure_on_one_rank_exits_instead_of_hanging(tmp_path):
+    """A rank whose solver cannot be built makes every rank stop (before any halo exchange), not wait forever."""
+    env = dict(os.environ, W3D_BENCH_FAIL_SETUP_RANK="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(29330 + os.getpid() % 50), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--cpu",
+           "--N", "24", "--steps", "2", "--warmup", "1"]
+    p = subprocess.run(cmd, env=env, timeout=120, capture_output=True, text=True)
+    assert p.returncode != 0
+    assert "injected solver setup failure" in p.stderr
+    assert not [l for l in p.stdout.splitlines() if l.startswith("{")]

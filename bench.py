@@ -4,194 +4,313 @@ readme.md:99-100, report.pdf p.16 §4.4).
 
 One bench "step" = one COMPLETE solve exactly as the reference times it: field init (u⁰, u¹) → 19 leapfrog steps →
 error check vs the analytic solution every 2nd step → global error log on the host. Nothing is cached between solves:
-every solve re-initialises the fields and recomputes all K steps. Warmup solves are untimed (the first one captures
-the hipGraph and sets up the RCCL peer connections).
+every solve re-initialises the fields and recomputes all K steps.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
-Rank 0 prints ONE JSON line. ``value`` = whole-job GCell-updates/s = N³·K / t_solve (reference convention), with
-t_solve the max over ranks of the per-solve wall-clock; ``ms_per_step`` = t_solve in ms; ``vs_baseline`` = value ÷ the
-reference's published total-time GCell/s at the same GPU count (1 GPU: 3.570 = 512³·20/0.752 s; 2 GPUs: 5.316 =
-512³·20/0.505 s; for 4 and 8 GPUs, where the reference publishes nothing, its best number, the 2-GPU 5.316).
-The problem size is fixed as GPUs are added: ``scaling`` is "strong".
+What runs: every rank starts the native runtime (``bin/wave3d``, C++ + HIP kernels + RCCL, built in-tree) as a child
+process on its GPU and hands it the launch (RANK / LOCAL_RANK / WORLD_SIZE from torchrun, a per-launch rendezvous
+nonce for the RCCL unique id). The child runs W untimed solves (plus, on several ranks, the schedule autotune, whose
+candidate solves are untimed too), then EXACTLY K solves between a device sync + RCCL barrier on both sides, and reports
+the interval as the max over ranks. This process only orchestrates (torch.distributed over gloo: nonce broadcast and
+the agreement on success); it never touches the GPU. The child runs on the system ROCm (HIP 7.2 + RCCL 2.27), whose
+stream capture of the multi-rank schedules is verified; the HIP 7.0 runtime bundled with PyTorch crashes in
+hipStreamEndCapture on those graphs (tools/capture_probe*.hip, csrc/src/solver_gpu.cpp multistream_capture_safe).
+
+Rank 0 prints ONE JSON line. ``value`` = whole-job GCell-updates/s = N³·K / t_solve (reference convention) with
+t_solve = (max over ranks of the K-solve interval) / K; ``ms_per_step`` = ``ms_per_solve`` = t_solve in ms (one bench
+step is one solve); ``vs_baseline`` = value ÷ the reference's published total-time GCell/s at the same GPU count (1 GPU:
+3.570 = 512³·20/0.752 s; 2 GPUs: 5.316 = 512³·20/0.505 s; for 4 and 8 GPUs, where the reference publishes nothing, its
+best number, the 2-GPU 5.316 — ``vs_baseline_basis`` says which). The problem size is fixed as GPUs are added:
+``scaling`` is "strong". ``rccl_nranks`` is the communicator size RCCL itself reports (ncclCommCount).
+
+If the native runtime fails on any rank, every rank stops with a non-zero exit and no JSON line. ``--allow-fallback``
+instead re-runs the solve in-process over the torch.distributed transport (the Python single-step loop) and marks the
+line ``"degraded": true`` with the error text. ``--python`` runs the in-process Python ``Solver`` path directly.
+``--cpu`` drives the same orchestration with the native CPU ranks (the contract test without a GPU).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
+import uuid
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 REF_GCELL = {1: 512**3 * 20 / 0.752 / 1e9, 2: 512**3 * 20 / 0.505 / 1e9}
 REF_FINAL_LINF = 3.960129e-09  # report.pdf p.16 §4.3.1, step 20
+CLI = os.path.join(ROOT, "bin", "wave3d")
 
 
-def _tiling(a) -> dict:
-    t = {"variant": a.variant}
-    if a.tile_rows:
-        t["rows" if a.variant == 1 else "ty"] = a.tile_rows
-    return t
-
-
-def main() -> int:
+def _args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20, help="timed full solves")
-    ap.add_argument("--warmup", type=int, default=3, help="untimed full solves (at least 1 is always run)")
+    ap.add_argument("--warmup", type=int, default=3, help="untimed full solves (at least 1; 2 on several ranks)")
     ap.add_argument("--N", type=int, default=512)
     ap.add_argument("--tau", type=float, default=1e-3)
     ap.add_argument("--K", type=int, default=20)
     ap.add_argument("--L", type=float, default=1.0)
-    ap.add_argument("--decomp", default="slab", help="slab | block | PxQxR")
-    ap.add_argument("--transport", default="rccl", choices=["rccl", "torch"])
+    ap.add_argument("--decomp", default="slab", help="slab | block | PxQxR (with --no-autotune)")
+    ap.add_argument("--temporal", type=int, default=4, help="at most this many leapfrog steps per HBM pass (1..4)")
+    ap.add_argument("--no-temporal", action="store_true", help="one leapfrog step per HBM pass")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--no-temporal", action="store_true", help="one leapfrog step per HBM pass (no temporal blocking)")
-    ap.add_argument("--temporal", type=int, default=4, help="at most this many leapfrog steps per HBM pass (2..4)")
-    ap.add_argument("--no-tb", action="store_true", help="one rank: two-step register-queue passes, not the LDS kernel")
-    ap.add_argument("--variant", type=int, default=1, help="leapfrog kernel (1 = register-queue, 0 = LDS tile)")
-    ap.add_argument("--tile-rows", type=int, default=0, help="rows per wave (v1) / per workgroup (v0); 0 = default")
-    ap.add_argument("--cpu", action="store_true", help="CPU backend (contract test without a GPU)")
-    ap.add_argument("--autotune", action="store_true", help="time the candidate schedules even on one rank")
     ap.add_argument("--no-autotune", action="store_true",
-                    help="multi-rank: use --decomp/--temporal as given instead of timing the candidate schedules")
+                    help="several ranks: use --decomp/--temporal as given instead of timing the candidate schedules")
+    ap.add_argument("--autotune", action="store_true", help="time the candidate schedules even on one rank")
+    ap.add_argument("--no-phases", action="store_true", help="skip the traced per-phase breakdown solve")
+    ap.add_argument("--cpu", action="store_true", help="native CPU ranks (contract test without a GPU)")
+    ap.add_argument("--python", action="store_true", help="in-process Python Solver instead of the native runtime")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "torch"], help="--python: halo transport")
+    ap.add_argument("--allow-fallback", action="store_true",
+                    help="if the native runtime fails, re-run over the torch transport (marked degraded)")
+    ap.add_argument("--share-gpus", action="store_true",
+                    help="rehearsal: allow more ranks than visible GPUs (ranks share GPUs; RCCL refuses this)")
+    ap.add_argument("--timeout", type=float, default=900.0, help="seconds before a native rank is killed")
     ap.add_argument("--out", default="", help="also append the JSON line to this file")
-    a = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+def _line(a, world, value, ms, cfg, extra) -> dict:
+    base = REF_GCELL.get(world, REF_GCELL[2])
+    line = {
+        "metric": f"gcell_updates_per_s_{a.N}cube_K{a.K}",
+        "value": round(value, 3),
+        "unit": "GCell-updates/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms, 4),
+        "ms_per_solve": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": round(value / base, 3),
+        "vs_baseline_basis": {1: "1x P100, 0.752 s", 2: "2x P100, 0.505 s"}.get(
+            world, "2x P100, 0.505 s (the reference publishes no 4/8-GPU number; its best)"),
+        "dtype": "fp64",
+        "data": "analytic initial condition sin(pi x)sin(pi y)sin(pi z) (synthetic, as the reference)",
+        "config": {"model": "wave3d leapfrog 7-point fp64 (AICCer1/MPI-CUDA mpigpu-1 config)", "global_batch": 1,
+                   "seq_len": a.N + 1, "grid": f"{a.N}^3", "N": a.N, "tau": a.tau, "K": a.K, "L": a.L, **cfg},
+    }
+    line.update(extra)
+    return line
+
+
+def _emit(a, line) -> None:
+    s = json.dumps(line)
+    print(s, flush=True)
+    if a.out:
+        with open(a.out, "a") as f:
+            f.write(s + "\n")
+
+
+def _correct(a, finite, final_linf) -> bool:
+    ref_cfg = a.N == 512 and a.K == 20 and a.tau == 1e-3 and a.L == 1.0
+    return bool(finite and (not ref_cfg or abs(final_linf / REF_FINAL_LINF - 1) < 1e-5))
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# native runtime (default)
+# ------------------------------------------------------------------------------------------------------------------
+def run_native(a, rank: int, world: int, local: int) -> int:
+    import torch.distributed as dist
+
+    from mpi_cuda_amd.parallel.rccl import broadcast_bytes
+
+    if not os.path.exists(CLI):
+        raise SystemExit(f"bench: native runtime {CLI} is missing (python tools/build.py)")
+    nonce = uuid.uuid4().hex.encode() if rank == 0 else None
+    if world > 1:
+        nonce = broadcast_bytes(nonce, 0)
+    nonce = nonce.decode()
+    tmp = tempfile.gettempdir()
+    rdzv = os.path.join(tmp, f"wave3d-bench-{nonce}.uid")
+    abort_flag = os.path.join(tmp, f"wave3d-bench-{nonce}.abort")
+    out_json = os.path.join(tmp, f"wave3d-bench-{nonce}.rank{rank}.json")
+    log_path = os.path.join(tmp, f"wave3d-bench-{nonce}.rank{rank}.log")
+    multi = world > 1
+    warm = max(a.warmup, 2 if multi else 1)
+    temporal = 1 if a.no_temporal else a.temporal
+    cmd = [CLI, str(a.N), repr(a.tau), str(a.K), repr(a.L), "--quiet", "--json", out_json,
+           "--warmup", str(warm - 1), "--repeat", "1", "--bench-steps", str(a.steps),
+           "--decomp", a.decomp, "--temporal", str(temporal)]
+    if a.cpu:
+        cmd.append("--cpu")
+    else:
+        if (multi or a.autotune) and not a.no_autotune:
+            cmd.append("--autotune")
+        if not a.no_phases:
+            cmd.append("--phases")
+        if a.no_overlap:
+            cmd.append("--no-overlap")
+        if a.no_graph:
+            cmd.append("--no-graph")
+    env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(local), W3D_RDZV_FILE=rdzv,
+               W3D_JOB_ID=f"bench{nonce}", W3D_TIMEOUT_S=os.environ.get("W3D_TIMEOUT_S", "180"))
+    if a.share_gpus:
+        env["W3D_SHARE_GPUS"] = "1"
+    fail_rank = os.environ.get("W3D_BENCH_FAIL_SETUP_RANK")  # fault injection (tests)
+    if fail_rank is not None:
+        env["W3D_FAULT_RANK"] = fail_rank
+    t0 = time.perf_counter()
+    with open(log_path, "w") as log:
+        p = subprocess.Popen(cmd, env=env, stdout=log, stderr=subprocess.STDOUT)
+        rc, why = None, ""
+        while rc is None:
+            try:
+                rc = p.wait(timeout=0.2)
+            except subprocess.TimeoutExpired:
+                if os.path.exists(abort_flag):
+                    why = "a peer rank failed"
+                elif time.perf_counter() - t0 > a.timeout:
+                    why = f"timed out after {a.timeout:.0f} s"
+                else:
+                    continue
+                p.kill()
+                rc = p.wait()
+    wall = time.perf_counter() - t0
+    if rc != 0:
+        open(abort_flag, "w").close()  # peers stop their children instead of waiting in a collective
+    with open(log_path) as f:
+        tail = f.read()[-2000:]
+    ok = 1 if rc == 0 else 0
+    if multi:
+        import torch
+
+        t = torch.tensor([ok], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        ok = int(t.item())
+    res = None
+    if ok and rank == 0:
+        with open(out_json) as f:
+            res = json.load(f)
+    for path in (out_json, log_path):
+        if os.path.exists(path):
+            os.remove(path)
+    if not ok:
+        err = tail.strip().splitlines()[-1] if tail.strip() else f"exit {rc}"
+        if rc != 0:
+            print(f"[bench rank {rank}] native runtime failed (rc={rc}{', ' + why if why else ''}): {err}\n{tail}",
+                  file=sys.stderr, flush=True)
+        if multi:
+            dist.barrier()
+            if rank == 0 and os.path.exists(abort_flag):
+                os.remove(abort_flag)
+        if a.allow_fallback and not a.cpu:
+            return run_python(a, rank, world, local, degraded=f"native runtime failed: {err}")
+        return 1
+    if rank == 0:
+        bench_s = float(res["bench_s"])
+        ms = bench_s / a.steps * 1e3
+        value = (a.N ** 3 * a.K) / (ms / 1e3) / 1e9
+        steps = res.get("steps") or []
+        final_linf = steps[-1][1] if steps else float("nan")
+        final_rms = steps[-1][2] if steps else None
+        correct = _correct(a, res.get("finite", False), final_linf)
+        dims = res.get("dims", [1, 1, 1])
+        sched = res.get("schedule", "")
+        par = (f"{sched.split('-')[0]}{world}" if multi else "single") if not a.cpu else f"cpu-ranks{world}"
+        cfg = {
+            "parallelism": par, "decomp": "x".join(map(str, dims)),
+            "transport": ("shm" if multi else "none") if a.cpu else ("rccl" if multi else "none"),
+            "runtime": "native bin/wave3d (C++/HIP/RCCL)" if not a.cpu else "native bin/wave3d --cpu (OpenMP ranks)",
+            "graph": bool(res.get("graph", False)), "overlap": bool(res.get("overlap", False)) and multi,
+            "temporal_blocking": int(res.get("temporal", 1)) > 1 and not a.cpu,
+            "schedule": sched if multi or a.cpu else f"fused-single-S{res.get('temporal', temporal)}",
+            "mode": res.get("mode", ""),
+            "autotune_ms": {k: round(v * 1e3, 4) for k, v in res.get("autotune_s", {}).items()} or None,
+        }
+        extra = {
+            "wall_clock_s": round(ms / 1e3, 6),
+            "best_solve_s": round(float(res.get("solve_s", 0.0)), 6),
+            "baseline_wall_clock_s": {1: 0.752, 2: 0.505}.get(world),
+            "final_max_err": final_linf,
+            "final_rms_err": final_rms,
+            "correct": correct,
+            "degraded": False,
+            "rccl_nranks": res.get("rccl_nranks") if not a.cpu else None,
+            "rccl_version": res.get("rccl_version"),
+            "hip_runtime": res.get("hip_runtime"),
+            "process_wall_s": round(wall, 3),
+            "rccl_init_s": res.get("rccl_init_s"),
+            "phases_ms": res.get("phases_ms"),
+            "distinct_gpus": None if a.cpu else _distinct_gpus(world),
+        }
+        _emit(a, _line(a, world, value, ms, cfg, extra))
+        return 0 if correct else 1
+    return 0
+
+
+def _distinct_gpus(world: int) -> int:
+    try:
+        import torch
+
+        return min(world, max(1, torch.cuda.device_count()))  # device_count does not initialise the GPU here
+    except Exception:  # noqa: BLE001
+        return world
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# in-process Python Solver (--python, or the --allow-fallback path)
+# ------------------------------------------------------------------------------------------------------------------
+def run_python(a, rank: int, world: int, local: int, degraded: str = "") -> int:
     import torch
     import torch.distributed as dist
 
     from mpi_cuda_amd import ProblemSpec
-    from mpi_cuda_amd.parallel.rccl import init_process_group
     from mpi_cuda_amd.solver import Solver
 
-    rank, world, local = init_process_group("gloo")
-    if not a.cpu:  # one rank per GPU on a node; more ranks than GPUs (a one-GPU rehearsal) share them round-robin
-        local %= max(1, torch.cuda.device_count())
-    if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit("bench.py --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     spec = ProblemSpec(N=a.N, tau=a.tau, K=a.K, L=a.L, check_every=2)
-    backend = "cpu" if a.cpu else "hip"
-    transport = ("torch" if world > 1 else "native") if a.cpu else a.transport
-    os.environ.setdefault("W3D_TIMEOUT_S", "180")
+    transport = "torch" if (degraded or a.cpu) and world > 1 else a.transport
+    if a.cpu:
+        transport = "torch" if world > 1 else "native"
+    group = None
+    if transport == "torch" and world > 1 and not a.cpu:
+        group = dist.new_group(backend="nccl")
 
-    fail_rank = os.environ.get("W3D_BENCH_FAIL_SETUP_RANK")  # fault injection (tests): this rank cannot build solvers
-
-    def make(transport, group=None, comm=None, decomp=None, temporal=None, overlap=None):
-        if fail_rank is not None and int(fail_rank) == rank:
-            raise RuntimeError(f"injected solver setup failure on rank {rank}")
-        return Solver(spec, backend=backend, transport=transport, decomp=decomp or a.decomp, rank=rank, world=world,
-                      device=None if a.cpu else local, overlap=(not a.no_overlap) if overlap is None else overlap,
-                      graph=not a.no_graph,
-                      tiling=_tiling(a), group=group, comm=comm,
-                      temporal=temporal or (1 if a.no_temporal else a.temporal), tb=not a.no_tb)
-
-    def agree(ok: int) -> int:  # every rank takes the same branch
+    def agree(ok: int) -> int:
         if world > 1:
             f = torch.tensor([ok], dtype=torch.int64)
             dist.all_reduce(f, op=dist.ReduceOp.MIN)
             ok = int(f.item())
         return ok
 
-    def timed_solve_max(s, n: int) -> float:  # best of n solves, max over ranks (seconds)
-        best = float("inf")
-        for _ in range(n):
-            t0 = time.perf_counter()
-            s.run()
-            best = min(best, time.perf_counter() - t0)
-        t = torch.tensor([best], dtype=torch.float64)
-        if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+    solver, r, err, ok = None, None, "", 1
+    comm = None
+    try:
+        if transport == "rccl" and world > 1:
+            from mpi_cuda_amd.parallel.rccl import make_comm
 
-    # Multi-rank schedule autotune (part of the warmup, untimed): the halo volume of the deep-halo passes (S + S−1
-    # planes per face per S steps) against the per-step exchanges of the single-step schedule is a trade of xGMI
-    # bandwidth against HBM traffic that depends on the node, so each candidate runs a few solves on the real
-    # interconnect and every rank adopts the one whose slowest rank was fastest. One RCCL communicator serves all.
-    # (CPU multi-process runs take the same path over the torch.distributed transport: contract tests of this logic)
-    # (--autotune forces it on one rank too: a GPU-box rehearsal of this path)
-    autotune = (world > 1 or a.autotune) and not a.no_autotune and (
-        transport == "rccl" or (a.cpu and transport in ("torch", "native")))
-    # "-seq": no overlap — each pass runs whole and its faces go out after it (no shell launches: cheaper compute,
-    # exposed exchange; wins when the links are fast against the ≈ 0.1 ms of shell passes per solve at 8 ranks)
-    cands = [("slab-S4", "slab", 4, True), ("slab-S4-seq", "slab", 4, False), ("slab-S3", "slab", 3, True),
-             ("slab-S2", "slab", 2, True), ("slab-S1", "slab", 1, True)]
-    if world >= 4:  # 2x2x1 / 2x2x2 blocks: smaller faces on more links (at 2 ranks "block" is the slab)
-        cands.append(("block-S1", "block", 1, True))
-    tuned = {}
-    solver, r, err, sched = None, None, "", f"{a.decomp}-S{1 if a.no_temporal else a.temporal}"
-    if autotune:
-        from mpi_cuda_amd.parallel.rccl import make_comm
-
-        comm, best_t, ok = None, float("inf"), 1
-        if transport == "rccl":
-            try:
-                comm = make_comm(rank, world)
-            except Exception as e:  # noqa: BLE001
-                ok, err = 0, f"{type(e).__name__}: {e}"
-        if agree(ok):
-            for name, dec, temp, ovl in cands:
-                s, t, ok = None, float("inf"), 1
-                try:
-                    s = make(transport, comm=comm, decomp=dec, temporal=temp, overlap=ovl)
-                except Exception as e:  # noqa: BLE001  (a schedule this decomposition cannot run: skip it everywhere)
-                    ok, err = 0, f"{type(e).__name__}: {e}"
-                    print(f"[bench rank {rank}] autotune candidate {name} rejected: {err}", file=sys.stderr, flush=True)
-                if not agree(ok):
-                    continue  # nothing was exchanged yet: the communicator is intact
-                try:
-                    s.run()  # eager: RCCL peer connections
-                    s.run()  # graph capture
-                    t, ok = timed_solve_max(s, 3), 1
-                except Exception as e:  # noqa: BLE001
-                    ok, err = 0, f"{type(e).__name__}: {e}"
-                    print(f"[bench rank {rank}] autotune candidate {name} failed: {err}", file=sys.stderr, flush=True)
-                if not agree(ok):
-                    break  # a failed RCCL exchange may leave the communicator unusable: stop here
-                tuned[name] = round(t * 1e3, 4)
-                if t < best_t:
-                    solver, best_t, sched = s, t, name
-                else:
-                    del s
-        if solver is not None:  # the winner must still work (a failed candidate may have hurt the communicator)
-            try:
-                r, ok = solver.run(), 1
-            except Exception as e:  # noqa: BLE001
-                ok, err = 0, f"{type(e).__name__}: {e}"
-            if not agree(ok):
-                solver, sched, tuned = None, f"{a.decomp}-S{1 if a.no_temporal else a.temporal}", {}
-    # The native RCCL runtime is the production path. If it fails on some rank (it throws; stuck exchanges time out),
-    # every rank switches together to the torch.distributed transport (RCCL through ProcessGroupNCCL) so the scaling
-    # run still measures the same kernels; the JSON line says which transport ran.
-    if solver is None:
-        # construction and the first solve are agreed on separately: a rank whose constructor failed must not leave
-        # the others blocked in the first solve's halo exchange
-        ok = 1
+            comm = make_comm(rank, world)
+    except Exception as e:  # noqa: BLE001
+        ok, err = 0, f"{type(e).__name__}: {e}"
+    if agree(ok):
         try:
-            solver = make(transport)
+            solver = Solver(spec, backend="cpu" if a.cpu else "hip", transport=transport, decomp=a.decomp, rank=rank,
+                            world=world, device=None if a.cpu else local, overlap=not a.no_overlap,
+                            graph=not a.no_graph, group=group, comm=comm,
+                            temporal=1 if a.no_temporal else a.temporal)
         except Exception as e:  # noqa: BLE001
             ok, err = 0, f"{type(e).__name__}: {e}"
-            print(f"[bench rank {rank}] {transport} solver setup failed: {err}", file=sys.stderr, flush=True)
-        if agree(ok):
-            try:
-                r = solver.run()  # first warmup: graph capture (one rank) or RCCL connection setup (several)
-            except Exception as e:  # noqa: BLE001
-                ok, err = 0, f"{type(e).__name__}: {e}"
-                print(f"[bench rank {rank}] {transport} path failed: {err}", file=sys.stderr, flush=True)
-        if not agree(ok):
-            if a.cpu or transport != "rccl":
-                raise SystemExit(f"bench: {transport} transport failed: {err}")
-            group = dist.new_group(backend="nccl") if world > 1 else None
-            transport = "torch"
-            solver = make(transport, group)
+    if not agree(ok):
+        print(f"[bench rank {rank}] python solver setup failed: {err}", file=sys.stderr, flush=True)
+        return 1
+    try:
+        for _ in range(max(a.warmup, 2 if world > 1 else 1)):
             r = solver.run()
+    except Exception as e:  # noqa: BLE001
+        ok, err = 0, f"{type(e).__name__}: {e}"
+    if not agree(ok):
+        print(f"[bench rank {rank}] python solve failed: {err}", file=sys.stderr, flush=True)
+        return 1
 
     def barrier_sync():
         if not a.cpu:
@@ -201,76 +320,63 @@ def main() -> int:
         if not a.cpu:
             torch.cuda.synchronize()
 
-    # RCCL ranks capture their hipGraph on the second solve (the first sets up the peer connections eagerly), so a
-    # multi-rank job always runs at least two untimed solves
-    for _ in range(max(0, a.warmup - 1, 1 if world > 1 else 0)):
-        r = solver.run()
     barrier_sync()
     t0 = time.perf_counter()
-    per = []
     for _ in range(a.steps):
-        ts = time.perf_counter()
         r = solver.run()
-        per.append(time.perf_counter() - ts)
     barrier_sync()
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed, min(per)], dtype=torch.float64)
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, best = float(t[0]), float(t[1])
-    ms = elapsed / a.steps * 1e3
+    ms = float(t[0]) / a.steps * 1e3
     value = spec.cell_updates / (ms / 1e3) / 1e9
-    base = REF_GCELL.get(world, REF_GCELL[2])
-    final_linf = r.max_err[-1] if r is not None and r.max_err else float("nan")
-    correct = bool(r is not None and r.finite and (a.N != 512 or a.K != 20 or a.tau != 1e-3 or a.L != 1.0
-                                                   or abs(final_linf / REF_FINAL_LINF - 1) < 1e-5))
+    final_linf = r.max_err[-1] if r.max_err else float("nan")
+    correct = _correct(a, r.finite, final_linf)
     if rank == 0:
-        par = f"{sched.split('-')[0]}{world}" if world > 1 else "single"
+        py_loop = transport == "torch"
         dims = "x".join(str(d) for d in solver.dims)
-        py_loop = transport == "torch" and not a.cpu  # GPU fallback path (CPU runs keep the candidate names)
-        line = {
-            "metric": f"gcell_updates_per_s_{a.N}cube_K{a.K}",
-            "value": round(value, 3),
-            "unit": "GCell-updates/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(ms, 4),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": round(value / base, 3),
-            "dtype": "fp64",
-            "data": "analytic initial condition sin(pi x)sin(pi y)sin(pi z) (synthetic, as the reference)",
-            "config": {  # the torch transport is the Python single-step loop (parallel/dist_solver.py)
-                "model": "wave3d leapfrog 7-point fp64 (AICCer1/MPI-CUDA mpigpu-1 config)",
-                "global_batch": 1,
-                "seq_len": a.N + 1,
-                "parallelism": par,
-                "grid": f"{a.N}^3", "N": a.N, "tau": a.tau, "K": a.K, "L": a.L,
-                "decomp": dims, "transport": transport, "graph": bool(not a.no_graph) and not py_loop,
-                "overlap": bool(not a.no_overlap) and not sched.endswith("-seq") and not py_loop,
-                "temporal_blocking": bool(not a.no_temporal and (world == 1 or not sched.endswith("S1")))
-                and not py_loop,
-                "schedule": ("python-step-loop-S1" if py_loop else sched if (world > 1 or tuned)
-                             else f"fused-single-S{1 if a.no_temporal else a.temporal}"),
-                "autotune_ms": tuned or None,
-            },
-            "wall_clock_s": round(ms / 1e3, 6),
-            "best_solve_s": round(best, 6),
-            "baseline_wall_clock_s": {1: 0.752, 2: 0.505}.get(world),
-            "final_max_err": final_linf,
-            "final_rms_err": r.rms_err[-1] if r is not None and r.rms_err else None,
-            "correct": correct,
-        }
-        s = json.dumps(line)
-        print(s, flush=True)
-        if a.out:
-            with open(a.out, "a") as f:
-                f.write(s + "\n")
+        cfg = {"parallelism": f"python{world}" if world > 1 else "single", "decomp": dims, "transport": transport,
+               "runtime": "in-process python Solver",
+               "graph": bool(not a.no_graph) and not py_loop and not a.cpu,
+               "overlap": bool(not a.no_overlap) and not py_loop and world > 1,
+               "temporal_blocking": not py_loop and not a.no_temporal and not a.cpu,
+               "schedule": "python-step-loop-S1" if py_loop else getattr(solver.native, "mode", "") or "",
+               "autotune_ms": None}
+        extra = {"wall_clock_s": round(ms / 1e3, 6), "baseline_wall_clock_s": {1: 0.752, 2: 0.505}.get(world),
+                 "final_max_err": final_linf, "final_rms_err": r.rms_err[-1] if r.rms_err else None,
+                 "correct": correct, "degraded": bool(degraded)}
+        if degraded:
+            extra["degraded_reason"] = degraded
+        _emit(a, _line(a, world, value, ms, cfg, extra))
     if world > 1:
         dist.barrier()
-        dist.destroy_process_group()
-    return 0 if correct else 1
+    return (0 if correct else 1) if not degraded else (0 if correct else 1)
+
+
+def main(argv=None) -> int:
+    a = _args(argv)
+    from mpi_cuda_amd.parallel.rccl import env_rank_world, init_process_group
+
+    rank, world, local = env_rank_world()
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("bench.py --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if not a.cpu and not a.share_gpus and world > 1:
+        n = _distinct_gpus(world)
+        if n < world:
+            raise SystemExit(f"bench: {world} ranks but {n} visible GPU(s); RCCL needs one GPU per rank "
+                             "(--share-gpus for a rehearsal)")
+    if world > 1:
+        init_process_group("gloo")
+    try:
+        rc = run_python(a, rank, world, local) if a.python else run_native(a, rank, world, local)
+    finally:
+        import torch.distributed as dist
+
+        if world > 1 and dist.is_initialized():
+            dist.destroy_process_group()
+    return rc
 
 
 if __name__ == "__main__":

@@ -17,6 +17,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <ctime>
 #include <fstream>
 #include <iostream>
 #include <memory>
@@ -50,6 +51,11 @@ struct Args {
   int tb_threads = 0;
   bool init2 = true;
   int fake_rank = -1, fake_world = 0;
+  int group = 0;                       // --group P: all P ranks in this process on one GPU
+  int bench_steps = 0;                 // --bench-steps K: timed block of K solves (bench.py contract)
+  bool autotune = false;               // --autotune: time the multi-rank schedule candidates, keep the fastest
+  bool phases = false;                 // --phases: per-phase breakdown from a traced solve of the timed schedule
+  std::string group_transport = "rccl-self";
   int t2_rows = 0, t2_target = -1, deep_min = -1, t2_occ = -1, tb_min = -1;
   bool force = false;
   int repeat = 1;
@@ -108,8 +114,15 @@ constexpr Personality kPersonalities[] = {
                "  --debug-sync       synchronize after every step (race triage)\n"
                "  --poison-ghosts    NaN-fill ghost layers before every exchange (missed-halo detector)\n"
                "  --fake-rank R/P    perf study: time rank R of a P-rank decomposition alone on one GPU, no transport\n"
+               "  --group P          all P ranks of the decomposition in this process on one GPU (rehearsal of the\n"
+               "                     multi-rank path; --group-transport rccl-self (default: RCCL send/recv, each rank\n"
+               "                     over a one-rank communicator) or loopback (device copies))\n"
                "  --t2-rows R / --t2-target W   fused two-step kernel: rows per wave, x-chunking target (waves)\n"
                "  --repeat R / --warmup W   timed / untimed solves (report min and mean)\n"
+               "  --bench-steps K    then K back-to-back solves between two sync+barriers (max over ranks)\n"
+               "  --autotune         time the multi-rank schedule candidates (slab S4/S4-seq/S3/S2/S1, block) and\n"
+               "                     keep the fastest (slowest rank decides)\n"
+               "  --phases           per-phase device times (init/compute/exchange/check) of the timed schedule\n"
                "  --variant V        leapfrog kernel: 1 = register-queue waves (default), 0 = LDS-staged tile\n"
                "  --tile-rows T      rows per wave (v1: 1,2,4,8) or per workgroup (v0: 4,8,16)\n"
                "  --target-blocks B  x-chunking target (waves for v1, workgroups for v0)\n"
@@ -169,6 +182,11 @@ Args parse(int argc, char** argv) {
       a.fake_rank = std::stoi(v.substr(0, v.find('/')));
       a.fake_world = std::stoi(v.substr(v.find('/') + 1));
     }
+    else if (s == "--group") a.group = std::stoi(next());
+    else if (s == "--bench-steps") a.bench_steps = std::stoi(next());
+    else if (s == "--autotune") a.autotune = true;
+    else if (s == "--phases") a.phases = true;
+    else if (s == "--group-transport") a.group_transport = next();
     else if (s == "--repeat") a.repeat = std::stoi(next());
     else if (s == "--warmup") a.warmup = std::stoi(next());
     else if (s == "--tile-rows") a.tile_rows = std::stoi(next());
@@ -234,6 +252,11 @@ double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Rendezvous of the RCCL unique id through a file on the node. The name is per launch: W3D_RDZV_FILE (the --np
+// self-spawn and bench.py pass a fresh nonce), else MASTER_PORT + TORCHELASTIC_RUN_ID + the launcher's pid (the ranks of
+// one torchrun/mpiexec job share their parent). Rank 0 removes a stale file of that name before publishing, and the
+// other ranks only accept a file written after this process started (minus a grace period for a fast rank 0), so a
+// file left by a crashed earlier job is never consumed.
 std::string rdzv_path() {
   if (const char* p = std::getenv("W3D_RDZV_FILE")) return p;
   const char* port = std::getenv("MASTER_PORT");
@@ -245,7 +268,9 @@ std::string rdzv_path() {
 
 std::string exchange_unique_id(int rank) {
   const std::string path = rdzv_path();
+  static const double t_start = static_cast<double>(std::time(nullptr));
   if (rank == 0) {
+    std::remove(path.c_str());
     const std::string id = Comm::make_unique_id();
     const std::string tmp = path + ".tmp";
     {
@@ -258,8 +283,9 @@ std::string exchange_unique_id(int rank) {
   }
   const double t0 = now_s();
   for (;;) {
-    std::ifstream f(path, std::ios::binary);
-    if (f) {
+    struct stat st {};
+    if (stat(path.c_str(), &st) == 0 && static_cast<double>(st.st_mtime) >= t_start - 60.0) {
+      std::ifstream f(path, std::ios::binary);
       std::string id((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
       if (id.size() == 128) return id;
     }
@@ -325,6 +351,20 @@ int spawn(int np, char** argv) {
   return rc;
 }
 
+// json helpers for the summary line
+std::string jstr(const std::string& v) { return "\"" + v + "\""; }
+std::string jnum(double v) {
+  char b[64];
+  std::snprintf(b, sizeof b, "%.10g", v);
+  return b;
+}
+std::string steps_json(const std::vector<int>& st, const std::vector<double>& mx, const std::vector<double>& rms) {
+  std::string o = "[";
+  for (size_t i = 0; i < st.size(); ++i)
+    o += (i ? ", [" : "[") + std::to_string(st[i]) + ", " + jnum(mx[i]) + ", " + jnum(rms[i]) + "]";
+  return o + "]";
+}
+
 int run_cpu(const Args& a) {
   CpuSolver s(a.prob, a.check_every, a.threads);
   CpuResult r;
@@ -336,17 +376,24 @@ int run_cpu(const Args& a) {
       sum += r.solve_s;
     }
   }
+  double bench_s = 0.0;
+  if (a.bench_steps > 0) {
+    const double t0 = now_s();
+    for (int i = 0; i < a.bench_steps; ++i) r = s.run();
+    bench_s = now_s() - t0;
+  }
   if (!a.quiet) print_errors(r.steps, r.max_err, r.rms_err, a.prob.tau);
   const double gcell = a.prob.cell_updates() / best / 1e9;
   std::printf("Total time: %.6f s (init %.6f s, compute %.6f s), threads %d, %.3f GCell/s\n", best, r.init_s,
               r.compute_s, cpu_max_threads(), gcell);
   if (!a.json.empty()) {
     std::ofstream j(a.json);
-    j << "{\"backend\": \"cpu\", \"N\": " << a.prob.N << ", \"tau\": " << a.prob.tau << ", \"K\": " << a.prob.K
-      << ", \"L\": " << a.prob.L << ", \"threads\": " << cpu_max_threads() << ", \"solve_s\": " << best
-      << ", \"mean_s\": " << sum / a.repeat << ", \"gcell_per_s\": " << gcell
-      << ", \"final_max_err\": " << (r.max_err.empty() ? 0.0 : r.max_err.back())
-      << ", \"final_rms_err\": " << (r.rms_err.empty() ? 0.0 : r.rms_err.back()) << "}\n";
+    j << "{\"backend\": \"cpu\", \"N\": " << a.prob.N << ", \"tau\": " << jnum(a.prob.tau) << ", \"K\": "
+      << a.prob.K << ", \"L\": " << jnum(a.prob.L) << ", \"ranks\": 1, \"dims\": [1, 1, 1], \"threads\": "
+      << cpu_max_threads() << ", \"solve_s\": " << jnum(best) << ", \"mean_s\": " << jnum(sum / a.repeat)
+      << ", \"gcell_per_s\": " << jnum(gcell) << ", \"schedule\": \"cpu-openmp\", \"bench_steps\": " << a.bench_steps
+      << ", \"bench_s\": " << jnum(bench_s) << ", \"finite\": " << (r.finite ? "true" : "false") << ", \"steps\": "
+      << steps_json(r.steps, r.max_err, r.rms_err) << "}\n";
   }
   if (!a.dump.empty()) write_dump(a.dump, a.prob, s.layout(), s.field(0), 0, 1, Dims{1, 1, 1});
   return r.finite ? 0 : 3;
@@ -368,6 +415,14 @@ int run_cpu_rank(const Args& a, ShmGroup& g, int rank) {
         sum += r.solve_s;
       }
     }
+    double bench_s = 0.0;  // the end barrier waits for the slowest rank: rank 0's interval is the max over ranks
+    if (a.bench_steps > 0) {
+      g.barrier();
+      const double t0 = now_s();
+      for (int i = 0; i < a.bench_steps; ++i) r = s.run();
+      g.barrier();
+      bench_s = now_s() - t0;
+    }
     const Dims d = g.dims();
     if (rank == 0) {
       if (!a.quiet) print_errors(r.steps, r.max_err, r.rms_err, a.prob.tau);
@@ -381,7 +436,10 @@ int run_cpu_rank(const Args& a, ShmGroup& g, int rank) {
           << ", \"L\": " << a.prob.L << ", \"threads\": " << cpu_max_threads() << ", \"solve_s\": " << best
           << ", \"mean_s\": " << sum / a.repeat << ", \"exchange_s\": " << exch << ", \"gcell_per_s\": " << gcell
           << ", \"final_max_err\": " << (r.max_err.empty() ? 0.0 : r.max_err.back())
-          << ", \"final_rms_err\": " << (r.rms_err.empty() ? 0.0 : r.rms_err.back()) << "}\n";
+          << ", \"final_rms_err\": " << (r.rms_err.empty() ? 0.0 : r.rms_err.back())
+          << ", \"schedule\": \"cpu-openmp-ranks\", \"bench_steps\": " << a.bench_steps << ", \"bench_s\": "
+          << jnum(bench_s) << ", \"finite\": " << (r.finite ? "true" : "false") << ", \"steps\": "
+          << steps_json(r.steps, r.max_err, r.rms_err) << "}\n";
       }
     }
     if (!a.dump.empty()) write_dump(a.dump, a.prob, s.layout(), s.field(0), rank, g.world(), d);
@@ -392,35 +450,8 @@ int run_cpu_rank(const Args& a, ShmGroup& g, int rank) {
   }
 }
 
-int run_gpu(const Args& a) {
-  static const char* const kRank[] = {"RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID", nullptr};
-  static const char* const kSize[] = {"WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "SLURM_NTASKS", nullptr};
-  static const char* const kLocal[] = {"LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", nullptr};
-  int rank = env_int(kRank, 0), world = env_int(kSize, 1);
-  const bool fake = a.fake_rank >= 0;
-  if (fake) {
-    rank = a.fake_rank;
-    world = a.fake_world;
-  }
-  const double t_proc0 = now_s();
-  int ndev = 0;
-  W3D_HIP(hipGetDeviceCount(&ndev));
-  W3D_REQUIRE(ndev > 0, "no GPU visible (use --cpu for the CPU path)");
-  const int local = env_int(kLocal, rank);
-  const int dev = local % ndev;
-  W3D_HIP(hipSetDevice(dev));
-  hipDeviceProp_t prop;
-  W3D_HIP(hipGetDeviceProperties(&prop, dev));
-
-  std::shared_ptr<Comm> comm;
-  const double t_comm0 = now_s();
-  if (world > 1 && !fake) {
-    const std::string id = exchange_unique_id(rank);
-    comm = std::make_shared<Comm>(rank, world, id);
-    if (rank == 0) std::remove(rdzv_path().c_str());
-  }
-  const double t_comm = now_s() - t_comm0;
-
+// Solver options from the command line (one candidate of the multi-rank schedule autotune overrides a few of them).
+SolverOptions options_from(const Args& a, bool fake) {
   SolverOptions o;
   o.decomp = a.decomp;
   o.check_every = a.check_every;
@@ -443,26 +474,189 @@ int run_gpu(const Args& a) {
   if (a.tile_rows > 0) (o.tiling.variant == 1 ? o.tiling.rows : o.tiling.ty) = a.tile_rows;
   o.tiling.target_blocks = a.target_blocks;
   if (a.nt_store >= 0) o.tiling.nt_store = a.nt_store != 0;
-  GpuSolver s(a.prob, o, rank, world, comm);
-  size_t free_b = 0, total_b = 0;
-  W3D_HIP(hipMemGetInfo(&free_b, &total_b));
+  return o;
+}
+
+int run_group(const Args& a, const SolverOptions& o, const hipDeviceProp_t& prop) {
+  GpuGroup g(a.prob, o, a.group, a.group_transport);
+  RunResult r;
+  double best = 1e30, sum = 0;
+  for (int i = 0; i < a.warmup + a.repeat; ++i) {
+    r = g.run();
+    if (i >= a.warmup) {
+      best = std::min(best, r.solve_s);
+      sum += r.solve_s;
+    }
+  }
+  const Dims d = g.rank(0).dims();
+  if (!a.quiet) {
+    std::printf("wave3d: N=%lld tau=%g K=%d L=%g group of %d ranks (%s) decomp=%dx%dx%d device=%s\n",
+                static_cast<long long>(a.prob.N), a.prob.tau, a.prob.K, a.prob.L, a.group, a.group_transport.c_str(),
+                d.px, d.py, d.pz, prop.gcnArchName);
+    print_errors(r.steps, r.max_err, r.rms_err, a.prob.tau);
+  }
+  std::printf("Total time: %.6f s (group solve on one GPU; best of %d, mean %.6f s); schedule %s, graph %s\n", best,
+              a.repeat, sum / a.repeat, g.rank(0).mode().c_str(), g.graph_enabled() ? "on" : "off");
+  if (!a.dump.empty())
+    for (int q = 0; q < g.world(); ++q)
+      write_dump(a.dump, a.prob, g.rank(q).layout(), g.rank(q).download(0), q, g.world(), d);
+  if (!a.json.empty()) {
+    std::vector<int> cc = g.comm_counts();
+    std::ofstream j(a.json);
+    j << "{\"backend\": \"hip\", \"group\": " << a.group << ", \"transport\": " << jstr(a.group_transport)
+      << ", \"graph\": " << (g.graph_enabled() ? "true" : "false") << ", \"schedule\": " << jstr(g.rank(0).mode())
+      << ", \"rccl_comms\": " << cc.size() << ", \"solve_s\": " << jnum(best) << ", \"steps\": [";
+    for (size_t i = 0; i < r.steps.size(); ++i)
+      j << (i ? ", " : "") << "[" << r.steps[i] << ", " << jnum(r.max_err[i]) << ", " << jnum(r.rms_err[i]) << "]";
+    j << "]}\n";
+  }
+  return r.finite ? 0 : 3;
+}
+
+// One schedule candidate of the multi-rank autotune (bench.py's --autotune): the halo volume of
+// S-deep passes against the per-step exchanges of single steps, overlap against whole passes, slabs against blocks —
+// a trade of xGMI bandwidth/latency against HBM traffic that depends on the node, so each candidate is timed on the
+// real interconnect and every rank adopts the one whose slowest rank was fastest.
+struct Candidate {
+  const char* name;
+  const char* decomp;
+  int temporal;
+  bool overlap;
+};
+constexpr Candidate kCandidates[] = {
+    {"slab-S4", "slab", 4, true},  {"slab-S4-seq", "slab", 4, false}, {"slab-S3", "slab", 3, true},
+    {"slab-S2", "slab", 2, true},  {"slab-S1", "slab", 1, true},      {"block-S1", "block", 1, true},
+};
+
+int run_gpu(const Args& a) {
+  static const char* const kRank[] = {"RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID", nullptr};
+  static const char* const kSize[] = {"WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "SLURM_NTASKS", nullptr};
+  static const char* const kLocal[] = {"LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", nullptr};
+  int rank = env_int(kRank, 0), world = env_int(kSize, 1);
+  const bool fake = a.fake_rank >= 0;
+  if (fake) {
+    rank = a.fake_rank;
+    world = a.fake_world;
+  }
+  const double t_proc0 = now_s();
+  int ndev = 0;
+  W3D_HIP(hipGetDeviceCount(&ndev));
+  W3D_REQUIRE(ndev > 0, "no GPU visible (use --cpu for the CPU path)");
+  const int local = env_int(kLocal, rank);
+  const int dev = local % ndev;
+  W3D_HIP(hipSetDevice(dev));
+  hipDeviceProp_t prop;
+  W3D_HIP(hipGetDeviceProperties(&prop, dev));
+  const SolverOptions base = options_from(a, fake);
+  if (a.group > 0) return run_group(a, base, prop);
+
+  std::shared_ptr<Comm> comm;
+  const double t_comm0 = now_s();
+  if (world > 1 && !fake) {
+    W3D_REQUIRE(local < ndev || std::getenv("W3D_SHARE_GPUS"),
+                "rank " + std::to_string(rank) + " has local rank " + std::to_string(local) + " but only " +
+                    std::to_string(ndev) + " GPU(s) are visible (RCCL needs one GPU per rank)");
+    const std::string id = exchange_unique_id(rank);
+    comm = std::make_shared<Comm>(rank, world, id);
+    if (rank == 0) std::remove(rdzv_path().c_str());
+  }
+  const double t_comm = now_s() - t_comm0;
+  const int rccl_nranks = comm ? comm->count() : 0;
+  // fault injection: W3D_FAULT_RANK=r makes rank r fail right after the communicator is up; its peers
+  // then fail in their next collective (GPU-wait timeout W3D_TIMEOUT_S) instead of hanging
+  if (const char* fr = std::getenv("W3D_FAULT_RANK"); fr && std::atoi(fr) == rank) fail("injected fault");
+
+  // every rank takes the same branch: min over ranks of a 0/1 flag (RCCL all-reduce)
+  auto agree = [&](bool ok) {
+    return comm ? comm_allreduce(*comm, ok ? 1.0 : 0.0, false) == static_cast<double>(world) : ok;
+  };
+  auto max_over_ranks = [&](double v) { return comm ? comm_allreduce(*comm, v, true) : v; };
+
+  std::unique_ptr<GpuSolver> s;
+  std::string sched = a.decomp + "-S" + std::to_string(a.temporal) + (a.overlap ? "" : "-seq");
+  std::vector<std::pair<std::string, double>> tuned;
+  if (a.autotune && (world > 1 || a.fake_rank < 0)) {
+    double best_t = 1e30;
+    for (const Candidate& c : kCandidates) {
+      if (std::string(c.decomp) == "block" && world < 4) continue;  // (2 ranks: "block" is the slab)
+      SolverOptions o = base;
+      o.decomp = c.decomp;
+      o.temporal = c.temporal;
+      o.overlap = c.overlap;
+      std::unique_ptr<GpuSolver> cand;
+      std::string err;
+      try {
+        cand = std::make_unique<GpuSolver>(a.prob, o, rank, world, comm);
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
+      if (!agree(static_cast<bool>(cand))) {  // a schedule some rank cannot build: skipped everywhere
+        if (!err.empty()) std::fprintf(stderr, "[wave3d rank %d] candidate %s rejected: %s\n", rank, c.name, err.c_str());
+        continue;
+      }
+      double t = 1e30;
+      cand->run();  // eager: RCCL peer connections
+      cand->run();  // graph capture
+      for (int k = 0; k < 3; ++k) {
+        if (comm) comm_barrier(*comm);
+        t = std::min(t, cand->run().solve_s);
+      }
+      t = max_over_ranks(t);
+      tuned.emplace_back(c.name, t);
+      if (t < best_t) {
+        best_t = t;
+        s = std::move(cand);
+        sched = c.name;
+      }
+    }
+    W3D_REQUIRE(s != nullptr, "autotune: no candidate schedule could be built");
+  } else {
+    s = std::make_unique<GpuSolver>(a.prob, base, rank, world, comm);
+  }
 
   RunResult r;
   double best = 1e30, sum = 0, first = 0;
   for (int i = 0; i < a.warmup + a.repeat; ++i) {
     if (comm) comm_barrier(*comm);
-    r = s.run();
-    double t = r.solve_s;
-    if (comm) t = comm_allreduce(*comm, t, true);  // max over ranks
+    r = s->run();
+    const double t = max_over_ranks(r.solve_s);
     if (i == 0) first = t;
     if (i >= a.warmup) {
       best = std::min(best, t);
       sum += t;
     }
   }
+  // --bench-steps K: the bench.py contract — K back-to-back solves bracketed by a device sync + barrier on both sides,
+  // elapsed time max over ranks
+  double bench_s = 0.0;
+  if (a.bench_steps > 0) {
+    W3D_HIP(hipDeviceSynchronize());
+    if (comm) comm_barrier(*comm);
+    const double t0 = now_s();
+    for (int i = 0; i < a.bench_steps; ++i) r = s->run();
+    W3D_HIP(hipDeviceSynchronize());
+    if (comm) comm_barrier(*comm);
+    bench_s = max_over_ranks(now_s() - t0);
+  }
+  // per-phase breakdown of the schedule that was timed: one more solve with the same kernels, traced with events
+  PhaseTimes ph;
+  if (a.phases && !a.timers) {
+    s->set_timers(true);  // same solver, same schedule and kernels, launched eagerly with events around each phase
+    if (comm) comm_barrier(*comm);
+    ph = s->run().phases;
+    s->set_timers(false);
+    ph.init_ms = max_over_ranks(ph.init_ms);
+    ph.shell_ms = max_over_ranks(ph.shell_ms);
+    ph.interior_ms = max_over_ranks(ph.interior_ms);
+    ph.comm_ms = max_over_ranks(ph.comm_ms);
+    ph.check_ms = max_over_ranks(ph.check_ms);
+    ph.gather_ms = max_over_ranks(ph.gather_ms);
+  }
   const double mean = sum / a.repeat;
   const double t_proc = now_s() - t_proc0;
-  const Dims d = s.dims();
+  const Dims d = s->dims();
+  int hipv = 0;
+  (void)hipRuntimeGetVersion(&hipv);
   if (rank == 0 || fake) {
     if (!a.quiet) {
       std::printf("wave3d: N=%lld tau=%g K=%d L=%g ranks=%d decomp=%dx%dx%d device=%s courant=%.3f\n",
@@ -474,26 +668,43 @@ int run_gpu(const Args& a) {
     std::printf("Total time: %.6f s (solve region, max over %d rank%s; best of %d, mean %.6f s, first %.6f s)\n", best,
                 world, world > 1 ? "s" : "", a.repeat, mean, first);
     std::printf(
-        "Throughput: %.2f GCell/s; process wall-clock %.3f s (RCCL init %.3f s); schedule %s, graph %s, overlap %s\n",
-        gcell, t_proc, t_comm, s.mode().c_str(), s.options().graph ? "on" : "off", a.overlap ? "on" : "off");
-    if (a.timers)
+        "Throughput: %.2f GCell/s; process wall-clock %.3f s (RCCL init %.3f s, %d ranks); schedule %s (%s), graph %s,"
+        " overlap %s\n",
+        gcell, t_proc, t_comm, rccl_nranks, s->mode().c_str(), sched.c_str(), s->options().graph ? "on" : "off",
+        s->options().overlap ? "on" : "off");
+    if (a.bench_steps > 0)
+      std::printf("Bench: %d solves in %.6f s (%.6f s per solve, max over ranks)\n", a.bench_steps, bench_s,
+                  bench_s / a.bench_steps);
+    const PhaseTimes& pp = a.timers ? r.phases : ph;
+    if (a.timers || a.phases)
       std::printf(
-          "Phases (rank 0, last run, device ms): init %.3f | compute %.3f (shell %.3f) | exchange %.3f | check %.3f"
+          "Phases (%s, device ms, max over ranks): init %.3f | compute %.3f (shell %.3f) | exchange %.3f | check %.3f"
           " | gather+sync (host) %.3f\n",
-          r.phases.init_ms, r.phases.interior_ms + r.phases.shell_ms, r.phases.shell_ms, r.phases.comm_ms,
-          r.phases.check_ms, r.phases.gather_ms);
+          a.timers ? "this run" : "traced solve of the timed schedule", pp.init_ms, pp.interior_ms + pp.shell_ms,
+          pp.shell_ms, pp.comm_ms, pp.check_ms, pp.gather_ms);
     if (!a.json.empty()) {
       std::ofstream j(a.json);
-      j.precision(10);
-      j << "{\"backend\": \"hip\", \"N\": " << a.prob.N << ", \"tau\": " << a.prob.tau << ", \"K\": " << a.prob.K
-        << ", \"L\": " << a.prob.L << ", \"ranks\": " << world << ", \"dims\": [" << d.px << ", " << d.py << ", "
-        << d.pz << "], \"solve_s\": " << best << ", \"mean_s\": " << mean << ", \"first_s\": " << first
-        << ", \"process_s\": " << t_proc << ", \"rccl_init_s\": " << t_comm << ", \"gcell_per_s\": " << gcell
-        << ", \"graph\": " << (s.options().graph ? "true" : "false") << ", \"overlap\": "
-        << (a.overlap ? "true" : "false") << ", \"schedule\": \"" << s.mode() << "\", \"device\": \""
-        << prop.gcnArchName << "\", \"steps\": [";
+      j << "{\"backend\": \"hip\", \"N\": " << a.prob.N << ", \"tau\": " << jnum(a.prob.tau) << ", \"K\": " << a.prob.K
+        << ", \"L\": " << jnum(a.prob.L) << ", \"ranks\": " << world << ", \"dims\": [" << d.px << ", " << d.py
+        << ", " << d.pz << "], \"solve_s\": " << jnum(best) << ", \"mean_s\": " << jnum(mean)
+        << ", \"first_s\": " << jnum(first) << ", \"process_s\": " << jnum(t_proc) << ", \"rccl_init_s\": "
+        << jnum(t_comm) << ", \"rccl_nranks\": " << rccl_nranks << ", \"rccl_version\": " << rccl_version()
+        << ", \"hip_runtime\": " << hipv << ", \"gcell_per_s\": " << jnum(gcell)
+        << ", \"graph\": " << (s->options().graph ? "true" : "false") << ", \"overlap\": "
+        << (s->options().overlap ? "true" : "false") << ", \"temporal\": " << s->options().temporal
+        << ", \"schedule\": " << jstr(sched) << ", \"mode\": " << jstr(s->mode()) << ", \"device\": "
+        << jstr(prop.gcnArchName) << ", \"bench_steps\": " << a.bench_steps << ", \"bench_s\": " << jnum(bench_s)
+        << ", \"warmup\": " << a.warmup << ", \"finite\": " << (r.finite ? "true" : "false") << ", \"autotune_s\": {";
+      for (size_t i = 0; i < tuned.size(); ++i) j << (i ? ", " : "") << jstr(tuned[i].first) << ": " << jnum(tuned[i].second);
+      j << "}";
+      if (a.timers || a.phases)
+        j << ", \"phases_ms\": {\"init\": " << jnum(pp.init_ms) << ", \"compute\": "
+          << jnum(pp.interior_ms + pp.shell_ms) << ", \"shell\": " << jnum(pp.shell_ms) << ", \"exchange\": "
+          << jnum(pp.comm_ms) << ", \"check\": " << jnum(pp.check_ms) << ", \"gather_host\": " << jnum(pp.gather_ms)
+          << "}";
+      j << ", \"steps\": [";
       for (size_t i = 0; i < r.steps.size(); ++i)
-        j << (i ? ", " : "") << "[" << r.steps[i] << ", " << r.max_err[i] << ", " << r.rms_err[i] << "]";
+        j << (i ? ", " : "") << "[" << r.steps[i] << ", " << jnum(r.max_err[i]) << ", " << jnum(r.rms_err[i]) << "]";
       j << "]}\n";
     }
   }
@@ -503,12 +714,10 @@ int run_gpu(const Args& a) {
     t.precision(6);
     for (const UnitTrace& u : r.trace)
       t << "{\"rank\": " << rank << ", \"unit\": " << u.unit << ", \"n\": " << u.n << ", \"steps\": " << u.steps
-        << ", \"schedule\": \"" << s.mode() << "\", \"shell_ms\": " << u.shell_ms << ", \"comm_ms\": " << u.comm_ms
+        << ", \"schedule\": \"" << s->mode() << "\", \"shell_ms\": " << u.shell_ms << ", \"comm_ms\": " << u.comm_ms
         << ", \"compute_ms\": " << u.compute_ms << ", \"check_ms\": " << u.check_ms << "}\n";
   }
-  if (!a.dump.empty()) write_dump(a.dump, a.prob, s.layout(), s.download(0), rank, world, d);
-  (void)free_b;
-  (void)total_b;
+  if (!a.dump.empty()) write_dump(a.dump, a.prob, s->layout(), s->download(0), rank, world, d);
   return r.finite ? 0 : 3;
 }
 

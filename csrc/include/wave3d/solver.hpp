@@ -89,6 +89,10 @@ class Comm {
   Comm& operator=(const Comm&) = delete;
   int rank() const { return rank_; }
   int world() const { return world_; }
+  // ranks of the communicator as RCCL itself reports them (ncclCommCount): proof of what RCCL saw
+  int count() const;
+  // device the communicator is bound to (ncclCommCuDevice)
+  int device() const;
   void* raw() const { return comm_; }  // ncclComm_t
   // Raise if RCCL reported an asynchronous error.
   void check_async() const;
@@ -109,6 +113,9 @@ class GpuSolver {
 
   // One full solve: u⁰, u¹ → K−1 leapfrog steps with error checks → global error log on the host.
   RunResult run();
+  // Per-phase event timers for the following run() calls (those launch eagerly; the captured graph is kept for when
+  // the timers are switched off again): a phase breakdown of exactly the schedule the graph replays.
+  void set_timers(bool on) { opt_.timers = on; }
 
   // Host copy of the local array holding u^K (which = 0) or u^{K−1} (which = 1), full padded layout.
   std::vector<double> download(int which) const;
@@ -131,7 +138,11 @@ class GpuSolver {
  private:
   friend class GpuGroup;
   void enqueue_solve();  // all device work of one solve on s0/s1 (graph-capturable)
-  void exchange(hipStream_t st);
+  // One halo exchange on stream st: pack → ncclGroup{ncclSend/ncclRecv per message} → unpack. `pull` != null: this
+  // rank belongs to an in-process group driven over a one-rank communicator (GpuGroup "rccl-self"); every message is
+  // then moved by a self send/recv pair on THIS rank's communicator, sending the peer's matching face (already packed
+  // by the peer) into this rank's receive region — the same RCCL calls, stream and events as the multi-process path.
+  void exchange(hipStream_t st, const std::vector<GpuSolver*>* pull = nullptr);
   void gather_errors(RunResult& r);
   // Schedule: a solve is phase_init() followed by units; a unit advances one step (in place over u^{n−1}) or 2..4
   // (a fused pass into the two free buffers). Multi-rank units run shell -> exchange -> interior.
@@ -149,6 +160,7 @@ class GpuSolver {
     double* recv;
     i64 count;
   };
+  const Msg& peer_msg(const Msg& m, const std::vector<GpuSolver*>& ranks) const;
   bool split() const;
   bool post_exchange() const;  // the unit's NEW field is exchanged after its shell (else: current field, before)
   // deep-tb without overlap: no shell launches; each pass runs whole and its faces are exchanged after it (on s0)
@@ -165,9 +177,10 @@ class GpuSolver {
   void unit_interior(int i);
   void tb_pass(const Unit& u, const LBox& box, int phase);  // one k_leapfrog_tb launch of unit u over box
   LBox tb_interior(int i) const;                            // deep-tb: the box left after unit i's shells
+  // in-process group steps (GpuGroup): pack own faces → (group barrier) → pull peers' faces → (group barrier)
   void lb_pack(int i);
-  void lb_pull(int i, const std::vector<GpuSolver*>& ranks);
-  void lb_fence(int i, const std::vector<GpuSolver*>& ranks);
+  void lb_pull(int i, const std::vector<GpuSolver*>& ranks, hipEvent_t all_packed);
+  void lb_fence(int i, hipEvent_t all_pulled);
 
   Problem prob_;
   SolverOptions opt_;
@@ -245,18 +258,47 @@ namespace wave3d {
 
 // P ranks of one decomposition inside ONE process on the current device, halos moved by device-to-device copies.
 // Same GpuSolver code as production except the transport; used to validate the multi-rank path on one GPU.
+// Transports:
+//   "loopback"  : halos by hipMemcpyAsync between the ranks' buffers (no RCCL);
+//   "rccl-self" : every rank owns a ONE-rank RCCL communicator (RCCL refuses two ranks of one communicator on one
+//                 device, but a one-rank communicator may send to itself) and moves each of its messages with
+//                 ncclGroupStart; ncclSend(peer's face, 0); ncclRecv(own ghosts, 0); ncclGroupEnd on its side stream,
+//                 the error logs go through ncclAllGather on the same communicators. This executes the production
+//                 RCCL calls, their stream placement and event joins on a one-GPU box.
+// With options.graph the whole group solve (every rank's streams forked from one group stream) is captured into one
+// hipGraph after the first (eager) run and replayed, RCCL kernels included.
 class GpuGroup {
  public:
-  GpuGroup(const Problem& prob, const SolverOptions& opt, int world);
+  GpuGroup(const Problem& prob, const SolverOptions& opt, int world, const std::string& transport = "loopback");
+  ~GpuGroup();
+  GpuGroup(const GpuGroup&) = delete;
+  GpuGroup& operator=(const GpuGroup&) = delete;
   RunResult run();  // global error log (rank-ordered combine), solve_s = wall time of the group solve
   GpuSolver& rank(int r) { return *ranks_[static_cast<size_t>(r)]; }
   int world() const { return static_cast<int>(ranks_.size()); }
+  const std::string& transport() const { return transport_; }
+  bool graph_enabled() const { return graph_; }
+  // RCCL communicators in use and the rank count each reports (rccl-self: world one-rank communicators)
+  std::vector<int> comm_counts() const;
 
  private:
+  void enqueue();
+  void join();
   std::vector<std::unique_ptr<GpuSolver>> ranks_;
+  std::string transport_;
+  bool graph_ = false;
+  int runs_ = 0;
+  hipStream_t gs_ = nullptr;
+  hipEvent_t fork_ = nullptr;
+  hipEvent_t all_packed_ = nullptr, all_pulled_ = nullptr;  // group barriers on gs_ (see enqueue)
+  std::vector<hipEvent_t> join_;
+  hipGraphExec_t exec_ = nullptr;
 };
 
 // Host-scalar collectives over the RCCL communicator (timer max-reduction, barriers). Blocking.
 double comm_allreduce(const Comm& c, double v, bool max_op);
+int rccl_version();  // ncclGetVersion of the RCCL resolved at run time
+// Whether this process's HIP runtime captures the multi-rank (multi-stream) schedules correctly (HIP >= 7.2).
+bool multistream_capture_safe();
 void comm_barrier(const Comm& c);
 }  // namespace wave3d

@@ -268,6 +268,19 @@ PYBIND11_MODULE(_C, m) {
     return n;
   });
   m.def("gpu_set_device", [](int d) { W3D_HIP(hipSetDevice(d)); });
+  // versions of the HIP runtime and RCCL this process actually resolved (torch may have loaded its bundled copies)
+  m.def("runtime_versions", []() {
+    int hv = 0, dv = 0, nv = 0;
+    (void)hipRuntimeGetVersion(&hv);
+    (void)hipDriverGetVersion(&dv);
+    nv = rccl_version();
+    py::dict d;
+    d["hip_runtime"] = hv;
+    d["hip_driver"] = dv;
+    d["rccl"] = nv;
+    d["multistream_capture_safe"] = multistream_capture_safe();
+    return d;
+  });
   m.def("gpu_synchronize", []() { W3D_HIP(hipDeviceSynchronize()); });
   m.def("gpu_arch", []() {
     int d = 0;
@@ -396,6 +409,8 @@ PYBIND11_MODULE(_C, m) {
       .def_static("make_unique_id", []() { return py::bytes(Comm::make_unique_id()); })
       .def_property_readonly("rank", &Comm::rank)
       .def_property_readonly("world", &Comm::world)
+      .def("count", &Comm::count)
+      .def("device", &Comm::device)
       .def("check_async", &Comm::check_async);
 
   py::class_<GpuSolver>(m, "GpuSolver")
@@ -432,8 +447,11 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("graph_enabled", [](const GpuSolver& s) { return s.options().graph; });
 
   py::class_<GpuGroup>(m, "GpuGroup")
-      .def(py::init<const Problem&, const SolverOptions&, int>(), py::arg("problem"), py::arg("options"),
-           py::arg("world"))
+      .def(py::init([](const Problem& p, const SolverOptions& o, int world, const std::string& transport) {
+             py::gil_scoped_release nogil;
+             return std::make_unique<GpuGroup>(p, o, world, transport);
+           }),
+           py::arg("problem"), py::arg("options"), py::arg("world"), py::arg("transport") = "loopback")
       .def("run",
            [](GpuGroup& g) {
              RunResult r;
@@ -452,5 +470,8 @@ PYBIND11_MODULE(_C, m) {
       .def("layout", [](GpuGroup& g, int rank) { return g.rank(rank).layout(); })
       .def("dims", [](GpuGroup& g) { return g.rank(0).dims(); })
       .def("mode", [](GpuGroup& g) { return g.rank(0).mode(); })
+      .def("comm_counts", &GpuGroup::comm_counts)
+      .def_property_readonly("transport", &GpuGroup::transport)
+      .def_property_readonly("graph_enabled", &GpuGroup::graph_enabled)
       .def_property_readonly("world", &GpuGroup::world);
 }

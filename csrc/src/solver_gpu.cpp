@@ -7,6 +7,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -34,18 +36,30 @@ Comm::Comm(int rank, int world, const std::string& unique_id) : rank_(rank), wor
   ncclComm_t c = nullptr;
   W3D_NCCL(ncclCommInitRank(&c, world, id, rank));
   comm_ = c;
-  // self-test: one all-reduce of 1 per rank must give the world size. A communicator that cannot move data fails here
-  // (with RCCL's error or the GPU-wait timeout) instead of inside a captured solve, so callers can fall back early.
-  if (world > 1) {
-    try {
-      const double n = comm_allreduce(*this, 1.0, false);
-      W3D_REQUIRE(n == static_cast<double>(world), "RCCL self-test: all-reduce of 1 per rank gave " + std::to_string(n));
-    } catch (...) {
-      ncclCommAbort(c);  // the destructor does not run for a throwing constructor
-      comm_ = nullptr;
-      throw;
-    }
+  // self-test: one all-reduce of 1 per rank must give the world size, and RCCL must report `world` ranks. A
+  // communicator that cannot move data fails here (with RCCL's error or the GPU-wait timeout) instead of inside a
+  // captured solve. Run for every size (a one-rank communicator of the rccl-self group included).
+  try {
+    W3D_REQUIRE(count() == world, "RCCL self-test: ncclCommCount gave " + std::to_string(count()));
+    const double n = comm_allreduce(*this, 1.0, false);
+    W3D_REQUIRE(n == static_cast<double>(world), "RCCL self-test: all-reduce of 1 per rank gave " + std::to_string(n));
+  } catch (...) {
+    ncclCommAbort(c);  // the destructor does not run for a throwing constructor
+    comm_ = nullptr;
+    throw;
   }
+}
+
+int Comm::count() const {
+  int n = 0;
+  W3D_NCCL(ncclCommCount(static_cast<ncclComm_t>(comm_), &n));
+  return n;
+}
+
+int Comm::device() const {
+  int d = -1;
+  W3D_NCCL(ncclCommCuDevice(static_cast<ncclComm_t>(comm_), &d));
+  return d;
 }
 
 Comm::~Comm() {
@@ -92,6 +106,22 @@ void wait_stream(hipStream_t s, const Comm* comm, double timeout_s) {
 }
 
 }  // namespace
+
+// Multi-stream captures with cross-stream event joins repeated per unit (the multi-rank schedules: side-stream
+// exchange joined back every pass) crash inside hipStreamEndCapture of the HIP 7.0 runtime that PyTorch-ROCm bundles
+// (tools/capture_probe.hip pattern 5, capture_probe2.hip); the system ROCm 7.2 runtime captures them correctly
+// (probed, and the rccl-self group graphs). Multi-rank solves are therefore captured only on HIP >= 7.2 (the native
+// CLI, which bench.py runs per rank, always is); inside a torch process they run eagerly. W3D_FORCE_CAPTURE=1
+// overrides the check.
+bool multistream_capture_safe() {
+  static const bool ok = [] {
+    if (const char* f = std::getenv("W3D_FORCE_CAPTURE"); f && *f == '1') return true;
+    int v = 0;
+    if (hipRuntimeGetVersion(&v) != hipSuccess) return false;
+    return v >= 70200000;
+  }();
+  return ok;
+}
 
 GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, int world, std::shared_ptr<Comm> comm,
                      bool loopback)
@@ -244,6 +274,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   W3D_HIP(hipMalloc(&errall_, static_cast<size_t>(world_) * (prob_.K + 1) * sizeof(Partial)));
   ct_.resize(static_cast<size_t>(prob_.K + 1));
   for (int n = 0; n <= prob_.K; ++n) ct_[static_cast<size_t>(n)] = time_factor(prob_, n);
+  // (group ranks: the GpuGroup captures the whole group solve itself)
   if (opt_.timers || opt_.debug_sync || loopback_) opt_.graph = false;
 }
 
@@ -530,16 +561,31 @@ void GpuSolver::unit_shell(int i) {
   }
 }
 
-void GpuSolver::exchange(hipStream_t st) {
+const GpuSolver::Msg& GpuSolver::peer_msg(const Msg& m, const std::vector<GpuSolver*>& ranks) const {
+  const GpuSolver* q = ranks[static_cast<size_t>(m.peer)];
+  const Msg* g = nullptr;
+  for (const Msg& h : q->msgs_)
+    if (h.peer == rank_ && h.tag == m.tag) g = &h;
+  W3D_REQUIRE(g && g->count == m.count, "group exchange: mismatched messages");
+  return *g;
+}
+
+void GpuSolver::exchange(hipStream_t st, const std::vector<GpuSolver*>* pull) {
   const bool packed = mode_ == Mode::kSingleStep && plan_.packed_doubles > 0;
   double* field = post_exchange() ? u_[old_] : u_[cur_];
-  if (packed) launch_pack(lay_, plan_, field, send_buf_, st);
+  if (packed && !pull) launch_pack(lay_, plan_, field, send_buf_, st);  // (group: each rank packed its own faces)
   if (!opt_.fake_comm) {  // fake_comm (perf study): one rank's schedule timed alone, ghosts keep stale values
     ncclComm_t c = static_cast<ncclComm_t>(comm_->raw());
     W3D_NCCL(ncclGroupStart());
     for (const Msg& m : msgs_) {
-      W3D_NCCL(ncclSend(m.send, static_cast<size_t>(m.count), ncclFloat64, m.peer, c, st));
-      W3D_NCCL(ncclRecv(m.recv, static_cast<size_t>(m.count), ncclFloat64, m.peer, c, st));
+      if (pull) {  // one-rank communicator: the k-th send to self pairs with the k-th receive from self
+        const Msg& g = peer_msg(m, *pull);
+        W3D_NCCL(ncclSend(g.send, static_cast<size_t>(m.count), ncclFloat64, 0, c, st));
+        W3D_NCCL(ncclRecv(m.recv, static_cast<size_t>(m.count), ncclFloat64, 0, c, st));
+      } else {
+        W3D_NCCL(ncclSend(m.send, static_cast<size_t>(m.count), ncclFloat64, m.peer, c, st));
+        W3D_NCCL(ncclRecv(m.recv, static_cast<size_t>(m.count), ncclFloat64, m.peer, c, st));
+      }
     }
     W3D_NCCL(ncclGroupEnd());
   }
@@ -593,7 +639,9 @@ void GpuSolver::unit_interior(int i) {
   const bool chk = is_check_[static_cast<size_t>(nc)] != 0;
   const double ct = ct_[static_cast<size_t>(nc)];
   const double* s = d_s_ + 1;
-  const bool wait = needs_exchange(i) && xstream() != s0_;
+  // (group ranks: lb_fence already put s0 behind every rank's pull, ev_halo_ included; a second, redundant wait on
+  // the own side stream after that fence crashes HIP 7.2's hipStreamEndCapture — tools/capture_probe2.hip flag 36)
+  const bool wait = needs_exchange(i) && xstream() != s0_ && !loopback_;
   int np = 0;  // partials to reduce
   if (mode_ == Mode::kDeep) {
     int off = 0;
@@ -724,33 +772,31 @@ void GpuSolver::lb_pack(int i) {
   W3D_HIP(hipEventRecord(ev_packed_, xs));
 }
 
-void GpuSolver::lb_pull(int i, const std::vector<GpuSolver*>& ranks) {
+void GpuSolver::lb_pull(int i, const std::vector<GpuSolver*>& ranks, hipEvent_t all_packed) {
   if (!needs_exchange(i)) return;
   hipStream_t xs = xstream();
   if (opt_.poison_ghosts) poison(xs);
-  for (const Msg& m : msgs_) {
-    const GpuSolver* q = ranks[static_cast<size_t>(m.peer)];
-    const Msg* g = nullptr;
-    for (const Msg& h : q->msgs_)
-      if (h.peer == rank_ && h.tag == m.tag) g = &h;
-    W3D_REQUIRE(g && g->count == m.count, "loopback: mismatched messages");
-    W3D_HIP(hipStreamWaitEvent(xs, q->ev_packed_, 0));
-    W3D_HIP(hipMemcpyAsync(m.recv, g->send, static_cast<size_t>(m.count) * sizeof(double), hipMemcpyDeviceToDevice,
-                           xs));
+  W3D_HIP(hipStreamWaitEvent(xs, all_packed, 0));  // every peer's faces are packed
+  if (comm_) {  // rccl-self: the production exchange (RCCL send/recv on xs) over this rank's one-rank communicator
+    timed(kPhaseComm, xs, [&] { exchange(xs, &ranks); });
+  } else {
+    for (const Msg& m : msgs_) {
+      const Msg& g = peer_msg(m, ranks);
+      W3D_HIP(hipMemcpyAsync(m.recv, g.send, static_cast<size_t>(m.count) * sizeof(double), hipMemcpyDeviceToDevice,
+                             xs));
+    }
+    if (mode_ == Mode::kSingleStep && plan_.packed_doubles > 0)
+      launch_unpack(lay_, plan_, recv_buf_, post_exchange() ? u_[old_] : u_[cur_], xs);
   }
-  if (mode_ == Mode::kSingleStep && plan_.packed_doubles > 0)
-    launch_unpack(lay_, plan_, recv_buf_, post_exchange() ? u_[old_] : u_[cur_], xs);
   W3D_HIP(hipEventRecord(ev_halo_, xs));
 }
 
-void GpuSolver::lb_fence(int i, const std::vector<GpuSolver*>& ranks) {
-  // the peers have read this rank's send regions once their pulls are done: keep both streams behind them
+void GpuSolver::lb_fence(int i, hipEvent_t all_pulled) {
+  // the peers have read this rank's send regions once their pulls are done: keep both streams behind them (the side
+  // stream only when this schedule uses it: a captured stream that only ever waits trips HIP 7.2's end of capture)
   if (!needs_exchange(i)) return;
-  for (const Msg& m : msgs_) {
-    const GpuSolver* q = ranks[static_cast<size_t>(m.peer)];
-    W3D_HIP(hipStreamWaitEvent(s0_, q->ev_halo_, 0));
-    W3D_HIP(hipStreamWaitEvent(s1_, q->ev_halo_, 0));
-  }
+  W3D_HIP(hipStreamWaitEvent(s0_, all_pulled, 0));
+  if (xstream() != s0_) W3D_HIP(hipStreamWaitEvent(s1_, all_pulled, 0));
 }
 
 void GpuSolver::gather_errors(RunResult& r) {
@@ -786,8 +832,9 @@ RunResult GpuSolver::run() {
   RunResult r;
   // RCCL ranks run their first solve eagerly: the peer connections (and RCCL's proxy threads) are set up at the
   // first send/recv, which must not happen inside a stream capture; the capture follows on the second run
+  if (world_ > 1 && !multistream_capture_safe()) opt_.graph = false;
   const bool capture_ok = !(world_ > 1 && comm_) || runs_ >= 1;
-  if (opt_.graph && !graph_exec_ && capture_ok) {
+  if (opt_.graph && !graph_exec_ && capture_ok && !opt_.timers) {
     // capture once (outside the timed region of later runs); fall back to eager launches if capture is refused
     hipGraph_t g = nullptr;
     bool ok = hipStreamBeginCapture(s0_, hipStreamCaptureModeThreadLocal) == hipSuccess;
@@ -809,7 +856,7 @@ RunResult GpuSolver::run() {
     }
   }
   const double t0 = now_s();
-  if (graph_exec_)
+  if (graph_exec_ && !opt_.timers)
     W3D_HIP(hipGraphLaunch(graph_exec_, s0_));
   else
     enqueue_solve();
@@ -851,46 +898,185 @@ double comm_allreduce(const Comm& c, double v, bool max_op) {
 
 void comm_barrier(const Comm& c) { (void)comm_allreduce(c, 0.0, false); }
 
+int rccl_version() {
+  int v = 0;
+  (void)ncclGetVersion(&v);
+  return v;
+}
+
 }  // namespace wave3d
 
 namespace wave3d {
 
-GpuGroup::GpuGroup(const Problem& prob, const SolverOptions& opt, int world) {
+GpuGroup::GpuGroup(const Problem& prob, const SolverOptions& opt, int world, const std::string& transport)
+    : transport_(transport) {
   W3D_REQUIRE(world >= 1, "world must be >= 1");
-  for (int r = 0; r < world; ++r) ranks_.push_back(std::make_unique<GpuSolver>(prob, opt, r, world, nullptr, true));
+  W3D_REQUIRE(transport == "loopback" || transport == "rccl-self",
+              "group transport must be loopback or rccl-self, not " + transport);
+  for (int r = 0; r < world; ++r) {
+    std::shared_ptr<Comm> c;
+    if (transport == "rccl-self") c = std::make_shared<Comm>(0, 1, Comm::make_unique_id());
+    ranks_.push_back(std::make_unique<GpuSolver>(prob, opt, r, world, c, true));
+  }
+  graph_ = opt.graph && !opt.timers && !opt.debug_sync && (world == 1 || multistream_capture_safe());
+  W3D_HIP(hipStreamCreateWithFlags(&gs_, hipStreamNonBlocking));
+  W3D_HIP(hipEventCreateWithFlags(&fork_, hipEventDisableTiming));
+  W3D_HIP(hipEventCreateWithFlags(&all_packed_, hipEventDisableTiming));
+  W3D_HIP(hipEventCreateWithFlags(&all_pulled_, hipEventDisableTiming));
+  join_.resize(2 * static_cast<size_t>(world));
+  for (hipEvent_t& e : join_) W3D_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+}
+
+GpuGroup::~GpuGroup() {
+  if (exec_) (void)hipGraphExecDestroy(exec_);
+  for (hipEvent_t e : join_) (void)hipEventDestroy(e);
+  for (hipEvent_t e : {fork_, all_packed_, all_pulled_})
+    if (e) (void)hipEventDestroy(e);
+  if (gs_) (void)hipStreamDestroy(gs_);
+}
+
+std::vector<int> GpuGroup::comm_counts() const {
+  std::vector<int> v;
+  for (const auto& r : ranks_)
+    if (r->comm_) v.push_back(r->comm_->count());
+  return v;
+}
+
+// Every rank's schedule, interleaved unit by unit exactly as the ranks of a multi-process run would issue them.
+void GpuGroup::enqueue() {
+  std::vector<GpuSolver*> rs;
+  for (auto& p : ranks_) rs.push_back(p.get());
+  const bool dbg = std::getenv("W3D_DEBUG") != nullptr;
+  auto step = [&](const char* what, int i) {
+    if (dbg) std::fprintf(stderr, "[group] unit %d %s\n", i, what);
+  };
+  for (auto* s : rs) {
+    s->phase_init();
+    s->tb_region_ = 0;
+    s->pending_.clear();
+  }
+  step("init", -1);
+  const int nu = static_cast<int>(rs[0]->units_.size());
+  const bool late = rs[0]->late_exchange();
+  for (int i = 0; i < nu; ++i) {
+    for (auto* s : rs) s->unit_shell(i);
+    step("shell", i);
+    if (late)
+      for (auto* s : rs) s->unit_interior(i);
+    // Cross-rank ordering goes through the group stream: it joins every rank's "packed" event, and every puller
+    // waits on the join (likewise "pulled" before anyone overwrites its send regions). Direct waits of one rank's
+    // stream on a PEER's side-stream event are avoided on purpose: HIP 7.2 crashes in hipStreamEndCapture on such
+    // sibling-to-sibling waits (tools/capture_probe2.hip, flag 1); fork/join through the origin captures fine.
+    for (auto* s : rs) s->lb_pack(i);
+    step("pack", i);
+    bool any = false;
+    for (auto* s : rs)
+      if (s->needs_exchange(i)) {
+        W3D_HIP(hipStreamWaitEvent(gs_, s->ev_packed_, 0));
+        any = true;
+      }
+    if (any) W3D_HIP(hipEventRecord(all_packed_, gs_));
+    for (auto* s : rs) s->lb_pull(i, rs, all_packed_);
+    step("pull", i);
+    for (auto* s : rs)
+      if (s->needs_exchange(i)) W3D_HIP(hipStreamWaitEvent(gs_, s->ev_halo_, 0));
+    if (any) W3D_HIP(hipEventRecord(all_pulled_, gs_));
+    for (auto* s : rs) s->lb_fence(i, all_pulled_);
+    step("fence", i);
+    if (!late)
+      for (auto* s : rs) s->unit_interior(i);
+    step("interior", i);
+  }
+  for (auto* s : rs) s->flush_reduces();
+  step("flush", nu);
+}
+
+// the group stream waits for every stream the ranks used
+void GpuGroup::join() {
+  for (size_t q = 0; q < ranks_.size(); ++q) {
+    GpuSolver* s = ranks_[q].get();
+    W3D_HIP(hipEventRecord(join_[2 * q], s->s0_));
+    W3D_HIP(hipStreamWaitEvent(gs_, join_[2 * q], 0));
+    if (s->xstream() != s->s0_) {
+      W3D_HIP(hipEventRecord(join_[2 * q + 1], s->s1_));
+      W3D_HIP(hipStreamWaitEvent(gs_, join_[2 * q + 1], 0));
+    }
+  }
 }
 
 RunResult GpuGroup::run() {
   std::vector<GpuSolver*> rs;
   for (auto& p : ranks_) rs.push_back(p.get());
   const int K = rs[0]->prob_.K;
+  // capture on the second run (RCCL connects its peers eagerly on the first send/recv, never inside a capture): the
+  // group stream forks into every rank's two streams and joins them back, so the graph holds all ranks' work
+  const bool dbg = std::getenv("W3D_DEBUG") != nullptr;
+  auto trace = [&](const char* what) {
+    if (dbg) {
+      (void)hipDeviceSynchronize();
+      std::fprintf(stderr, "[group] %s: %s\n", what, hipGetErrorString(hipGetLastError()));
+    }
+  };
+  if (graph_ && !exec_ && runs_ >= 1) {
+    hipGraph_t g = nullptr;
+    bool ok = hipStreamBeginCapture(gs_, hipStreamCaptureModeThreadLocal) == hipSuccess;
+    if (dbg) std::fprintf(stderr, "[group] begin capture ok=%d\n", ok ? 1 : 0);
+    if (ok) {
+      try {
+        W3D_HIP(hipEventRecord(fork_, gs_));
+        for (auto* s : rs) {
+          W3D_HIP(hipStreamWaitEvent(s->s0_, fork_, 0));
+          if (s->xstream() != s->s0_) W3D_HIP(hipStreamWaitEvent(s->s1_, fork_, 0));
+        }
+        enqueue();
+        join();
+      } catch (const std::exception& ex) {
+        if (dbg) std::fprintf(stderr, "[group] capture enqueue failed: %s\n", ex.what());
+        ok = false;
+      }
+      const hipError_t e = hipStreamEndCapture(gs_, &g);
+      if (dbg) std::fprintf(stderr, "[group] end capture: %s graph=%p\n", hipGetErrorString(e), (void*)g);
+      ok = ok && e == hipSuccess && g != nullptr;
+    }
+    if (ok) {
+      const hipError_t e = hipGraphInstantiate(&exec_, g, nullptr, nullptr, 0);
+      if (dbg) std::fprintf(stderr, "[group] instantiate: %s\n", hipGetErrorString(e));
+      ok = e == hipSuccess;
+    }
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    if (!ok) {
+      exec_ = nullptr;
+      graph_ = false;
+    }
+  }
   const double t0 = now_s();
-  for (auto* s : rs) {
-    s->phase_init();
-    s->tb_region_ = 0;
-    s->pending_.clear();
+  if (exec_) {
+    W3D_HIP(hipGraphLaunch(exec_, gs_));
+    trace("graph launch");
+  } else {
+    enqueue();
+    join();  // the gathers below run on the group stream
   }
-  const int nu = static_cast<int>(rs[0]->units_.size());
-  const bool late = rs[0]->late_exchange();
-  for (int i = 0; i < nu; ++i) {
-    for (auto* s : rs) s->unit_shell(i);
-    if (late)
-      for (auto* s : rs) s->unit_interior(i);
-    for (auto* s : rs) s->lb_pack(i);
-    for (auto* s : rs) s->lb_pull(i, rs);
-    for (auto* s : rs) s->lb_fence(i, rs);
-    if (!late)
-      for (auto* s : rs) s->unit_interior(i);
-  }
-  for (auto* s : rs) s->flush_reduces();
-  // combine the per-rank error logs in rank order (what the RCCL all-gather does across processes)
+  // per-rank error logs to the host: through ncclAllGather on each rank's communicator (rccl-self; one rank each, so
+  // the gathered log is the rank's own) or straight from errlog_; combined in rank order as the multi-process
+  // all-gather is
   const size_t per = static_cast<size_t>(K + 1);
   std::vector<Partial> all(per * rs.size());
   for (size_t q = 0; q < rs.size(); ++q) {
-    W3D_HIP(hipMemcpyAsync(all.data() + q * per, rs[q]->errlog_, per * sizeof(Partial), hipMemcpyDeviceToHost,
-                           rs[q]->s0_));
+    GpuSolver* s = rs[q];
+    const Partial* src = s->errlog_;
+    if (s->comm_) {
+      W3D_NCCL(ncclAllGather(s->errlog_, s->errall_, 2 * per, ncclFloat64, static_cast<ncclComm_t>(s->comm_->raw()),
+                             gs_));
+      src = s->errall_;
+    }
+    W3D_HIP(hipMemcpyAsync(all.data() + q * per, src, per * sizeof(Partial), hipMemcpyDeviceToHost, gs_));
   }
-  for (auto* s : rs) wait_stream(s->s0_, nullptr, gpu_timeout_s());
+  trace("gathers");
+  wait_stream(gs_, rs[0]->comm_.get(), gpu_timeout_s());
+  for (auto* s : rs)
+    if (s->comm_) s->comm_->check_async();
   RunResult r;
   const double n_int = static_cast<double>(rs[0]->prob_.N - 1);
   for (int n : rs[0]->check_steps()) {
@@ -906,6 +1092,8 @@ RunResult GpuGroup::run() {
     if (!std::isfinite(m) || !std::isfinite(sum)) r.finite = false;
   }
   r.solve_s = now_s() - t0;
+  rs[0]->collect_phases(r);  // (timers: rank 0's phases, as the CLI reports)
+  ++runs_;
   return r;
 }
 

@@ -10,6 +10,8 @@ hip        rccl        native C++ GpuSolver: HIP kernels, C++ step loop, RCCL P2
 hip        torch       Python step loop, HIP kernels, halos over torch.distributed (RCCL, or gloo staged via host)
 hip        loopback    native GpuGroup: all ranks of a decomposition in THIS process on one GPU, device-copy halos
                        (exercises the production multi-rank C++ path on a single GPU; tests)
+hip        rccl-self   native GpuGroup as above, halos moved by the production RCCL ncclSend/ncclRecv calls, each rank
+                       over its own one-rank communicator (RCCL refuses 2 ranks of one communicator on one GPU)
 cpu        native      C++ CpuSolver, OpenMP (the reference's sequential / OpenMP programs), world == 1
 cpu        torch       Python step loop, native OpenMP kernels, halos over torch.distributed gloo (MPI analogue)
 torch      -           plain PyTorch fp64 reference solver (oracle), world == 1
@@ -55,7 +57,8 @@ def _resolve(backend: str, transport: str, world: int) -> tuple[str, str]:
         backend = "hip" if torch.cuda.is_available() else "cpu"
     if transport == "auto":
         transport = {"hip": "rccl", "cpu": "native" if world == 1 else "torch", "torch": "none"}[backend]
-    ok = {("hip", "rccl"), ("hip", "torch"), ("hip", "loopback"), ("cpu", "native"), ("cpu", "torch"),
+    ok = {("hip", "rccl"), ("hip", "torch"), ("hip", "loopback"), ("hip", "rccl-self"), ("cpu", "native"),
+          ("cpu", "torch"),
           ("torch", "none")}
     if (backend, transport) not in ok:
         raise ValueError(f"unsupported backend/transport combination {backend}/{transport}")
@@ -101,14 +104,14 @@ class Solver:
             self.device = torch.device("cuda", dev)
         else:
             self.device = torch.device("cpu")
-        if self.backend == "hip" and self.transport == "loopback":
-            opts = self._options(C, decomp, spec, overlap, False, tiling, temporal, tiling2, init2, tb, tiling_tb)
+        if self.backend == "hip" and self.transport in ("loopback", "rccl-self"):
+            opts = self._options(C, decomp, spec, overlap, graph, tiling, temporal, tiling2, init2, tb, tiling_tb)
             opts.timers, opts.debug_sync, opts.poison_ghosts = timers, debug_sync, poison_ghosts
             if deep_min_planes is not None:
                 opts.deep_min_planes = deep_min_planes
             if tb_min_planes is not None:
                 opts.tb_min_planes = tb_min_planes
-            self._impl = C.GpuGroup(spec.native(), opts, world)
+            self._impl = C.GpuGroup(spec.native(), opts, world, self.transport)
             self.dims = self._impl.dims().as_tuple()
         elif self.backend == "hip" and self.transport == "rccl":
             from .parallel.rccl import make_comm
@@ -182,7 +185,7 @@ class Solver:
         """The whole (N+1)³ field u^K (which=0) / u^{K-1} (which=1) on the CPU (single rank or loopback group)."""
         from .ops.stencil import grid_view
 
-        if self.transport != "loopback":
+        if self.transport not in ("loopback", "rccl-self"):
             if self.world != 1:
                 raise RuntimeError("global_field needs world == 1 or the loopback transport")
             return self.owned_field(which)

@@ -1,0 +1,67 @@
+#!/bin/bash
+# One parametrised GPU-box driver (replaces the round-1 scratch scripts/gpu_*.sh). Every step that touches the GPU runs
+# under its own time limit and the steps are chained with &&: the first failure, fault or timeout ends the call.
+#
+#   scripts/gpu.sh test [pytest -k expr]     pytest -m gpu (one process, per-test timeout) -> gpurun_out/pytest_gpu.log
+#   scripts/gpu.sh bench [bench.py args]     1-GPU bench.py line                            -> gpurun_out/bench.log
+#   scripts/gpu.sh prof [wave3d args]        rocprofv3 kernel trace + stats of the 512^3 CLI solve -> gpurun_out/prof/
+#   scripts/gpu.sh profbench [bench args]    rocprofv3 kernel trace + stats of bench.py     -> gpurun_out/profbench/
+#   scripts/gpu.sh pmc "<counters>" [wave3d args]  one PMC pass (counters of one block budget) -> gpurun_out/pmc/
+#   scripts/gpu.sh cli [wave3d args]         the reference-config CLI run (512 0.001 20 1)   -> gpurun_out/cli.log
+#   scripts/gpu.sh all                       test && cli && bench && profbench
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+what=${1:-all}
+shift || true
+
+run_test() {
+  local k=()
+  [ $# -gt 0 ] && k=(-k "$*")
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread "${k[@]}" \
+    > gpurun_out/pytest_gpu.log 2>&1
+  local rc=$?
+  tail -3 gpurun_out/pytest_gpu.log
+  return $rc
+}
+run_bench() {
+  timeout -k 10 300 python -u bench.py "$@" > gpurun_out/bench.log 2>&1
+  local rc=$?
+  tail -2 gpurun_out/bench.log
+  return $rc
+}
+run_cli() {
+  timeout -k 10 120 ./bin/wave3d 512 0.001 20 1 --repeat 10 --warmup 2 "$@" > gpurun_out/cli.log 2>&1
+  local rc=$?
+  tail -4 gpurun_out/cli.log
+  return $rc
+}
+run_prof() {
+  rm -rf gpurun_out/prof
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
+    ./bin/wave3d 512 0.001 20 1 --repeat 5 --warmup 1 "$@" > gpurun_out/prof.log 2>&1
+}
+run_profbench() {
+  rm -rf gpurun_out/profbench
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profbench -o run -- \
+    python3 bench.py --steps 5 --warmup 2 "$@" > gpurun_out/profbench.log 2>&1
+}
+run_pmc() {
+  local counters=$1
+  shift
+  rm -rf gpurun_out/pmc
+  timeout -s KILL 90 rocprofv3 --pmc $counters --kernel-trace --output-format csv -d gpurun_out/pmc -o run -- \
+    ./bin/wave3d 512 0.001 20 1 --repeat 2 --warmup 1 "$@" > gpurun_out/pmc.log 2>&1
+}
+
+case "$what" in
+  test) run_test "$@" ;;
+  bench) run_bench "$@" ;;
+  cli) run_cli "$@" ;;
+  prof) run_prof "$@" ;;
+  profbench) run_profbench "$@" ;;
+  pmc) run_pmc "$@" ;;
+  all) run_test && run_cli && run_bench && run_profbench ;;
+  *) echo "unknown step $what" >&2; exit 2 ;;
+esac

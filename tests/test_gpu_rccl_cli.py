@@ -1,0 +1,75 @@
+"""The production RCCL calls on one GPU, captured in a hipGraph, through the native runtime (bin/wave3d).
+
+``bin/wave3d ... --group P`` runs all P ranks of a decomposition in one process on one GPU with the rccl-self
+transport: every rank owns a one-rank RCCL communicator and moves each halo message with ncclGroupStart / ncclSend /
+ncclRecv / ncclGroupEnd on its high-priority side stream, joined to the compute stream with the same events as the
+multi-process path; the error logs go through ncclAllGather. The binary runs on the system ROCm 7.2 runtime (HIP +
+RCCL), which captures these multi-stream schedules, so solve 1 runs eagerly (RCCL connects), solve 2 is captured and the
+later ones replay the graph. The dumped fields must be BIT-identical to the single-GPU solve and the printed error lines
+identical (the reference's 1-GPU log == 2-GPU log property, report.pdf p.15-16).
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from mpi_cuda_amd import ProblemSpec
+from mpi_cuda_amd.solver import Solver
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "bin", "wave3d")
+
+
+def _single(N, K, check_every=2):
+    s = Solver(ProblemSpec(N=N, tau=1e-3, K=K, check_every=check_every), backend="hip", device=0)
+    r = s.run()
+    return r, s.global_field(0).numpy()
+
+
+def _group(tmp_path, N, K, world, decomp, transport="rccl-self", extra=()):
+    prefix = str(tmp_path / "f")
+    js = str(tmp_path / "g.json")
+    cmd = [CLI, str(N), "0.001", str(K), "1", "--group", str(world), "--group-transport", transport, "--decomp",
+           decomp, "--warmup", "2", "--repeat", "2", "--dump", prefix, "--json", js, "--quiet", *extra]
+    out = subprocess.run(cmd, check=True, timeout=120, capture_output=True, text=True).stdout
+    meta = json.loads(open(js).read())
+    field = np.zeros((N + 1,) * 3)
+    for r in range(world):
+        m = json.loads(open(f"{prefix}.rank{r}.json").read())
+        nx, ny, nz = m["shape"]
+        x0, y0, z0 = m["offset"]
+        field[x0:x0 + nx, y0:y0 + ny, z0:z0 + nz] = np.fromfile(f"{prefix}.rank{r}.bin").reshape(nx, ny, nz)
+    return meta, field, out
+
+
+@pytest.mark.parametrize("world,decomp,K", [(2, "slab", 20), (4, "slab", 20), (8, "slab", 9), (3, "slab", 11),
+                                            (4, "2x2x1", 9), (8, "2x2x2", 10), (6, "1x2x3", 9)])
+def test_rccl_self_graph_bitexact(gpu, tmp_path, world, decomp, K):
+    N = 70
+    r1, f1 = _single(N, K)
+    meta, f, _ = _group(tmp_path, N, K, world, decomp)
+    assert meta["transport"] == "rccl-self" and meta["rccl_comms"] == world
+    assert meta["graph"] is True  # captured (ROCm 7.2 runtime), RCCL kernels inside the graph
+    assert np.array_equal(f, f1)
+    assert [s[0] for s in meta["steps"]] == r1.steps
+    for (n, m, e), m1, e1 in zip(meta["steps"], r1.max_err, r1.rms_err):
+        assert m == pytest.approx(m1, rel=1e-9) and e == pytest.approx(e1, rel=1e-9)
+
+
+@pytest.mark.parametrize("extra", [("--no-overlap",), ("--poison-ghosts",), ("--temporal", "1"),
+                                   ("--no-tb", "--deep-min-planes", "3")])
+def test_rccl_self_graph_schedules(gpu, tmp_path, extra):
+    """Late-exchange deep-tb (no overlap), NaN-poisoned ghosts, single steps and two-step deep halos, captured."""
+    N, K = 66, 10
+    _, f1 = _single(N, K)
+    meta, f, _ = _group(tmp_path, N, K, 3, "slab", extra=extra)
+    assert meta["graph"] is True and np.array_equal(f, f1)
+
+
+def test_loopback_graph_bitexact(gpu, tmp_path):
+    _, f1 = _single(70, 9)
+    meta, f, _ = _group(tmp_path, 70, 9, 4, "2x2x1", transport="loopback")
+    assert meta["graph"] is True and meta["rccl_comms"] == 0 and np.array_equal(f, f1)

@@ -109,34 +109,41 @@ inline int neighbor_rank(const Dims& d, int rank, int axis, int side) {
   return coords_rank(d, c[0], c[1], c[2]);
 }
 
-// Local storage of one rank's box with a ghost layer of width 1 on every side.
-//   offset(ix,iy,iz) = (ix+1)·plane + (iy+1)·pitch + (iz+1+zs),  ix ∈ [-1,nx], iy ∈ [-1,ny], iz ∈ [-1,nz]
+// Local storage of one rank's box with xg / yg / zg ghost layers on the two sides of each axis (1 for single steps; S
+// on the split axes of ranks that run S-step passes with S-deep halos):
+//   offset(ix,iy,iz) = (ix+xg)·plane + (iy+yg)·pitch + (iz+zg+zs),  ix ∈ [-xg,nx+xg), iy ∈ [-yg,ny+yg), iz ∈ [-zg,nz+zg)
 // zs ∈ [0,15] shifts the row so that the first updated z node sits on a 128-byte line boundary: kernels move nodes
 // in 16-byte pairs (dwordx4) and a wave's 64 pairs then cover exactly eight whole 128-B lines. pitch is a multiple of
-// 16 doubles (128 B, so every row starts on a line) and keeps at least one spare pair after the ghost node so the pair
-// holding a row's right neighbour never straddles into the next row.
+// 16 doubles (128 B, so every row starts on a line) and keeps at least two spare doubles after the last ghost node so
+// the pair holding a row's right neighbour never straddles into the next row. The last of them in the last row of every
+// plane is never written by anything but zeros (zero_off): kernels load it for positions outside the global interior.
 struct Layout {
   i64 N = 0;
-  i64 xg = 1;                     // ghost planes on each x side (2 for the deep-halo temporally blocked slab path)
+  i64 xg = 1, yg = 1, zg = 1;     // ghost layers on each side of x / y / z
   i64 nx = 0, ny = 0, nz = 0;     // owned nodes
   i64 gx0 = 0, gy0 = 0, gz0 = 0;  // global index of local node 0
   i64 zs = 0, pitch = 0, plane = 0, total = 0;
   // Local index range of the nodes this rank updates: owned ∩ global interior [1, N-1].
   i64 cx0 = 0, cx1 = 0, cy0 = 0, cy1 = 0, cz0 = 0, cz1 = 0;
 
-  W3D_HD i64 off(i64 ix, i64 iy, i64 iz) const { return (ix + xg) * plane + (iy + 1) * pitch + (iz + 1 + zs); }
-  // Kernels address plane x at (x+1)·plane from their base pointer; base = field + kbase() accounts for extra ghosts.
-  W3D_HD i64 kbase() const { return (xg - 1) * plane; }
+  W3D_HD i64 off(i64 ix, i64 iy, i64 iz) const { return (ix + xg) * plane + (iy + yg) * pitch + (iz + zg + zs); }
+  // Kernels address local node (x,y,z) at (x+1)·plane + (y+1)·pitch + (z+1+zs) from their base pointer;
+  // base = field + kbase() accounts for the ghost depths.
+  W3D_HD i64 kbase() const { return (xg - 1) * plane + (yg - 1) * pitch + (zg - 1); }
   // first element of plane ix (its ghost rows and row padding included)
   W3D_HD i64 plane_off(i64 ix) const { return (ix + xg) * plane; }
+  // offset from a plane's first element of a slot that always holds 0 (the last padding double of its last row)
+  W3D_HD i64 zero_off() const { return plane - 1; }
   W3D_HD i64 bytes() const { return total * static_cast<i64>(sizeof(double)); }
   W3D_HD bool has_work() const { return cx1 > cx0 && cy1 > cy0 && cz1 > cz0; }
 };
 
-inline Layout make_layout(const Problem& p, const Box& b, i64 pitch_align = 16, i64 xg = 1) {
+inline Layout make_layout(const Problem& p, const Box& b, i64 pitch_align = 16, i64 xg = 1, i64 yg = 1, i64 zg = 1) {
   Layout l;
   l.N = p.N;
   l.xg = xg;
+  l.yg = yg;
+  l.zg = zg;
   l.nx = b.nx();
   l.ny = b.ny();
   l.nz = b.nz();
@@ -151,9 +158,9 @@ inline Layout make_layout(const Problem& p, const Box& b, i64 pitch_align = 16, 
   l.cy1 = imax(l.cy0, hi(b.y0, l.ny));
   l.cz0 = lo(b.z0);
   l.cz1 = imax(l.cz0, hi(b.z0, l.nz));
-  l.zs = (16 - (l.cz0 + 1) % 16) % 16;
-  l.pitch = round_up(l.nz + 2 + l.zs + 2, pitch_align);
-  l.plane = (l.ny + 2) * l.pitch;
+  l.zs = (16 - (l.cz0 + l.zg) % 16) % 16;
+  l.pitch = round_up(l.nz + 2 * l.zg + l.zs + 2, pitch_align);
+  l.plane = (l.ny + 2 * l.yg) * l.pitch;
   l.total = (l.nx + 2 * l.xg) * l.plane;
   return l;
 }

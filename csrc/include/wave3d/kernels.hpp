@@ -13,6 +13,7 @@
 
 #include "wave3d/cpu.hpp"
 #include "wave3d/decomp.hpp"
+#include "wave3d/deep_plan.hpp"
 #include "wave3d/problem.hpp"
 
 namespace wave3d {
@@ -69,7 +70,7 @@ void launch_leapfrog2(const Layout& l, const Coeffs& c, const double* prev, cons
                       const Leapfrog2Tiling& t, hipStream_t stream, i64 sx0 = 1, i64 sx1 = 0);
 
 // Deep temporal blocking: S = 2..4 leapfrog steps in one pass, all intermediate levels in LDS (32 × 32 (y,z) tiles
-// marching in x, one workgroup per CU). Reads u^{n−1}, u^n; writes u^{n+S−1} into out1 and u^{n+S} into out2: 32/S
+// marching in x (or in x chunks when the tiles alone do not fill the GPU), one workgroup per CU). Reads u^{n−1}, u^n; writes u^{n+S−1} into out1 and u^{n+S} into out2: 32/S
 // compulsory bytes per node-step. Same preconditions as launch_leapfrog2 with S−1 stage-1 planes beyond the box.
 // Error check of u^{n+k} when bit k−1 of `check_mask` is set (ct[k−1] = its time factor); stage k's partials go to
 // partials + (k−1)·level_stride (0: leapfrog_tb_partials(), the launch's block count). analytic_start: the pass starts at n = 1 from u⁰ = φ and u¹ computed in
@@ -79,15 +80,21 @@ struct LeapfrogTbTiling {
   int threads = 1024;     // workgroup size (512 or 1024; 1024 measured faster at every S)
   bool xcd_remap = true;  // (stores are always non-temporal: measured faster at every S)
   bool xcd_blocks = false; // with xcd_remap: each XCD owns a square-ish tile block, not two-row strips (measured: no gain)
+  int target_blocks = 256; // fewer (y,z) tiles than this: split x into chunks (one workgroup per CU at 1 WG/CU)
+  int min_chunk = 16;      // ... of at least this many planes (each chunk recomputes S−1 planes on both sides)
 };
+// Stage-real ranges of an LDS pass: per axis, where the intermediate levels hold real values (S−1 nodes into the
+// S-deep ghosts towards neighbouring ranks); lo > hi: the axis default (x: compute box, y/z: no restriction).
+inline LBox tb_default_real() { return LBox{1, 0, 1, 0, 1, 0}; }
 // Raise the dynamic-LDS limit of every instantiation (call before capturing launches into a graph).
 void leapfrog_tb_prepare();
 size_t leapfrog_tb_lds_bytes(int stages);
 int leapfrog_tb_partials(const Layout& l, const LBox& box, const LeapfrogTbTiling& t);
 void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
                         double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
-                        Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, i64 sx0 = 1, i64 sx1 = 0,
-                        bool analytic_start = false, int level_stride = 0);
+                        Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream,
+                        const LBox& real = tb_default_real(), bool analytic_start = false, int level_stride = 0,
+                        int grid_blocks = 0);
 
 // Error of a stored field vs φ·ct over `box` (step 1 / standalone check). Writes leapfrog-compatible partials and
 // returns how many.
@@ -104,6 +111,26 @@ struct ReduceJob {
   Partial* out;
 };
 void launch_reduce_batch(const ReduceJob* jobs, int njobs, hipStream_t stream);
+
+// S-deep exchange regions (deep_plan.hpp) <-> contiguous staging buffers. The job table is built once per plan and kept
+// in device memory. mode 0: pack the send regions of u^{n+S} (u_s) and u^{n+S−1} (u_s1) into buf; 1: unpack buf into
+// their receive (ghost) regions; 2: fill the receive regions with NaN (--poison-ghosts).
+struct BoxJob {
+  i64 buf;        // offset of the region in the staging buffer
+  int count;      // nodes in the region
+  int field;      // 0: u_s, 1: u_s1
+  int x0, y0, z0; // first node (local)
+  int ny, nz;     // extents of the region in y and z
+  int blk0;       // first workgroup of this job
+};
+struct BoxCopyTable {
+  BoxJob* jobs = nullptr;  // device
+  int njobs = 0, nblocks = 0;
+};
+BoxCopyTable make_box_copy_table(const DeepPlan& plan, bool recv_side);
+void free_box_copy_table(BoxCopyTable& t);
+void launch_box_copy(const Layout& l, const BoxCopyTable& t, int mode, double* u_s, double* u_s1, double* buf,
+                     hipStream_t stream);
 
 // Pack all strided faces of `plan` from `u` into `buf`, or unpack `buf` into the ghost layers of `u`.
 void launch_pack(const Layout& l, const HaloPlan& plan, const double* u, double* buf, hipStream_t stream);

@@ -143,6 +143,9 @@ class GpuSolver {
   // then moved by a self send/recv pair on THIS rank's communicator, sending the peer's matching face (already packed
   // by the peer) into this rank's receive region — the same RCCL calls, stream and events as the multi-process path.
   void exchange(hipStream_t st, const std::vector<GpuSolver*>* pull = nullptr);
+  bool packs() const;               // this schedule's messages go through the staging buffers
+  void pack_halo(hipStream_t st);   // faces (single steps) / S-deep regions (block passes) → send_buf_
+  void unpack_halo(hipStream_t st); // recv_buf_ → ghost layers
   void gather_errors(RunResult& r);
   // Schedule: a solve is phase_init() followed by units; a unit advances one step (in place over u^{n−1}) or 2..4
   // (a fused pass into the two free buffers). Multi-rank units run shell -> exchange -> interior.
@@ -204,6 +207,12 @@ class GpuSolver {
   std::vector<LBox> dshell_;      // deep mode: output x-slabs next to neighbours (shell) ...
   LBox dint_;                     // ... and the rest (interior)
   i64 sx0_ = 0, sx1_ = 0;         // deep mode: stage-1 x range (one ghost plane beyond each neighbour face)
+  LBox sreal_;                    // deep-tb: stage-real ranges per axis (temporal − 1 nodes into each neighbour's ghosts)
+  bool block_tb_ = false;         // deep-tb on a 3-D block decomposition (S-deep ghosts on every split axis)
+  DeepPlan deep_[5];              // block_tb_: exchange plan before a pass of s steps (index s = 2..temporal)
+  BoxCopyTable pack_tab_[5], unpack_tab_[5];  // ... and its device job tables (send / receive regions)
+  i64 deep_max_ = 0;              // largest staging buffer of those plans (doubles)
+  int deep_s_ = 2;                // depth of the exchange being issued
   std::vector<int> n_dshell_;     // partials per deep shell launch
   int n_dint_ = 0;
   int prev_buf_ = 1;             // buffer index holding u^{K−1} after a solve

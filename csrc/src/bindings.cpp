@@ -143,6 +143,9 @@ PYBIND11_MODULE(_C, m) {
   py::class_<Layout>(m, "Layout")
       .def_readonly("N", &Layout::N)
       .def_readonly("xg", &Layout::xg)
+      .def_readonly("yg", &Layout::yg)
+      .def_readonly("zg", &Layout::zg)
+      .def("zero_off", &Layout::zero_off)
       .def_readonly("nx", &Layout::nx)
       .def_readonly("ny", &Layout::ny)
       .def_readonly("nz", &Layout::nz)
@@ -161,7 +164,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("cz1", &Layout::cz1)
       .def("off", [](const Layout& l, i64 x, i64 y, i64 z) { return l.off(x, y, z); });
   m.def("make_layout", &make_layout, py::arg("problem"), py::arg("box"), py::arg("pitch_align") = 16,
-        py::arg("xg") = 1);
+        py::arg("xg") = 1, py::arg("yg") = 1, py::arg("zg") = 1);
 
   py::class_<Face>(m, "Face")
       .def_readonly("axis", &Face::axis)
@@ -179,6 +182,23 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("packed_doubles", &HaloPlan::packed_doubles);
   m.def("make_halo_plan", &make_halo_plan);
 
+  py::class_<DeepPart>(m, "DeepPart")
+      .def_readonly("field", &DeepPart::field)
+      .def_readonly("send", &DeepPart::send)
+      .def_readonly("recv", &DeepPart::recv)
+      .def_readonly("off", &DeepPart::off);
+  py::class_<DeepPeer>(m, "DeepPeer")
+      .def_readonly("peer", &DeepPeer::peer)
+      .def_readonly("dir", &DeepPeer::dir)
+      .def_readonly("count", &DeepPeer::count)
+      .def_readonly("buf_off", &DeepPeer::buf_off)
+      .def_readonly("parts", &DeepPeer::parts);
+  py::class_<DeepPlan>(m, "DeepPlan")
+      .def_readonly("s", &DeepPlan::s)
+      .def_readonly("peers", &DeepPlan::peers)
+      .def_readonly("total", &DeepPlan::total);
+  m.def("make_deep_plan", &make_deep_plan, py::arg("layout"), py::arg("dims"), py::arg("rank"), py::arg("s"));
+
   py::class_<LBox>(m, "LBox")
       .def(py::init([](i64 x0, i64 x1, i64 y0, i64 y1, i64 z0, i64 z1) { return LBox{x0, x1, y0, y1, z0, z1}; }))
       .def_readwrite("x0", &LBox::x0)
@@ -188,7 +208,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("z0", &LBox::z0)
       .def_readwrite("z1", &LBox::z1)
       .def("empty", &LBox::empty)
-      .def("count", &LBox::count);
+      .def("count", &LBox::count)
+      .def("as_tuple", [](const LBox& b) { return py::make_tuple(b.x0, b.x1, b.y0, b.y1, b.z0, b.z1); });
   m.def("compute_box", &compute_box);
 
   // ---------------- CPU kernels ----------------
@@ -343,22 +364,24 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("stages", &LeapfrogTbTiling::stages)
       .def_readwrite("threads", &LeapfrogTbTiling::threads)
       .def_readwrite("xcd_remap", &LeapfrogTbTiling::xcd_remap)
-      .def_readwrite("xcd_blocks", &LeapfrogTbTiling::xcd_blocks);
+      .def_readwrite("xcd_blocks", &LeapfrogTbTiling::xcd_blocks)
+      .def_readwrite("target_blocks", &LeapfrogTbTiling::target_blocks)
+      .def_readwrite("min_chunk", &LeapfrogTbTiling::min_chunk);
   m.def("gpu_leapfrog_tb_lds_bytes", &leapfrog_tb_lds_bytes);
   m.def("gpu_leapfrog_tb_partials", &leapfrog_tb_partials);
   m.def("gpu_leapfrog_tb",
         [](const Layout& l, const Coeffs& c, std::uintptr_t prev, std::uintptr_t cur, std::uintptr_t out1,
            std::uintptr_t out2, const LBox& box, std::uintptr_t s, std::vector<double> ct, int check_mask,
-           std::uintptr_t partials, const LeapfrogTbTiling& t, std::uintptr_t stream, i64 sx0, i64 sx1,
+           std::uintptr_t partials, const LeapfrogTbTiling& t, std::uintptr_t stream, const LBox& real,
            bool analytic_start) {
           ct.resize(4, 0.0);
           launch_leapfrog_tb(l, c, dptr<const double>(prev), dptr<const double>(cur), dptr<double>(out1),
                              dptr<double>(out2), box, dptr<const double>(s) + 1, ct.data(), check_mask,
-                             dptr<Partial>(partials), t, sptr(stream), sx0, sx1, analytic_start);
+                             dptr<Partial>(partials), t, sptr(stream), real, analytic_start);
         },
         py::arg("layout"), py::arg("coeffs"), py::arg("prev"), py::arg("cur"), py::arg("out1"), py::arg("out2"),
         py::arg("box"), py::arg("s"), py::arg("ct"), py::arg("check_mask"), py::arg("partials"), py::arg("tiling"),
-        py::arg("stream"), py::arg("sx0") = 1, py::arg("sx1") = 0, py::arg("analytic_start") = false);
+        py::arg("stream"), py::arg("real") = tb_default_real(), py::arg("analytic_start") = false);
   m.def("gpu_error_blocks", &error_blocks);
   m.def("gpu_error", [](const Layout& l, std::uintptr_t u, const LBox& b, std::uintptr_t s, double ct,
                         std::uintptr_t partials, std::uintptr_t stream) {

@@ -1,4 +1,5 @@
-// Halo pack / unpack kernels for the strided (y and z) faces of the 3-D block decomposition (reference kernel K6,
+// Halo pack / unpack kernels: the strided (y and z) faces of the single-step 3-D block decomposition (k_pack) and the
+// S-deep face/edge/corner regions of the multi-step block passes (k_box_copy) (reference kernel K6,
 // SURVEY.md §2.5; the reference staged faces through the host, report.pdf p.16 §4.4 H2D/D2H column).
 // x faces are whole contiguous planes and go to RCCL straight from the field: no kernel at all.
 //
@@ -79,7 +80,113 @@ void launch(const Layout& l, const HaloPlan& plan, double* field, double* buf, h
   if (e != hipSuccess) fail(std::string("pack/unpack launch: ") + hipGetErrorString(e));
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// k_box_copy: general box <-> staging-buffer copies of the S-deep exchanges (deep_plan.hpp). One launch moves every
+// region of every peer message (both fields); the job table lives in device memory (built once per plan, so a
+// captured graph holds only the pointers). Element e of a box runs in C order (x, y, z): consecutive lanes read
+// consecutive z nodes of a row — whole 128-B lines for x and y faces, the w ≤ 4 contiguous nodes of each row for z
+// faces (what the layout offers) — and the staging side is written fully contiguous.
+// ---------------------------------------------------------------------------------------------------------------
+constexpr int kBoxThreads = 256, kBoxPer = 4;  // elements per thread
+
+struct BoxCopyParams {
+  double* f[2];
+  double* buf;
+  const BoxJob* jobs;
+  int njobs;
+  i64 plane, pitch, zs;
+};
+
+template <int MODE>  // 0 pack, 1 unpack, 2 poison (NaN into the receive regions)
+__global__ __launch_bounds__(kBoxThreads) void k_box_copy(const BoxCopyParams p) {
+  const int b = static_cast<int>(blockIdx.x);
+  int j = 0;
+  while (j + 1 < p.njobs && p.jobs[j + 1].blk0 <= b) ++j;  // (≤ 52 jobs, wave-uniform scalar loads)
+  const BoxJob jb = p.jobs[j];
+  double* f = p.f[jb.field];
+  const int base = (b - jb.blk0) * (kBoxThreads * kBoxPer) + static_cast<int>(threadIdx.x);
+#pragma unroll
+  for (int k = 0; k < kBoxPer; ++k) {
+    const int e = base + k * kBoxThreads;
+    if (e >= jb.count) break;
+    const int t = e / jb.nz;
+    const int z = jb.z0 + (e - t * jb.nz);
+    const int yy = t / jb.ny;
+    const int y = jb.y0 + (t - yy * jb.ny);
+    const int x = jb.x0 + yy;
+    const i64 o = static_cast<i64>(x + 1) * p.plane + static_cast<i64>(y + 1) * p.pitch + (z + 1 + p.zs);
+    if constexpr (MODE == 0)
+      p.buf[jb.buf + e] = f[o];
+    else if constexpr (MODE == 1)
+      f[o] = p.buf[jb.buf + e];
+    else
+      f[o] = __builtin_nan("");
+  }
+}
+
 }  // namespace
+
+BoxCopyTable make_box_copy_table(const DeepPlan& plan, bool recv_side) {
+  std::vector<BoxJob> jobs;
+  int blk = 0;
+  for (const DeepPeer& q : plan.peers)
+    for (const DeepPart& part : q.parts) {
+      const LBox& b = recv_side ? part.recv : part.send;
+      const i64 cnt = b.count();
+      if (cnt == 0) continue;
+      W3D_REQUIRE(cnt < (1ll << 31) - kBoxThreads * kBoxPer, "box copy: region too large for 32-bit indexing");
+      BoxJob jb;
+      jb.buf = q.buf_off + part.off;
+      jb.count = static_cast<int>(cnt);
+      jb.field = part.field;
+      jb.x0 = static_cast<int>(b.x0);
+      jb.y0 = static_cast<int>(b.y0);
+      jb.z0 = static_cast<int>(b.z0);
+      jb.ny = static_cast<int>(b.y1 - b.y0);
+      jb.nz = static_cast<int>(b.z1 - b.z0);
+      jb.blk0 = blk;
+      blk += static_cast<int>(ceil_div(cnt, kBoxThreads * kBoxPer));
+      jobs.push_back(jb);
+    }
+  BoxCopyTable t;
+  t.njobs = static_cast<int>(jobs.size());
+  t.nblocks = blk;
+  if (!jobs.empty()) {
+    hipError_t e = hipMalloc(&t.jobs, jobs.size() * sizeof(BoxJob));
+    if (e == hipSuccess) e = hipMemcpy(t.jobs, jobs.data(), jobs.size() * sizeof(BoxJob), hipMemcpyHostToDevice);
+    if (e != hipSuccess) fail(std::string("box copy table: ") + hipGetErrorString(e));
+  }
+  return t;
+}
+
+void free_box_copy_table(BoxCopyTable& t) {
+  if (t.jobs) (void)hipFree(t.jobs);
+  t.jobs = nullptr;
+  t.njobs = t.nblocks = 0;
+}
+
+void launch_box_copy(const Layout& l, const BoxCopyTable& t, int mode, double* u_s, double* u_s1, double* buf,
+                     hipStream_t st) {
+  if (t.njobs == 0) return;
+  BoxCopyParams p{};
+  p.f[0] = u_s + l.kbase();
+  p.f[1] = u_s1 + l.kbase();
+  p.buf = buf;
+  p.jobs = t.jobs;
+  p.njobs = t.njobs;
+  p.plane = l.plane;
+  p.pitch = l.pitch;
+  p.zs = l.zs;
+  const dim3 grid(static_cast<unsigned>(t.nblocks));
+  if (mode == 0)
+    hipLaunchKernelGGL(k_box_copy<0>, grid, dim3(kBoxThreads), 0, st, p);
+  else if (mode == 1)
+    hipLaunchKernelGGL(k_box_copy<1>, grid, dim3(kBoxThreads), 0, st, p);
+  else
+    hipLaunchKernelGGL(k_box_copy<2>, grid, dim3(kBoxThreads), 0, st, p);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) fail(std::string("box copy launch: ") + hipGetErrorString(e));
+}
 
 void launch_pack(const Layout& l, const HaloPlan& plan, const double* u, double* buf, hipStream_t stream) {
   launch<true>(l, plan, const_cast<double*>(u), buf, stream);

@@ -193,14 +193,14 @@ Init2Params make_params(const Layout& l, const Coeffs& c) {
   p.gy0 = l.gy0;
   p.gz0 = l.gz0;
   p.zs = l.zs;
-  // written box: local indices in [−1, n] whose global index is interior
+  // written box: local indices in [−g, n+g) (g = the axis's ghost depth) whose global index is interior
   auto lo = [&](i64 g0, i64 gw) { return imax(-gw, 1 - g0); };
   auto hi = [&](i64 g0, i64 n, i64 gw) { return imin(n + gw, l.N - g0); };
   p.x0 = lo(l.gx0, l.xg);
   p.x1 = imax(p.x0, hi(l.gx0, l.nx, l.xg));
-  p.y0 = lo(l.gy0, 1);
-  p.y1 = imax(p.y0, hi(l.gy0, l.ny, 1));
-  const i64 z0 = lo(l.gz0, 1), z1 = imax(z0, hi(l.gz0, l.nz, 1));
+  p.y0 = lo(l.gy0, l.yg);
+  p.y1 = imax(p.y0, hi(l.gy0, l.ny, l.yg));
+  const i64 z0 = lo(l.gz0, l.zg), z1 = imax(z0, hi(l.gz0, l.nz, l.zg));
   p.zo0 = z0 + 1 + l.zs;
   p.zo1 = z1 + 1 + l.zs;
   p.cx0 = l.cx0;

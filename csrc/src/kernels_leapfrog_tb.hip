@@ -14,10 +14,13 @@
 //   * u^n is prefetched two planes ahead (global → register queue; the halo ring of the tile → two ring registers),
 //     u^{n−1} one plane ahead straight into registers (it is only ever the "old" level of the thread's own nodes);
 //   * stages S−1 and S store the tile (u^{n+S−1}, u^{n+S}): 2 reads + 2 writes per node per pass = 32/S B/node-step;
-//   * (y,z) positions outside the global interior load the boundary node (y,z) = (0,0) of their plane instead, which
-//     is 0 in every buffer on every init path (φ = 0 on it: sin-table boundary zero; the updates never write it), so
-//     no select follows a load and its wait is deferred to the first use; planes beyond the boundary only feed stage
-//     values outside the interior, which are forced to 0 like every stage output there;
+//   * (y,z) positions outside the global interior, outside the rank's allocation, or (thread-owned positions) outside
+//     the range where stage values are real, load the plane's zero slot instead (Layout::zero_off, a padding double
+//     that only ever holds 0), so no select follows a load and its wait is deferred to the first use; such positions
+//     only feed stage values that no owned output reads, forced to 0 like every stage output outside the real range;
+//   * 3-D block ranks (S-deep ghosts on the split y/z axes too) pass their real y/z ranges like the x one; small
+//     boxes split x into chunks (each workgroup marches one chunk, recomputing S−1 planes on each side) so that a
+//     launch still fills the 256 CUs;
 //   * any subset of the S new levels can carry the fused error check (per-stage partials); the check's s_x·s_y row
 //     factor is tabulated once per plane (row_tables) and each position's s_z factor sits in a register;
 //   * the analytic-start variant (INIT) reads nothing: a φ stage computes u⁰ = φ once per node and plane into an extra
@@ -60,8 +63,13 @@ struct TbParams {
   Partial* partials;   // stage k's block of nblocks partials at (k−1)·lstride (checked stages only)
   i64 plane, pitch, zs;
   int x0, x1;          // output x range (local)
+  int xlen, nxc;       // x chunk length and chunk count (block c marches [x0 + c·xlen, min(x1, x0 + (c+1)·xlen)))
   int sx0, sx1;        // x range where stage outputs are real (outside: Dirichlet 0)
   int ax0, ax1;        // allocated x range (local planes that may be read)
+  int sy0, sy1, sz0, sz1;  // y / z ranges where stage outputs are real (3-D block ranks; whole planes: everything)
+  int ay0, ay1, az0, az1;  // allocated y / z ranges (ghosts included)
+  int zero_off;            // in-plane offset of the zero slot (Layout::zero_off)
+  int yg, zg;              // y / z ghost depths (in-plane offsets count from the plane start)
   int N, gx0, gy0, gz0;
   int y0, y1, z0, z1;  // output (y, z) range (local)
   double ihx2, ihy2, ihz2, tau2, half_tau2;
@@ -106,18 +114,25 @@ constexpr int tb_nx_table(int nx_box) {
 // accumulators or check code (registers: the S = 4 kernel sits at the 128-VGPR limit of 4 waves per SIMD).
 // INIT: analytic start at n = 1 — u^{n−1} = u⁰ = φ and u^n = u¹ = u⁰ + τ²/2·Δ_h u⁰ are computed from the sin tables
 // (k_init_first's formulas and operation order) instead of loaded: the pass reads nothing from HBM.
-template <int S, int T, int NT, int CM, bool INIT>
+// CH: x-chunked launch (small boxes). Without it the block's x range is the kernel argument itself, which the compiler
+// re-reads instead of keeping live (measured: a computed range costs the S = 4 kernel 5 % in extra spills).
+template <int S, int T, int NT, int CM, bool INIT, bool CH>
 __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
   using G = TbGeom<S, T, NT>;
   constexpr int Q = G::Q, QR = G::QR, H1 = G::H1, W0 = G::W0, PLP = G::PLP;
   constexpr int kOwn = 1 << 30;   // gof flag: tile node inside the output box
-  constexpr int kReal = 1 << 29;  // gof flag: node inside the global interior
-  constexpr int kOff = kReal - 1;  // gof bits of the in-plane offset
+  constexpr int kReal = 1 << 29;  // gof flag: stage values are real at this node (interior ∩ stage-real range)
+  constexpr int kLd = 1 << 28;    // gof flag: node inside the global interior and the allocation (loaded)
+  constexpr int kOff = kLd - 1;   // gof bits of the in-plane offset
   extern __shared__ double lds[];
   const int tid = static_cast<int>(threadIdx.x);
   int blk = static_cast<int>(blockIdx.x);
   if (p.xcd_remap) blk = (blk & 7) * (p.nblocks >> 3) + (blk >> 3);
-  const bool active = blk < p.nty * p.ntz;
+  const int ntiles = p.nty * p.ntz;
+  const bool active = blk < ntiles * (CH ? p.nxc : 1);
+  // chunk-major: consecutive blocks (one XCD after the remap) are neighbouring tiles of one x chunk
+  const int chunk = (CH && active) ? blk / ntiles : 0;
+  if constexpr (CH) blk -= chunk * ntiles;
   int tzi = active ? blk % p.ntz : 0, tyi = active ? blk / p.ntz : 0;
   if (p.bby > 0) {  // XCD x (= blk / per after the remap) owns block x of the tile grid: halo re-reads stay in its L2
     const int per = p.bby * p.bbz, x = blk / per, w = blk - x * per, nbz = p.ntz / p.bbz;
@@ -125,11 +140,16 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     tzi = (x - (x / nbz) * nbz) * p.bbz + (w - (w / p.bbz) * p.bbz);
   }
   const int ty0 = p.y0 + tyi * T, tz0 = p.z0 + tzi * T;
+  const int x0 = CH ? p.x0 + chunk * p.xlen : p.x0;  // this block's output x range
+  const int x1 = CH ? imin(p.x1, x0 + p.xlen) : p.x1;
   const int N = p.N;
   const i64 P = p.plane;
-  const int R = static_cast<int>(p.pitch), zs1 = static_cast<int>(p.zs) + 1;
+  // in-plane offsets count from the plane's first element (always ≥ 0, also for the y/z ghosts of block ranks):
+  // node (y, z) at (y + yg)·pitch + z + zg + zs; the field pointers are offset by (xg − 1) planes only
+  const int R = static_cast<int>(p.pitch), ya = p.yg, za = p.zg + static_cast<int>(p.zs);
   const double tau2 = p.tau2;  // = τ²/h² (the coefficient of d2sum)
   auto inside = [&](int g) { return static_cast<unsigned>(g - 1) < static_cast<unsigned>(N - 1); };
+  auto in_rng = [](int v, int lo, int hi) { return static_cast<unsigned>(v - lo) < static_cast<unsigned>(hi - lo); };
 
   double emax[S], esum[S];
 #pragma unroll
@@ -137,8 +157,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
 
   if (active) {
     // ---- per-thread descriptors of the owned positions (stage-1 region coordinates a, b ∈ [0, H1))
-    // zero node: (y, z) = (0, 0), a global boundary node for whole-plane ranks (gy0 = gz0 = 0)
-    const int zero_off = R + zs1;
+    const int zero_off = p.zero_off;
     int lid[Q];   // LDS index (u^n-region coordinates a+1, b+1); the pad's dummy node for lanes without a position
     int gof[Q];   // in-plane offset to load (zero node outside the interior) | kReal | kOwn
 #pragma unroll
@@ -147,10 +166,14 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       const int a = idx / H1, b = idx - (idx / H1) * H1;
       const int y = ty0 - (S - 1) + a, z = tz0 - (S - 1) + b;
       const bool valid = idx < G::NP;
-      const bool real = valid && inside(p.gy0 + y) && inside(p.gz0 + z);
+      // u^n / u^{n−1} are loaded wherever the rank holds them (its neighbours' ghost values included); the stage
+      // values are real only in the stage-real range (S−1 into the ghosts)
+      const bool ld = valid && inside(p.gy0 + y) && inside(p.gz0 + z) && in_rng(y, p.ay0, p.ay1) &&
+                      in_rng(z, p.az0, p.az1);
+      const bool real = ld && in_rng(y, p.sy0, p.sy1) && in_rng(z, p.sz0, p.sz1);
       const bool own = real && a >= S - 1 && a < S - 1 + T && b >= S - 1 && b < S - 1 + T && y < p.y1 && z < p.z1;
       lid[q] = valid ? (a + 1) * W0 + (b + 1) : G::DUMMY;
-      gof[q] = real ? (((y + 1) * R + z + zs1) | kReal | (own ? kOwn : 0)) : zero_off;
+      gof[q] = ld ? (((y + ya) * R + z + za) | kLd | (real ? kReal : 0) | (own ? kOwn : 0)) : zero_off;
     }
     // wave-uniform stage masks: bit k−1 of wsm[q] is set when some lane of this wave's position set q lies inside stage
     // k's region (rows [k−1, H1−k+1) of the stage-1 region); other (wave, q, stage) combinations are skipped with a
@@ -191,7 +214,9 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       const int y = ty0 - S + a0, z = tz0 - S + b0;
       const bool valid = ridx < G::NR;
       lrid[r] = valid ? a0 * W0 + b0 : G::DUMMY;
-      grof[r] = (valid && inside(p.gy0 + y) && inside(p.gz0 + z)) ? ((y + 1) * R + z + zs1) | kReal : zero_off;
+      grof[r] = (valid && inside(p.gy0 + y) && inside(p.gz0 + z) && in_rng(y, p.ay0, p.ay1) && in_rng(z, p.az0, p.az1))
+                    ? ((y + ya) * R + z + za) | kLd
+                    : zero_off;
     }
     // sin tables: syw[j] = s[y] for y = ty0 − S − 1 + j (the u^n region ± 1), szw likewise, sxw[i] = s[x] for
     // x = x0 − S − 1 + i; indices clamped into −1..N+1 (only nodes of the interior, and their neighbours, use them)
@@ -206,14 +231,14 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         syw[t] = sc(p.gy0 + ty0 - S - 1 + t);
         szw[t] = sc(p.gz0 + tz0 - S - 1 + t);
       }
-      for (int i = tid; i < tb_nx_table<S>(p.x1 - p.x0); i += NT) sxw[i] = sc(p.gx0 + p.x0 - S - 1 + i);
+      for (int i = tid; i < tb_nx_table<S>(x1 - x0); i += NT) sxw[i] = sc(p.gx0 + x0 - S - 1 + i);
       __syncthreads();
     }
     // table indices of an LDS position li (u^n-region coordinates): y ↔ li / W0 + 1, z ↔ li % W0 + 1 (the pad's dummy
     // node is clamped into the table)
     auto ytab = [&](int li) { return imin(li / W0 + 1, W0); };
     auto ztab = [&](int li) { return li - (li / W0) * W0 + 1; };
-    const int xtab0 = S + 1 - p.x0;  // x ↔ sxw[x + xtab0]
+    const int xtab0 = S + 1 - x0;  // x ↔ sxw[x + xtab0]
     // analytic u⁰ = φ and u¹ at plane x, LDS position li (INIT)
     auto phi_at = [&](int x, int li) {
       return (sxw[x + xtab0] * syw[ytab(li)]) * szw[ztab(li)];
@@ -235,7 +260,6 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     double L[S][Q][4] = {};  // L[0] = u^n, L[k] = u^{n+k} (k < S)
     double Lm[Q][2] = {};    // u^{n−1}
     double Rg[QR][2] = {};   // u^n ring
-    const int x0 = p.x0, x1 = p.x1;
     const int i0 = x0 - S + 1, i1 = x1 + S - 2;
     auto lds_plane = [&](int j, int par) { return lds + (j * 2 + par) * PLP; };
 
@@ -246,10 +270,10 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       if constexpr (INIT) {
 #pragma unroll
         for (int q = 0; q < Q; ++q)
-          if (wsm[q]) L[0][q][slot] = u1_at(x, lid[q], gof[q] & kReal);
+          if (wsm[q]) L[0][q][slot] = u1_at(x, lid[q], gof[q] & kLd);
 #pragma unroll
         for (int r = 0; r < QR; ++r)
-          if (wbase_r + r * NT < G::NR) Rg[r][rs] = u1_at(x, lrid[r], grof[r] & kReal);
+          if (wbase_r + r * NT < G::NR) Rg[r][rs] = u1_at(x, lrid[r], grof[r] & kLd);
       } else {
         const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;  // always an allocated plane
         const double* base = p.cur + static_cast<i64>(xs + 1) * P;
@@ -293,10 +317,8 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     // (S = 4: the queues leave no room for them — the factors are re-read from the LDS tables per use instead)
     constexpr bool kFacReg = S < 4;
     double fy[Q], fz[Q], fyr[QR], fzr[QR];
-    // checked passes: each position's z factor of the analytic solution (loop-invariant) in a register
-    double czs[Q];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) czs[q] = (CM != 0 && p.check_mask) ? szw[ztab(lid[q])] : 0.0;
+    // (the check's z factor of a position is re-read from the LDS table per use: keeping it in a register per position
+    // spills at S = 4 since the y/z stage-real ranges of the block ranks were added)
     auto fyq = [&](int q) { return kFacReg ? fy[q] : syw[ytab(lid[q])]; };
     auto fzq = [&](int q) { return kFacReg ? fz[q] : szw[ztab(lid[q])]; };
     auto fyrr = [&](int r) { return kFacReg ? fyr[r] : syw[ytab(lrid[r])]; };
@@ -344,14 +366,14 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         p3[li] = f3;
         const double c = p2[li];                     // φ(i+2)
         const double lap = d2sum(c, f1, f3, p2[li - W0], p2[li + W0], p2[li - 1], p2[li + 1]);
-        L[0][q][(F + 2) & 3] = ((gof[q] & kReal) && xin) ? first_step(c, lap, p.half_tau2) : 0.0;
+        L[0][q][(F + 2) & 3] = ((gof[q] & kLd) && xin) ? first_step(c, lap, p.half_tau2) : 0.0;
         Lm[q][(F + 1) & 1] = f1;
       }
 #pragma unroll
       for (int r = 0; r < QR; ++r) {
         if (wbase_r + r * NT < G::NR) {
           p3[lrid[r]] = (sx3 * fyrr(r)) * fzrr(r);
-          Rg[r][(F + 2) & 1] = u1_at(i + 2, lrid[r], grof[r] & kReal);
+          Rg[r][(F + 2) & 1] = u1_at(i + 2, lrid[r], grof[r] & kLd);
         }
       }
     };
@@ -397,7 +419,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         }
         if constexpr (kChk) {
           if (chk && own && xreal) {
-            const double e = fabs(v - (rowk[ytab(li)] * czs[q]) * p.ct[k - 1]);
+            const double e = fabs(v - (rowk[ytab(li)] * szw[ztab(li)]) * p.ct[k - 1]);
             emax[k - 1] = fmax(e, emax[k - 1]);  // = (e > m ? e : m) for every non-NaN e; a NaN shows in the sum
             esum[k - 1] += e * e;
           }
@@ -532,25 +554,44 @@ struct TbPlan {
   int nblocks = 0;
 };
 
-TbPlan make_plan_tb(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, i64 sx0, i64 sx1) {
+// `real`: per axis, the local range where stage values are real (outside: Dirichlet 0 / unused); an axis with lo > hi
+// takes the default (x: the compute box; y, z: the whole allocation, i.e. no restriction besides the global interior).
+TbPlan make_plan_tb(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, LBox real) {
   W3D_REQUIRE(t.stages >= 2 && t.stages <= 4, "leapfrog_tb: stages must be 2, 3 or 4");
   W3D_REQUIRE(t.threads == 512 || t.threads == 1024, "leapfrog_tb: threads must be 512 or 1024");
   const LBox full = compute_box(l);
-  // no halo exchange inside a pass: every (y,z) node of the plane must be local (slab ranks / one rank)
-  W3D_REQUIRE(l.gy0 == 0 && l.gz0 == 0 && l.ny == l.N + 1 && l.nz == l.N + 1,
-              "leapfrog_tb needs whole (y,z) planes on the rank");
+  if (real.x0 > real.x1) {
+    real.x0 = full.x0;
+    real.x1 = full.x1;
+  }
+  if (real.y0 > real.y1) {
+    real.y0 = -l.yg;
+    real.y1 = l.ny + l.yg;
+  }
+  if (real.z0 > real.z1) {
+    real.z0 = -l.zg;
+    real.z1 = l.nz + l.zg;
+  }
   W3D_REQUIRE(b.x0 >= full.x0 && b.x1 <= full.x1 && b.y0 >= full.y0 && b.y1 <= full.y1 && b.z0 >= full.z0 &&
                   b.z1 <= full.z1,
               "leapfrog_tb box outside the compute box");
-  W3D_REQUIRE(l.N < (1 << 20) && l.plane < (1 << 29), "leapfrog_tb: plane too large for 29-bit in-plane offsets");
+  W3D_REQUIRE(l.N < (1 << 20) && l.plane < (1 << 28), "leapfrog_tb: plane too large for 28-bit in-plane offsets");
   const i64 S = t.stages;
-  // u^{n+k} (k < S) is read up to S−k planes beyond the box: its values there must be real (sx range) unless they lie
-  // beyond the global boundary (structural zeros); u^n is read S planes beyond the box, within the allocation
-  const bool lo_ok = sx0 <= b.x0 - (S - 1) || l.gx0 + sx0 <= 1;
-  const bool hi_ok = sx1 >= b.x1 + (S - 1) || l.gx0 + sx1 >= l.N;
-  W3D_REQUIRE(lo_ok && hi_ok, "leapfrog_tb: stage-1 range does not cover the box halo");
-  W3D_REQUIRE(l.gx0 + b.x0 - S <= 0 || b.x0 - S >= -l.xg, "leapfrog_tb: x halo deeper than the ghost layers");
-  W3D_REQUIRE(l.gx0 + b.x1 + S - 1 >= l.N || b.x1 + S - 1 < l.nx + l.xg, "leapfrog_tb: x halo deeper than the ghosts");
+  // per axis: u^{n+k} (k < S) is read up to S−k nodes beyond the box, so its values there must be real (the `real`
+  // range) unless they lie beyond the global boundary (structural zeros); u^n is read S nodes beyond the box, within
+  // the allocation (ghost depth g) unless beyond the global boundary
+  auto axis_ok = [&](i64 b0, i64 b1, i64 r0, i64 r1, i64 g0, i64 n, i64 g, const char* ax) {
+    const bool lo_ok = r0 <= b0 - (S - 1) || g0 + r0 <= 1;
+    const bool hi_ok = r1 >= b1 + (S - 1) || g0 + r1 >= l.N;
+    W3D_REQUIRE(lo_ok && hi_ok, std::string("leapfrog_tb: stage-1 range does not cover the box halo in ") + ax);
+    W3D_REQUIRE(g0 + b0 - S <= 0 || b0 - S >= -g, std::string("leapfrog_tb: halo deeper than the ghosts in ") + ax);
+    W3D_REQUIRE(g0 + b1 + S - 1 >= l.N || b1 + S - 1 < n + g,
+                std::string("leapfrog_tb: halo deeper than the ghosts in ") + ax);
+    W3D_REQUIRE(r0 >= -g && r1 <= n + g, std::string("leapfrog_tb: real range outside the allocation in ") + ax);
+  };
+  axis_ok(b.x0, b.x1, real.x0, real.x1, l.gx0, l.nx, l.xg, "x");
+  axis_ok(b.y0, b.y1, real.y0, real.y1, l.gy0, l.ny, l.yg, "y");
+  axis_ok(b.z0, b.z1, real.z0, real.z1, l.gz0, l.nz, l.zg, "z");
   TbPlan pl;
   TbParams& p = pl.prm;
   p.plane = l.plane;
@@ -558,10 +599,23 @@ TbPlan make_plan_tb(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, i
   p.zs = l.zs;
   p.x0 = static_cast<int>(b.x0);
   p.x1 = static_cast<int>(b.x1);
-  p.sx0 = static_cast<int>(sx0);
-  p.sx1 = static_cast<int>(sx1);
+  p.xlen = static_cast<int>(imax(1, b.x1 - b.x0));
+  p.nxc = 1;
+  p.sx0 = static_cast<int>(real.x0);
+  p.sx1 = static_cast<int>(real.x1);
   p.ax0 = static_cast<int>(-l.xg);
   p.ax1 = static_cast<int>(l.nx + l.xg);
+  p.sy0 = static_cast<int>(real.y0);
+  p.sy1 = static_cast<int>(real.y1);
+  p.sz0 = static_cast<int>(real.z0);
+  p.sz1 = static_cast<int>(real.z1);
+  p.ay0 = static_cast<int>(-l.yg);
+  p.ay1 = static_cast<int>(l.ny + l.yg);
+  p.az0 = static_cast<int>(-l.zg);
+  p.az1 = static_cast<int>(l.nz + l.zg);
+  p.zero_off = static_cast<int>(l.zero_off());
+  p.yg = static_cast<int>(l.yg);
+  p.zg = static_cast<int>(l.zg);
   p.N = static_cast<int>(l.N);
   p.gx0 = static_cast<int>(l.gx0);
   p.gy0 = static_cast<int>(l.gy0);
@@ -574,12 +628,20 @@ TbPlan make_plan_tb(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, i
   p.nty = static_cast<int>(ceil_div(b.y1 - b.y0, kTile));
   p.ntz = static_cast<int>(ceil_div(b.z1 - b.z0, kTile));
   const int tiles = p.nty * p.ntz;
-  pl.nblocks = t.xcd_remap ? static_cast<int>(round_up(tiles, 8)) : tiles;
+  // x chunks when the tile grid alone leaves CUs idle (3-D block boxes): at least min_chunk planes per chunk
+  if (t.target_blocks > tiles) {
+    const i64 nxb = b.x1 - b.x0;
+    const i64 want = imin(ceil_div(t.target_blocks, tiles), imax(1, nxb / imax(1, t.min_chunk)));
+    p.xlen = static_cast<int>(ceil_div(nxb, imax(1, want)));
+    p.nxc = static_cast<int>(ceil_div(nxb, p.xlen));
+  }
+  const int blocks = tiles * p.nxc;
+  pl.nblocks = t.xcd_remap ? static_cast<int>(round_up(blocks, 8)) : blocks;
   p.nblocks = pl.nblocks;
   p.xcd_remap = t.xcd_remap ? 1 : 0;
   // blocked XCD ownership when the tile grid splits into 8 equal blocks (one per XCD), the squarest such block
   p.bby = p.bbz = 0;
-  if (t.xcd_remap && t.xcd_blocks && tiles == pl.nblocks && tiles % 8 == 0) {
+  if (t.xcd_remap && t.xcd_blocks && p.nxc == 1 && tiles == pl.nblocks && tiles % 8 == 0) {
     const int per = tiles / 8;
     int best = 1 << 30;
     for (int by = 1; by <= per; ++by) {
@@ -605,11 +667,11 @@ constexpr size_t max_dyn_lds() {
 // allow the dynamic LDS size once per instantiation (outside any stream capture: see leapfrog_tb_prepare): the CU's
 // 160 KiB minus the kernel's static LDS (the reduction arrays as the compiler laid them out, alignment included);
 // returns that limit
-template <int S, int NT, int CM, bool INIT>
+template <int S, int NT, int CM, bool INIT, bool CH>
 size_t prepare_cfg() {
   static_assert(tb_lds_bytes<S, kTile, NT, INIT>() <= max_dyn_lds<NT>(), "leapfrog_tb tile does not fit in LDS");
   static const size_t limit = [] {
-    const void* fn = reinterpret_cast<const void*>(k_leapfrog_tb<S, kTile, NT, CM, INIT>);
+    const void* fn = reinterpret_cast<const void*>(k_leapfrog_tb<S, kTile, NT, CM, INIT, CH>);
     hipFuncAttributes fa{};
     hipError_t e = hipFuncGetAttributes(&fa, fn);
     if (e != hipSuccess) fail(std::string("leapfrog_tb attributes: ") + hipGetErrorString(e));
@@ -623,10 +685,16 @@ size_t prepare_cfg() {
 
 template <int S, int NT, int CM, bool INIT>
 void launch_cfg(const TbParams& p, int nblocks, hipStream_t st) {
-  const size_t limit = prepare_cfg<S, NT, CM, INIT>();
-  const size_t shmem = tb_lds_bytes<S, kTile, NT, INIT>((p.check_mask || INIT) ? tb_nx_table<S>(p.x1 - p.x0) : 0);
-  W3D_REQUIRE(shmem <= limit, "leapfrog_tb: too many planes for the LDS sin table");
-  hipLaunchKernelGGL((k_leapfrog_tb<S, kTile, NT, CM, INIT>), dim3(nblocks), dim3(NT), shmem, st, p);
+  const size_t shmem = tb_lds_bytes<S, kTile, NT, INIT>((p.check_mask || INIT) ? tb_nx_table<S>(p.xlen) : 0);
+  if (p.nxc > 1) {
+    const size_t lim = prepare_cfg<S, NT, CM, INIT, true>();
+    W3D_REQUIRE(shmem <= lim, "leapfrog_tb: too many planes for the LDS sin table");
+    hipLaunchKernelGGL((k_leapfrog_tb<S, kTile, NT, CM, INIT, true>), dim3(nblocks), dim3(NT), shmem, st, p);
+  } else {
+    const size_t lim = prepare_cfg<S, NT, CM, INIT, false>();
+    W3D_REQUIRE(shmem <= lim, "leapfrog_tb: too many planes for the LDS sin table");
+    hipLaunchKernelGGL((k_leapfrog_tb<S, kTile, NT, CM, INIT, false>), dim3(nblocks), dim3(NT), shmem, st, p);
+  }
 }
 
 // instantiated check supersets per S: none, even levels, odd levels, all (checks every 2nd step hit one parity)
@@ -661,12 +729,17 @@ void launch_s(const TbParams& p, int nblocks, const LeapfrogTbTiling& t, bool in
     launch_nt<S, 512, false>(p, nblocks, st);
 }
 
+template <int S, int NT, bool INIT, bool CH>
+void prepare_ch() {
+  prepare_cfg<S, NT, 0, INIT, CH>();
+  prepare_cfg<S, NT, kEven<S>, INIT, CH>();
+  prepare_cfg<S, NT, kOdd<S>, INIT, CH>();
+  prepare_cfg<S, NT, kFull<S>, INIT, CH>();
+}
 template <int S, int NT, bool INIT>
 void prepare_nt() {
-  prepare_cfg<S, NT, 0, INIT>();
-  prepare_cfg<S, NT, kEven<S>, INIT>();
-  prepare_cfg<S, NT, kOdd<S>, INIT>();
-  prepare_cfg<S, NT, kFull<S>, INIT>();
+  prepare_ch<S, NT, INIT, false>();
+  prepare_ch<S, NT, INIT, true>();
 }
 
 }  // namespace
@@ -689,25 +762,30 @@ size_t leapfrog_tb_lds_bytes(int stages) {
 }
 
 int leapfrog_tb_partials(const Layout& l, const LBox& box, const LeapfrogTbTiling& t) {
-  // the block count depends on the (y,z) tiling only: a stage range wide enough for any box passes the halo checks
-  return make_plan_tb(l, box, t, box.x0 - (t.stages - 1), box.x1 + (t.stages - 1)).nblocks;
+  // the block count depends on the (y,z) tiling and the x chunks only: the widest real ranges pass the halo checks
+  const LBox real{-l.xg, l.nx + l.xg, -l.yg, l.ny + l.yg, -l.zg, l.nz + l.zg};
+  LeapfrogTbTiling t1 = t;
+  t1.stages = 2;  // (block count independent of S; S = 2 keeps the ghost-depth checks satisfiable)
+  return make_plan_tb(l, box, t1, real).nblocks;
 }
 
 void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
                         double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
-                        Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, i64 sx0, i64 sx1,
-                        bool analytic_start, int level_stride) {
+                        Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, const LBox& real,
+                        bool analytic_start, int level_stride, int grid_blocks) {
   W3D_REQUIRE(out1 != out2 && (analytic_start || (prev != out1 && prev != out2 && cur != out1 && cur != out2)),
               "leapfrog_tb needs four distinct buffers");
-  if (sx0 > sx1) {
-    const LBox full = compute_box(l);
-    sx0 = full.x0;
-    sx1 = full.x1;
-  }
-  TbPlan pl = make_plan_tb(l, box, t, sx0, sx1);
+  TbPlan pl = make_plan_tb(l, box, t, real);
   if (pl.nblocks == 0) return;
   TbParams& p = pl.prm;
-  const i64 kb = l.kbase();
+  // a padded grid (several launches sharing one level's partial slots, each of grid_blocks entries): the extra
+  // workgroups have no tile and write (0, 0) partials, so every slot entry a reduction reads is written
+  if (grid_blocks > 0) {
+    W3D_REQUIRE(grid_blocks >= pl.nblocks && (!t.xcd_remap || grid_blocks % 8 == 0), "leapfrog_tb: bad grid_blocks");
+    pl.nblocks = p.nblocks = grid_blocks;
+    p.bby = p.bbz = 0;
+  }
+  const i64 kb = (l.xg - 1) * l.plane;  // x base only: in-plane offsets are plane-relative (non-negative)
   p.prev = analytic_start ? nullptr : prev + kb;
   p.cur = analytic_start ? nullptr : cur + kb;
   p.out1 = out1 + kb;

@@ -63,7 +63,7 @@ struct InitParams {
   double* u0;
   double* u1;
   const double* s;
-  i64 plane, N, nx, ny, nz, gx0, gy0, gz0, zs, xg;
+  i64 plane, N, nx, ny, nz, gx0, gy0, gz0, zs, xg, yg, zg;
   int pairs_per_row, pairs_per_plane;
   double ihx2, ihy2, ihz2, half_tau2;
 };
@@ -74,18 +74,20 @@ __global__ __launch_bounds__(256) void k_init_first(const InitParams p) {
   const i64 ix = static_cast<i64>(blockIdx.y) - p.xg;
   const int r = q / p.pairs_per_row;
   const int c = q - r * p.pairs_per_row;
-  const i64 iy = r - 1;
+  const i64 iy = r - p.yg;
   const i64 gx = p.gx0 + ix, gy = p.gy0 + iy;
   const double* s = p.s;
   const bool xy_in = gx > 0 && gx < p.N && gy > 0 && gy < p.N;
-  const bool xy_ok = iy <= p.ny;  // rows past the ghost row do not exist (r < ny + 2 always holds)
+  const bool xy_ok = iy < p.ny + p.yg;  // (r < ny + 2·yg always holds)
   double a0[2], a1[2];
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
-    const i64 iz = 2 * static_cast<i64>(c) + e - 1 - p.zs;
+    const i64 iz = 2 * static_cast<i64>(c) + e - p.zg - p.zs;
     double v = 0.0, w = 0.0;
-    if (xy_ok && iz >= -1 && iz <= p.nz) {
-      const i64 gz = p.gz0 + iz;
+    const i64 gz = p.gz0 + iz;
+    // nodes beyond the global boundary stay 0 (as on the CPU path; the sin table only spans global −1..N+1)
+    if (xy_ok && iz >= -p.zg && iz < p.nz + p.zg && gx >= 0 && gx <= p.N && gy >= 0 && gy <= p.N && gz >= 0 &&
+        gz <= p.N) {
       v = phi(s, gx, gy, gz);
       if (xy_in && gz > 0 && gz < p.N) {
         const double lap = d2sum(v, phi(s, gx - 1, gy, gz), phi(s, gx + 1, gy, gz), phi(s, gx, gy - 1, gz),
@@ -679,6 +681,8 @@ InitParams init_params(const Layout& l, const Coeffs& c, const double* d_s, doub
   p.gz0 = l.gz0;
   p.zs = l.zs;
   p.xg = l.xg;
+  p.yg = l.yg;
+  p.zg = l.zg;
   W3D_REQUIRE(l.pitch % 2 == 0 && l.plane / 2 < (1ll << 31), "plane too large for the init kernel");
   W3D_REQUIRE(l.nx + 2 * l.xg <= 65535, "too many planes for the init kernel grid");
   p.pairs_per_row = static_cast<int>(l.pitch / 2);

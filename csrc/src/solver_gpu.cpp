@@ -140,19 +140,35 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   mode_ = Mode::kSingleStep;
   W3D_REQUIRE(opt_.temporal >= 1 && opt_.temporal <= 4, "temporal must be 1..4");
   if (opt_.temporal >= 2 && world == 1) mode_ = Mode::kFusedSingle;
-  if (opt_.temporal >= 2 && world > 1 && dims_.py == 1 && dims_.pz == 1) {
-    i64 min_nx = box.nx();
-    for (int r = 0; r < world; ++r) min_nx = imin(min_nx, rank_box(prob_, dims_, r).nx());
+  const bool slab = dims_.py == 1 && dims_.pz == 1;
+  if (opt_.temporal >= 2 && world > 1) {
+    // smallest extent of any rank along each axis (every rank must be able to feed its neighbours' deep halos)
+    i64 mn[3] = {box.nx(), box.ny(), box.nz()};
+    for (int r = 0; r < world; ++r) {
+      const Box b = rank_box(prob_, dims_, r);
+      mn[0] = imin(mn[0], b.nx());
+      mn[1] = imin(mn[1], b.ny());
+      mn[2] = imin(mn[2], b.nz());
+    }
     const int rem = prob_.K - (analytic_ok() ? 1 : 2);  // steps left to the passes (each takes 2..temporal)
-    if (opt_.tb && opt_.init2 && rem >= 2 && min_nx >= imax(opt_.tb_min_planes, 2 * opt_.temporal))
+    const i64 T2 = 2 * opt_.temporal;
+    // 3-D blocks: S-deep ghosts on every split axis, one exchange (faces, edges, corners) between passes
+    const bool block_fits = (dims_.px == 1 || mn[0] >= imax(T2, 8)) && (dims_.py == 1 || mn[1] >= imax(T2, 8)) &&
+                            (dims_.pz == 1 || mn[2] >= imax(T2, 8));
+    if (opt_.tb && opt_.init2 && rem >= 2 && slab && mn[0] >= imax(opt_.tb_min_planes, T2))
+      mode_ = Mode::kDeepTb;
+    else if (opt_.tb && opt_.init2 && rem >= 2 && !slab && block_fits)
       mode_ = Mode::kDeepTb;
     // (two-step passes, measured with --fake-rank on 512³: they win from ~128 local planes up, but at 64 planes the
     // two 2-plane shell passes and the per-chunk stage-1 recompute cost more than the saved traffic)
-    else if (min_nx >= opt_.deep_min_planes && min_nx >= 3 && pairable())
+    else if (slab && mn[0] >= opt_.deep_min_planes && mn[0] >= 3 && pairable())
       mode_ = Mode::kDeep;
   }
+  block_tb_ = mode_ == Mode::kDeepTb && !slab;
   for (int attempt = 0; attempt < 2; ++attempt) {
-    lay_ = make_layout(prob_, box, 16, mode_ == Mode::kDeep ? 2 : mode_ == Mode::kDeepTb ? opt_.temporal : 1);
+    const i64 T = opt_.temporal;
+    lay_ = make_layout(prob_, box, 16, mode_ == Mode::kDeep ? 2 : (mode_ == Mode::kDeepTb && dims_.px > 1) ? T : 1,
+                       block_tb_ && dims_.py > 1 ? T : 1, block_tb_ && dims_.pz > 1 ? T : 1);
     // memory plan: temporal blocking needs four field buffers; fall back to the two-buffer in-place scheme when four
     // do not fit next to the other allocations (2049³ fp64 is 68.8 GB per buffer)
     size_t free_b = 0, total_b = 0;
@@ -160,6 +176,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
     const double need2 = 2.0 * static_cast<double>(lay_.bytes()), headroom = 2.0e9;
     if (mode_ != Mode::kSingleStep && 2.0 * need2 + headroom > static_cast<double>(free_b)) {
       mode_ = Mode::kSingleStep;
+      block_tb_ = false;
       continue;
     }
     W3D_REQUIRE(need2 + 1.0e8 < static_cast<double>(free_b),
@@ -218,8 +235,18 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   nb_lo_ = nb[0][0];
   nb_hi_ = nb[0][1];
   if (mode_ == Mode::kDeepTb) {
-    sx0_ = full_.x0 - (nb_lo_ ? opt_.temporal - 1 : 0);
-    sx1_ = full_.x1 + (nb_hi_ ? opt_.temporal - 1 : 0);
+    const i64 T1 = opt_.temporal - 1;
+    sx0_ = full_.x0 - (nb_lo_ ? T1 : 0);
+    sx1_ = full_.x1 + (nb_hi_ ? T1 : 0);
+    sreal_ = LBox{sx0_, sx1_, full_.y0 - (nb[1][0] ? T1 : 0), full_.y1 + (nb[1][1] ? T1 : 0),
+                  full_.z0 - (nb[2][0] ? T1 : 0), full_.z1 + (nb[2][1] ? T1 : 0)};
+  }
+  // 3-D block passes: one plan (and device job tables) per pass depth that can follow an exchange
+  if (block_tb_) {
+    for (int st = 2; st <= opt_.temporal; ++st) {
+      deep_[st] = make_deep_plan(lay_, dims_, rank_, st);
+      deep_max_ = imax(deep_max_, deep_[st].total);
+    }
   }
 
   // device memory
@@ -242,10 +269,16 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   const std::vector<double> s = sin_table_ext(prob_);
   W3D_HIP(hipMalloc(&d_s_, s.size() * sizeof(double)));
   W3D_HIP(hipMemcpy(d_s_, s.data(), s.size() * sizeof(double), hipMemcpyHostToDevice));
-  if (plan_.packed_doubles > 0) {
-    W3D_HIP(hipMalloc(&send_buf_, static_cast<size_t>(plan_.packed_doubles) * sizeof(double)));
-    W3D_HIP(hipMalloc(&recv_buf_, static_cast<size_t>(plan_.packed_doubles) * sizeof(double)));
+  const i64 stage = imax(plan_.packed_doubles, deep_max_);
+  if (stage > 0) {
+    W3D_HIP(hipMalloc(&send_buf_, static_cast<size_t>(stage) * sizeof(double)));
+    W3D_HIP(hipMalloc(&recv_buf_, static_cast<size_t>(stage) * sizeof(double)));
   }
+  if (block_tb_)
+    for (int st = 2; st <= opt_.temporal; ++st) {
+      pack_tab_[st] = make_box_copy_table(deep_[st], false);
+      unpack_tab_[st] = make_box_copy_table(deep_[st], true);
+    }
   n_full_ = leapfrog_blocks(lay_, &full_, 1, opt_.tiling);
   n_shell_ = leapfrog_blocks(lay_, shell_.data(), static_cast<int>(shell_.size()), opt_.tiling);
   n_int_ = leapfrog_blocks(lay_, &interior_, 1, opt_.tiling);
@@ -281,6 +314,8 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
 GpuSolver::~GpuSolver() {
   // a destructor must not throw: release errors are dropped on purpose (the device may already be in an error state)
   if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
+  for (BoxCopyTable& t : pack_tab_) free_box_copy_table(t);
+  for (BoxCopyTable& t : unpack_tab_) free_box_copy_table(t);
   for (double* p : {u_[0], u_[1], u_[2], u_[3], d_s_, send_buf_, recv_buf_})
     if (p) (void)hipFree(p);
   if (partials_) (void)hipFree(partials_);
@@ -296,7 +331,8 @@ GpuSolver::~GpuSolver() {
 }
 
 size_t GpuSolver::device_bytes() const {
-  return static_cast<size_t>(nbuf_) * static_cast<size_t>(lay_.bytes()) + 2 * static_cast<size_t>(plan_.packed_doubles) * sizeof(double) +
+  return static_cast<size_t>(nbuf_) * static_cast<size_t>(lay_.bytes()) +
+         2 * static_cast<size_t>(imax(plan_.packed_doubles, deep_max_)) * sizeof(double) +
          static_cast<size_t>(n_partials_) * sizeof(Partial) + static_cast<size_t>(prob_.N + 3) * sizeof(double) +
          static_cast<size_t>(kTbRegions) * 4 * 3 * static_cast<size_t>(n_tb_) * sizeof(Partial);
 }
@@ -313,7 +349,7 @@ std::string GpuSolver::mode() const {
   switch (mode_) {
     case Mode::kFusedSingle: return "fused-single";
     case Mode::kDeep: return "deep-halo";
-    case Mode::kDeepTb: return "deep-tb";
+    case Mode::kDeepTb: return block_tb_ ? "deep-tb-block" : "deep-tb";
     default: return "single-step";
   }
 }
@@ -324,14 +360,16 @@ std::string GpuSolver::mode() const {
 bool GpuSolver::split() const { return opt_.overlap && plan_.any(); }
 bool GpuSolver::post_exchange() const { return mode_ == Mode::kDeep || mode_ == Mode::kDeepTb || split(); }
 
-bool GpuSolver::late_exchange() const { return mode_ == Mode::kDeepTb && !opt_.overlap; }
+// (3-D block passes always exchange after the whole pass: the y/z face shells of S-deep halos would be thin tile
+// strips recomputing most of their tiles)
+bool GpuSolver::late_exchange() const { return mode_ == Mode::kDeepTb && (!opt_.overlap || block_tb_); }
 
 bool GpuSolver::needs_exchange(int i) const {
   if (!plan_.any()) return false;
   return post_exchange() ? i + 1 < static_cast<int>(units_.size()) : i > 0;
 }
 
-hipStream_t GpuSolver::xstream() const { return post_exchange() && opt_.overlap ? s1_ : s0_; }
+hipStream_t GpuSolver::xstream() const { return post_exchange() && opt_.overlap && !late_exchange() ? s1_ : s0_; }
 
 // Deep-halo fused passes need every unit to be a pair with no error check on its intermediate step, starting from the
 // analytic (u¹, u²): K even and no odd check step below K.
@@ -408,6 +446,13 @@ void GpuSolver::build_units() {
 
 void GpuSolver::build_msgs(int i) {
   msgs_.clear();
+  if (block_tb_) {
+    // one packed message per neighbour (faces, edges, corners): u^{n+S} s deep, then u^{n+S−1} s − 1 deep
+    deep_s_ = units_[static_cast<size_t>(i) + 1].steps;
+    for (const DeepPeer& q : deep_[deep_s_].peers)
+      msgs_.push_back(Msg{q.peer, 0, send_buf_ + q.buf_off, recv_buf_ + q.buf_off, q.count});
+    return;
+  }
   if (mode_ == Mode::kDeepTb) {
     // the next pass of s steps reads u^{n+S} (this pass's out2) on s ghost planes and u^{n+S−1} (out1) on s − 1
     const i64 s = units_[static_cast<size_t>(i) + 1].steps, P = lay_.plane, nx = lay_.nx;
@@ -570,10 +615,25 @@ const GpuSolver::Msg& GpuSolver::peer_msg(const Msg& m, const std::vector<GpuSol
   return *g;
 }
 
+bool GpuSolver::packs() const { return (mode_ == Mode::kSingleStep && plan_.packed_doubles > 0) || block_tb_; }
+
+void GpuSolver::pack_halo(hipStream_t st) {
+  if (block_tb_)
+    launch_box_copy(lay_, pack_tab_[deep_s_], 0, u_[uf_[1]], u_[uf_[0]], send_buf_, st);
+  else if (mode_ == Mode::kSingleStep && plan_.packed_doubles > 0)
+    launch_pack(lay_, plan_, post_exchange() ? u_[old_] : u_[cur_], send_buf_, st);
+}
+
+void GpuSolver::unpack_halo(hipStream_t st) {
+  if (block_tb_)
+    launch_box_copy(lay_, unpack_tab_[deep_s_], 1, u_[uf_[1]], u_[uf_[0]], recv_buf_, st);
+  else if (mode_ == Mode::kSingleStep && plan_.packed_doubles > 0)
+    launch_unpack(lay_, plan_, recv_buf_, post_exchange() ? u_[old_] : u_[cur_], st);
+}
+
 void GpuSolver::exchange(hipStream_t st, const std::vector<GpuSolver*>* pull) {
-  const bool packed = mode_ == Mode::kSingleStep && plan_.packed_doubles > 0;
-  double* field = post_exchange() ? u_[old_] : u_[cur_];
-  if (packed && !pull) launch_pack(lay_, plan_, field, send_buf_, st);  // (group: each rank packed its own faces)
+  const bool packed = packs();
+  if (packed && !pull) pack_halo(st);  // (group: each rank packed its own faces)
   if (!opt_.fake_comm) {  // fake_comm (perf study): one rank's schedule timed alone, ghosts keep stale values
     ncclComm_t c = static_cast<ncclComm_t>(comm_->raw());
     W3D_NCCL(ncclGroupStart());
@@ -589,7 +649,7 @@ void GpuSolver::exchange(hipStream_t st, const std::vector<GpuSolver*>* pull) {
     }
     W3D_NCCL(ncclGroupEnd());
   }
-  if (packed) launch_unpack(lay_, plan_, recv_buf_, field, st);
+  if (packed) unpack_halo(st);
 }
 
 void GpuSolver::unit_exchange_rccl(int i) {
@@ -615,10 +675,11 @@ void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase) {
   const int slots = mode_ == Mode::kDeepTb ? 3 : 1;
   W3D_REQUIRE(tb_slots_ < slots, "leapfrog_tb: too many launches in one unit");
   Partial* part = mask ? tb_partials_ + tb_region_ * (4 * slots * n_tb_) + tb_slots_ * n_tb_ : nullptr;
-  const i64 sx0 = mode_ == Mode::kDeepTb ? sx0_ : 1, sx1 = mode_ == Mode::kDeepTb ? sx1_ : 0;
+  const LBox real = mode_ == Mode::kDeepTb ? sreal_ : tb_default_real();
   timed(phase, s0_, [&] {
+    // (every launch fills its whole slot of n_tb_ partials: shell and interior boxes may have fewer x chunks)
     launch_leapfrog_tb(lay_, coef_, u_[old_], u_[cur_], u_[uf_[0]], u_[uf_[1]], box, d_s_ + 1, cts, mask, part, t,
-                       s0_, sx0, sx1, u.analytic, slots * n_tb_);
+                       s0_, real, u.analytic, slots * n_tb_, n_tb_);
   });
   if (mask) ++tb_slots_;
 }
@@ -729,6 +790,10 @@ void GpuSolver::enqueue_solve() {
 // Debug aid: fill the ghost regions that the next exchange must overwrite with NaN, so a halo that
 // is not delivered shows up in the error norms at once instead of silently reusing stale values.
 void GpuSolver::poison(hipStream_t st) {
+  if (block_tb_) {  // the ghost regions themselves (the messages land in a staging buffer first)
+    launch_box_copy(lay_, unpack_tab_[deep_s_], 2, u_[uf_[1]], u_[uf_[0]], nullptr, st);
+    return;
+  }
   for (const Msg& m : msgs_)
     W3D_HIP(hipMemsetAsync(m.recv, 0xFF, static_cast<size_t>(m.count) * sizeof(double), st));
 }
@@ -767,8 +832,7 @@ void GpuSolver::lb_pack(int i) {
   if (!needs_exchange(i)) return;
   hipStream_t xs = xstream();
   if (xs != s0_) W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
-  if (mode_ == Mode::kSingleStep && plan_.packed_doubles > 0)
-    launch_pack(lay_, plan_, post_exchange() ? u_[old_] : u_[cur_], send_buf_, xs);
+  pack_halo(xs);
   W3D_HIP(hipEventRecord(ev_packed_, xs));
 }
 
@@ -785,8 +849,7 @@ void GpuSolver::lb_pull(int i, const std::vector<GpuSolver*>& ranks, hipEvent_t 
       W3D_HIP(hipMemcpyAsync(m.recv, g.send, static_cast<size_t>(m.count) * sizeof(double), hipMemcpyDeviceToDevice,
                              xs));
     }
-    if (mode_ == Mode::kSingleStep && plan_.packed_doubles > 0)
-      launch_unpack(lay_, plan_, recv_buf_, post_exchange() ? u_[old_] : u_[cur_], xs);
+    unpack_halo(xs);
   }
   W3D_HIP(hipEventRecord(ev_halo_, xs));
 }

@@ -33,8 +33,10 @@ def grid_view(layout, u: torch.Tensor) -> torch.Tensor:
     """Dense (nx+2, ny+2, nz+2) view (one ghost layer on every side) of a padded flat field."""
     nx, ny, nz, p, zs = int(layout.nx), int(layout.ny), int(layout.nz), int(layout.pitch), int(layout.zs)
     xg = int(getattr(layout, "xg", 1))
-    rows = u.view(nx + 2 * xg, ny + 2, p)
-    return rows[xg - 1: xg + nx + 1, :, zs: zs + nz + 2]
+    yg = int(getattr(layout, "yg", 1))
+    zg = int(getattr(layout, "zg", 1))
+    rows = u.view(nx + 2 * xg, ny + 2 * yg, p)
+    return rows[xg - 1: xg + nx + 1, yg - 1: yg + ny + 1, zs + zg - 1: zs + zg + nz + 1]
 
 
 def to_grid(layout, u: torch.Tensor) -> torch.Tensor:

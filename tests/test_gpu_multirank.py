@@ -221,7 +221,11 @@ def test_schedule_modes(gpu):
     assert Solver(even, backend="hip", device=0).native.mode == "fused-single"
     assert Solver(even, backend="hip", device=0, temporal=1).native.mode == "single-step"
     assert Solver(even, backend="hip", transport="loopback", world=4, rank=0, decomp="2x2x1",
+                  device=0).native.mode() == "deep-tb-block"  # S-deep ghosts on x and y
+    assert Solver(even, backend="hip", transport="loopback", world=4, rank=0, decomp="2x2x1", temporal=1,
                   device=0).native.mode() == "single-step"
+    assert Solver(even, backend="hip", transport="loopback", world=16, rank=0, decomp="8x2x1",
+                  device=0).native.mode() == "single-step"  # x boxes of 5 planes < 2·temporal
     assert Solver(odd_check, backend="hip", transport="loopback", world=2, rank=0, decomp="slab",
                   device=0, deep_min_planes=3, tb=False).native.mode() == "single-step"  # odd checks: no pairs
     assert Solver(odd_check, backend="hip", transport="loopback", world=2, rank=0, decomp="slab",
@@ -234,3 +238,24 @@ def test_schedule_modes(gpu):
                   device=0).native.mode() == "deep-tb"  # 20 planes per rank >= default 16
     assert Solver(even, backend="hip", transport="loopback", world=4, rank=0, decomp="slab",
                   device=0).native.mode() == "single-step"  # 10 planes per rank < 16
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("world,decomp", [(4, "2x2x1"), (4, "1x2x2"), (8, "2x2x2"), (6, "3x2x1"), (4, "2x1x2")])
+@pytest.mark.parametrize("K,check_every,temporal", [(20, 2, 4), (9, 1, 4), (12, 3, 3), (11, 2, 2)])
+def test_block_deep_tb_bitexact(gpu, world, decomp, overlap, K, check_every, temporal):
+    """3-D block ranks on the LDS S-step kernel with S-deep ghosts on every split axis: one exchange of faces, edges and
+    corners (packed per neighbour by k_box_copy) between passes, small boxes split into x chunks. Bit-identical to one
+    GPU with NaN-poisoned ghost regions; odd-level checks and a checked step 1 (no analytic start) included."""
+    spec = ProblemSpec(N=66, tau=1e-3, K=K, check_every=check_every)
+    ref = Solver(spec, backend="hip", device=0, temporal=1)
+    r1 = ref.run()
+    f0, f1 = ref.global_field(0), ref.global_field(1)
+    g = Solver(spec, backend="hip", transport="loopback", world=world, rank=0, decomp=decomp, overlap=overlap,
+               device=0, poison_ghosts=True, temporal=temporal)
+    assert g.native.mode() == "deep-tb-block"
+    for _ in range(2):
+        r = g.run()
+        _same(r, r1)
+        assert torch.equal(g.global_field(0), f0)
+        assert torch.equal(g.global_field(1), f1)

@@ -73,3 +73,15 @@ def test_loopback_graph_bitexact(gpu, tmp_path):
     _, f1 = _single(70, 9)
     meta, f, _ = _group(tmp_path, 70, 9, 4, "2x2x1", transport="loopback")
     assert meta["graph"] is True and meta["rccl_comms"] == 0 and np.array_equal(f, f1)
+
+
+@pytest.mark.parametrize("world,decomp,K", [(4, "2x2x1", 20), (8, "2x2x2", 20), (4, "1x2x2", 9), (6, "3x2x1", 12)])
+def test_rccl_self_block_deep_tb_graph(gpu, tmp_path, world, decomp, K):
+    """3-D block deep-tb ranks (S-deep ghosts, faces + edges + corners to up to 26 neighbours in one RCCL group),
+    captured with RCCL inside the graph: bit-identical to one GPU, also with poisoned ghost regions."""
+    N = 66
+    _, f1 = _single(N, K)
+    for extra in ((), ("--poison-ghosts",)):
+        meta, f, _ = _group(tmp_path, N, K, world, decomp, extra=extra)
+        assert meta["schedule"] == "deep-tb-block" and meta["graph"] is True
+        assert np.array_equal(f, f1)

@@ -28,20 +28,27 @@ def lap7(c, xm, xp, ym, yp, zm, zp, ihx2, ihy2, ihz2):
 
 
 def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2: np.ndarray, box, s_ext: np.ndarray,
-             S: int, sx, ct=None, check_mask: int = 0, analytic_start: bool = False):
+             S: int, sx, ct=None, check_mask: int = 0, analytic_start: bool = False, xlen: int | None = None):
     """Emulate one launch. Arrays are the flat padded fields (layout.total doubles); s_ext is the extended sin table
     (element g+1 ↔ global g). Returns {k: (max, sumsq)} for checked stages (per-tile partials combined in order).
     analytic_start: u^{n-1} = φ and u^n = u¹ come from the kernel's LDS sin tables (same index math and clamping)
-    instead of prev/cur."""
+    instead of prev/cur. sx: the stage-real range, (sx0, sx1) or (sx0, sx1, sy0, sy1, sz0, sz1) (y/z default: the whole
+    allocation). xlen: x chunk length (the kernel's chunking of small boxes; default: one chunk)."""
     G = Geom(S)
     N = int(lay.N)
     P, R, zs, xg = int(lay.plane), int(lay.pitch), int(lay.zs), int(lay.xg)
+    yg, zg = int(getattr(lay, "yg", 1)), int(getattr(lay, "zg", 1))
+    nyl, nzl = int(lay.ny), int(lay.nz)
     gx0, gy0, gz0 = int(lay.gx0), int(lay.gy0), int(lay.gz0)
     total = int(lay.total)
-    kb = (xg - 1) * P
-    x0, x1, y0, y1, z0, z1 = int(box.x0), int(box.x1), int(box.y0), int(box.y1), int(box.z0), int(box.z1)
-    sx0, sx1 = sx  # the kernel's default is the rank's compute-box x range
+    kb = (xg - 1) * P + (yg - 1) * R + (zg - 1)
+    zero_off = P - 1  # Layout::zero_off: the plane's last double (row padding), only ever 0
+    bx0, bx1, y0, y1, z0, z1 = int(box.x0), int(box.x1), int(box.y0), int(box.y1), int(box.z0), int(box.z1)
+    sx = tuple(sx)
+    sx0, sx1 = sx[0], sx[1]  # the kernel's default is the rank's compute-box x range
+    sy0, sy1, sz0, sz1 = sx[2:6] if len(sx) == 6 else (-yg, nyl + yg, -zg, nzl + zg)
     ax0, ax1 = -xg, int(lay.nx) + xg
+    ay0, ay1, az0, az1 = -yg, nyl + yg, -zg, nzl + zg
     ihx2, ihy2, ihz2, tau2 = co.ihx2, co.ihy2, co.ihz2, co.lam  # tau2 here: τ²/h², the coefficient of d2sum
     ct = list(ct) if ct is not None else [0.0] * S
 
@@ -49,9 +56,20 @@ def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2:
         return (g >= 1) & (g <= N - 1)
 
     def goff(x, y, z):
-        o = kb + (x + 1) * P + (y + 1) * R + (z + 1 + zs)
+        # the kernel's split: plane base (x + xg)·P plus a plane-relative offset that must fit its 28 flag-free bits
+        inp = (y + yg) * R + (z + zg + zs)
+        if np.any(inp < 0) or np.any(inp >= min(P, 1 << 28)):
+            raise IndexError(f"in-plane offset out of range at x={x}")
+        o = (x + xg) * P + inp
+        assert np.all(o == kb + (x + 1) * P + (y + 1) * R + (z + 1 + zs))
         if np.any(o < 0) or np.any(o >= total):
             raise IndexError(f"global offset out of range at x={x}")
+        return o
+
+    def zoff(x):  # the zero slot of plane x
+        o = (x + xg) * P + zero_off
+        if o < 0 or o >= total:
+            raise IndexError(f"zero slot out of range at x={x}")
         return o
 
     def sget(g):
@@ -61,10 +79,12 @@ def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2:
         return s_ext[g + 1]
 
     nty, ntz = -(-(y1 - y0) // T), -(-(z1 - z0) // T)
-    i0, i1 = x0 - S + 1, x1 + S - 2
+    xlen = xlen or max(1, bx1 - bx0)
+    chunks = [(c, min(bx1, c + xlen)) for c in range(bx0, bx1, xlen)]
     errs = {k: [0.0, 0.0] for k in range(1, S + 1) if check_mask >> (k - 1) & 1}
-    for tyi in range(nty):
-        for tzi in range(ntz):
+    for (x0, x1), tyi, tzi in ((c, a, b) for c in chunks for a in range(nty) for b in range(ntz)):
+        i0, i1 = x0 - S + 1, x1 + S - 2
+        if True:
             ty0, tz0 = y0 + tyi * T, z0 + tzi * T
             ring = {j: [np.zeros((G.W(j), G.W(j))) for _ in range(1 if j < 0 else 3)] for j in range(-1, S)}
             emax = [0.0] * S
@@ -108,11 +128,16 @@ def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2:
                         return c
                     lap = lap7(c, (sxw[xi - 1] * sy) * sz, (sxw[xi + 1] * sy) * sz, (sxc * syw[ya - 1]) * sz,
                                (sxc * syw[ya + 1]) * sz, cy * szw[zb - 1], cy * szw[zb + 1], co.ihx2, co.ihy2, co.ihz2)
-                    real = inside(gy0 + y) & inside(gz0 + z) & (1 <= gx0 + x <= N - 1)
+                    in_a = (y >= ay0) & (y < ay1) & (z >= az0) & (z < az1)
+                    real = inside(gy0 + y) & inside(gz0 + z) & (1 <= gx0 + x <= N - 1) & in_a
                     return np.where(real, c + co.half_lam * lap, 0.0)
                 if ax0 <= x < ax1 and 1 <= gx0 + x <= N - 1:
-                    m = inside(gy0 + y) & inside(gz0 + z)
+                    # loaded wherever the rank holds the node (interior ∩ allocation); elsewhere the zero slot
+                    in_a = (y >= ay0) & (y < ay1) & (z >= az0) & (z < az1)
+                    m = inside(gy0 + y) & inside(gz0 + z) & in_a
                     v[m] = src[goff(x, y[m], z[m])]
+                    if (~m).any():
+                        v[~m] = src[zoff(x)]
                 return v
 
             def commit(x):
@@ -137,7 +162,7 @@ def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2:
                 y = ty0 - hk + a[:, None] + 0 * a[None, :]
                 z = tz0 - hk + a[None, :] + 0 * a[:, None]
                 xreal = sx0 <= xp < sx1 and 1 <= gx0 + xp <= N - 1
-                real = xreal & inside(gy0 + y) & inside(gz0 + z)
+                real = xreal & inside(gy0 + y) & inside(gz0 + z) & (y >= sy0) & (y < sy1) & (z >= sz0) & (z < sz1)
                 v = np.where(real, (2.0 * c - o) + tau2 * lap, 0.0)
                 if k < S:
                     ring[k][xp % 3] = v

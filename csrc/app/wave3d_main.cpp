@@ -120,7 +120,8 @@ constexpr Personality kPersonalities[] = {
                "  --t2-rows R / --t2-target W   fused two-step kernel: rows per wave, x-chunking target (waves)\n"
                "  --repeat R / --warmup W   timed / untimed solves (report min and mean)\n"
                "  --bench-steps K    then K back-to-back solves between two sync+barriers (max over ranks)\n"
-               "  --autotune         time the multi-rank schedule candidates (slab S4/S4-seq/S3/S2/S1, block) and\n"
+               "  --autotune         time the multi-rank schedule candidates (slab S4/S4-seq/S3/S2/S1, block S4/S3/S1)\n"
+               "                     and\n"
                "                     keep the fastest (slowest rank decides)\n"
                "  --phases           per-phase device times (init/compute/exchange/check) of the timed schedule\n"
                "  --variant V        leapfrog kernel: 1 = register-queue waves (default), 0 = LDS-staged tile\n"
@@ -524,8 +525,9 @@ struct Candidate {
   bool overlap;
 };
 constexpr Candidate kCandidates[] = {
-    {"slab-S4", "slab", 4, true},  {"slab-S4-seq", "slab", 4, false}, {"slab-S3", "slab", 3, true},
-    {"slab-S2", "slab", 2, true},  {"slab-S1", "slab", 1, true},      {"block-S1", "block", 1, true},
+    {"slab-S4", "slab", 4, true},   {"slab-S4-seq", "slab", 4, false}, {"slab-S3", "slab", 3, true},
+    {"slab-S2", "slab", 2, true},   {"slab-S1", "slab", 1, true},      {"block-S4", "block", 4, true},
+    {"block-S3", "block", 3, true}, {"block-S1", "block", 1, true},
 };
 
 int run_gpu(const Args& a) {

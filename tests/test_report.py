@@ -49,3 +49,30 @@ def test_scaling_report_plot(tmp_path):
         out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scaling_report.py"), str(src), "--plot",
                               str(png)], check=True, capture_output=True, text=True).stdout
         assert "figure:" in out and png.stat().st_size > 1000
+
+
+def test_scaling_report_reads_driver_scale_record(tmp_path):
+    """A driver SCALE record (bench lines nested per GPU count, repeated under "parsed" and "run") gives one row per
+    GPU count, the speedup/efficiency table, the per-phase breakdown and the figure."""
+    def line(n, ms):
+        return {"metric": "gcell_updates_per_s_512cube_K20", "n_gpus": n, "ms_per_step": ms,
+                "value": 512 ** 3 * 20 / (ms / 1e3) / 1e9, "config": {"schedule": "slab-S4" if n > 1 else "fused"},
+                "phases_ms": {"compute": ms * 0.9, "shell": 0.1 if n > 1 else 0, "exchange": 0.05 * (n > 1),
+                              "check": 0.02, "gather_host": ms}}
+    rec = {"runs": {str(n): {"parsed": line(n, ms), "run": {"stdout": "...", "parsed": line(n, ms)}}
+                    for n, ms in ((1, 4.97), (2, 2.6), (4, 1.4), (8, 0.9))}}
+    p = tmp_path / "SCALE_r02.json"
+    p.write_text(json.dumps(rec))
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import scaling_report
+
+    rows = scaling_report.load(str(p))
+    assert sorted(r["n_gpus"] for r in rows) == [1, 2, 4, 8]
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scaling_report.py"), str(p)], check=True,
+                         capture_output=True, text=True).stdout
+    assert "| 8 | 0.00090 |" in out and "Phase breakdown" in out and "| 8 | slab-S4 |" in out
+    pytest.importorskip("matplotlib")
+    png = tmp_path / "scale.png"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scaling_report.py"), str(p), "--plot", str(png)],
+                   check=True, capture_output=True)
+    assert png.stat().st_size > 1000

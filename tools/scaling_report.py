@@ -21,8 +21,41 @@ REF = {1: 0.752, 2: 0.505}
 REF_GCELL = {p: 512**3 * 20 / t / 1e9 for p, t in REF.items()}
 
 
+def _bench_records(obj, out):
+    """Every bench.py line inside a (possibly nested) JSON object: the driver's SCALE_rNN.json / BENCH_rNN.json files
+    wrap the lines (e.g. under "parsed"), a --out file holds them one per line."""
+    if isinstance(obj, dict):
+        if "n_gpus" in obj and "ms_per_step" in obj:
+            out.append(obj)
+            return
+        for v in obj.values():
+            _bench_records(v, out)
+    elif isinstance(obj, list):
+        for v in obj:
+            _bench_records(v, out)
+
+
 def load(path):
-    return [json.loads(l) for l in open(path) if l.strip().startswith("{")]
+    text = open(path).read()
+    try:  # one JSON document (driver records)
+        doc = json.loads(text)
+    except json.JSONDecodeError:
+        doc = None
+    if isinstance(doc, (dict, list)):
+        rows = []
+        _bench_records(doc, rows)
+        if rows or isinstance(doc, list):
+            return _dedupe(rows)
+        return [doc] if "workers" in doc else []
+    return [json.loads(l) for l in text.splitlines() if l.strip().startswith("{")]
+
+
+def _dedupe(rows):
+    """One line per GPU count (a driver record may repeat a line as "parsed" and inside "run"); the last wins."""
+    by = {}
+    for r in rows:
+        by[(r.get("metric"), r["n_gpus"])] = r
+    return list(by.values())
 
 
 def gpu_rows(rows):
@@ -62,6 +95,17 @@ def print_tables(rows):
             vs = f"{ref / g['t']:.1f}x" if ref else "—"
             print(f"| {g['p']} | {g['t']:.5f} | {g['gcell']:.1f} | {g['speedup']:.2f} | {g['eff']:.2f} | "
                   f"{ref if ref else '—'} | {vs} |")
+        ph = [r for r in sorted(rows, key=lambda r: r["n_gpus"]) if r.get("phases_ms")]
+        if ph:  # the reference's per-GPU-count time breakdown (report.pdf p.16 §4.4: compute / copies / MPI)
+            print("\nPhase breakdown (device ms per solve, max over ranks, traced solve of the timed schedule; exchange "
+                  "overlaps compute when the schedule overlaps):\n")
+            print("| GPUs | schedule | compute | of which shells | exchange | error check | host gather+sync |")
+            print("|---|---|---|---|---|---|---|")
+            for r in ph:
+                p = r["phases_ms"]
+                print(f"| {r['n_gpus']} | {r.get('config', {}).get('schedule', '')} | {p.get('compute', 0):.3f} | "
+                      f"{p.get('shell', 0):.3f} | {p.get('exchange', 0):.3f} | {p.get('check', 0):.3f} | "
+                      f"{p.get('gather_host', 0):.3f} |")
         return
     for (mode, N), rs in cpu_groups(rows).items():
         print(f"\n{mode}, {N}^3:\n\n| workers | time s | speedup | efficiency | GCell/s |")

@@ -65,7 +65,7 @@ struct Args {
   int variant = -1;
   int target_blocks = 0;
   int nt_store = -1;
-  std::string json, dump, trace;
+  std::string json, dump, trace, checkpoint, resume;
   bool quiet = false;
   std::string program = "wave3d";  // reference program personality (argv[0])
 };
@@ -131,6 +131,8 @@ constexpr Personality kPersonalities[] = {
                "  --json PATH        machine-readable summary (rank 0)\n"
                "  --trace PATH       per-unit device times as JSON lines (PATH[.rankR] per rank; implies --timers)\n"
                "  --dump PREFIX      write u^K: PREFIX[.rankR].bin (fp64, C order, owned nodes) + .json\n"
+               "  --checkpoint P     write u^{K-1}, u^K as P.prev / P.cur dumps (resumable)\n"
+               "  --resume P         start from the P.prev / P.cur checkpoint (step n0) and continue to K\n"
                "  --force            run even if the CFL condition is violated\n"
                "  --quiet            only the summary\n");
   std::exit(2);
@@ -200,6 +202,8 @@ Args parse(int argc, char** argv) {
       a.timers = true;
     }
     else if (s == "--dump") a.dump = next();
+    else if (s == "--checkpoint") a.checkpoint = next();
+    else if (s == "--resume") a.resume = next();
     else if (s == "--force") a.force = true;
     else if (s == "--quiet") a.quiet = true;
     else if (s == "-h" || s == "--help") usage();
@@ -302,7 +306,8 @@ void print_errors(const std::vector<int>& steps, const std::vector<double>& mx, 
 }
 
 void write_dump(const std::string& prefix, const Problem& p, const Layout& l, const std::vector<double>& u, int rank,
-                int world, const Dims& d) {
+                int world, const Dims& d, int step = -1) {
+  if (step < 0) step = p.K;
   const std::string base = world > 1 ? prefix + ".rank" + std::to_string(rank) : prefix;
   std::ofstream f(base + ".bin", std::ios::binary | std::ios::trunc);
   std::vector<double> row(static_cast<size_t>(l.nz));
@@ -313,12 +318,94 @@ void write_dump(const std::string& prefix, const Problem& p, const Layout& l, co
       f.write(reinterpret_cast<const char*>(row.data()), static_cast<std::streamsize>(row.size() * sizeof(double)));
     }
   std::ofstream j(base + ".json", std::ios::trunc);
+  j.precision(17);
   j << "{\"format\": \"wave3d-dump-v1\", \"dtype\": \"float64\", \"order\": \"C\", \"N\": " << p.N
-    << ", \"L\": " << p.L << ", \"tau\": " << p.tau << ", \"step\": " << p.K << ", \"t\": " << p.K * p.tau
+    << ", \"L\": " << p.L << ", \"tau\": " << p.tau << ", \"step\": " << step << ", \"t\": " << step * p.tau
     << ", \"shape\": [" << l.nx << ", " << l.ny << ", " << l.nz << "], \"offset\": [" << l.gx0 << ", " << l.gy0
     << ", " << l.gz0 << "], \"global_shape\": [" << p.N + 1 << ", " << p.N + 1 << ", " << p.N + 1
     << "], \"rank\": " << rank << ", \"world\": " << world << ", \"dims\": [" << d.px << ", " << d.py << ", " << d.pz
     << "]}\n";
+}
+
+// --checkpoint PREFIX: u^K → PREFIX.cur, u^{K−1} → PREFIX.prev (wave3d-dump-v1, per rank when world > 1)
+void write_checkpoint(const std::string& prefix, const Problem& p, const Layout& l, const std::vector<double>& cur,
+                      const std::vector<double>& prev, int rank, int world, const Dims& d) {
+  write_dump(prefix + ".cur", p, l, cur, rank, world, d, p.K);
+  write_dump(prefix + ".prev", p, l, prev, rank, world, d, p.K - 1);
+}
+
+// Number after "key": in a one-line JSON object (the dump sidecars this program writes).
+std::vector<double> json_numbers(const std::string& text, const std::string& key) {
+  std::vector<double> out;
+  const size_t k = text.find("\"" + key + "\"");
+  if (k == std::string::npos) return out;
+  size_t i = text.find(':', k) + 1;
+  const bool list = text.find_first_not_of(" ", i) != std::string::npos && text[text.find_first_not_of(" ", i)] == '[';
+  if (list) i = text.find('[', i) + 1;
+  for (;;) {
+    char* end = nullptr;
+    const double v = std::strtod(text.c_str() + i, &end);
+    if (end == text.c_str() + i) break;
+    out.push_back(v);
+    i = static_cast<size_t>(end - text.c_str());
+    if (!list) break;
+    i = text.find_first_of(",]", i);
+    if (i == std::string::npos || text[i] == ']') break;
+    ++i;
+  }
+  return out;
+}
+
+// The GLOBAL (N+1)³ field of a dump PREFIX (one file, or PREFIX.rankR of any decomposition); returns its step.
+int load_dump_global(const std::string& prefix, const Problem& p, std::vector<double>& g) {
+  auto slurp = [](const std::string& path) {
+    std::ifstream f(path);
+    return std::string((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  };
+  std::string meta = slurp(prefix + ".json");
+  std::vector<std::string> bases;
+  if (!meta.empty()) {
+    bases.push_back(prefix);
+  } else {
+    meta = slurp(prefix + ".rank0.json");
+    W3D_REQUIRE(!meta.empty(), "resume: no dump " + prefix + ".json or " + prefix + ".rank0.json");
+    const std::vector<double> w = json_numbers(meta, "world");
+    W3D_REQUIRE(!w.empty() && w[0] >= 1, "resume: dump without a world size");
+    for (int r = 0; r < static_cast<int>(w[0]); ++r) bases.push_back(prefix + ".rank" + std::to_string(r));
+  }
+  const i64 n1 = p.N + 1;
+  g.assign(static_cast<size_t>(n1 * n1 * n1), 0.0);
+  int step = -1;
+  for (const std::string& b : bases) {
+    const std::string m = slurp(b + ".json");
+    const std::vector<double> sh = json_numbers(m, "shape"), of = json_numbers(m, "offset"), st = json_numbers(m, "step"),
+                              nn = json_numbers(m, "N");
+    W3D_REQUIRE(sh.size() == 3 && of.size() == 3 && st.size() == 1 && nn.size() == 1, "resume: bad sidecar " + b);
+    W3D_REQUIRE(static_cast<i64>(nn[0]) == p.N, "resume: dump N differs from the run's N");
+    W3D_REQUIRE(step < 0 || step == static_cast<int>(st[0]), "resume: rank dumps of different steps");
+    step = static_cast<int>(st[0]);
+    const i64 nx = static_cast<i64>(sh[0]), ny = static_cast<i64>(sh[1]), nz = static_cast<i64>(sh[2]);
+    const i64 x0 = static_cast<i64>(of[0]), y0 = static_cast<i64>(of[1]), z0 = static_cast<i64>(of[2]);
+    W3D_REQUIRE(x0 >= 0 && y0 >= 0 && z0 >= 0 && x0 + nx <= n1 && y0 + ny <= n1 && z0 + nz <= n1,
+                "resume: dump box outside the grid");
+    std::ifstream f(b + ".bin", std::ios::binary);
+    W3D_REQUIRE(static_cast<bool>(f), "resume: cannot read " + b + ".bin");
+    for (i64 x = 0; x < nx; ++x)
+      for (i64 y = 0; y < ny; ++y)
+        f.read(reinterpret_cast<char*>(g.data() + ((x0 + x) * n1 + (y0 + y)) * n1 + z0),
+               static_cast<std::streamsize>(nz * static_cast<i64>(sizeof(double))));
+    W3D_REQUIRE(static_cast<bool>(f), "resume: short file " + b + ".bin");
+  }
+  return step;
+}
+
+// --resume PREFIX: u^{n0−1} from PREFIX.prev, u^{n0} from PREFIX.cur; returns n0
+int load_checkpoint(const std::string& prefix, const Problem& p, std::vector<double>& prev, std::vector<double>& cur) {
+  const int sc = load_dump_global(prefix + ".cur", p, cur);
+  const int sp = load_dump_global(prefix + ".prev", p, prev);
+  W3D_REQUIRE(sp == sc - 1, "resume: PREFIX.prev must hold the step before PREFIX.cur");
+  W3D_REQUIRE(sc >= 1 && sc < p.K, "resume: checkpoint step " + std::to_string(sc) + " is not before K");
+  return sc;
 }
 
 int spawn(int np, char** argv) {
@@ -368,6 +455,11 @@ std::string steps_json(const std::vector<int>& st, const std::vector<double>& mx
 
 int run_cpu(const Args& a) {
   CpuSolver s(a.prob, a.check_every, a.threads);
+  if (!a.resume.empty()) {
+    std::vector<double> prev, cur;
+    const int n0 = load_checkpoint(a.resume, a.prob, prev, cur);
+    s.set_state(prev.data(), cur.data(), n0);
+  }
   CpuResult r;
   double best = 1e30, sum = 0;
   for (int i = 0; i < a.warmup + a.repeat; ++i) {
@@ -397,11 +489,14 @@ int run_cpu(const Args& a) {
       << steps_json(r.steps, r.max_err, r.rms_err) << "}\n";
   }
   if (!a.dump.empty()) write_dump(a.dump, a.prob, s.layout(), s.field(0), 0, 1, Dims{1, 1, 1});
+  if (!a.checkpoint.empty())
+    write_checkpoint(a.checkpoint, a.prob, s.layout(), s.field(0), s.field(1), 0, 1, Dims{1, 1, 1});
   return r.finite ? 0 : 3;
 }
 
 // One rank of the multi-process CPU path (--cpu --np P): the reference's MPI / MPI+OpenMP programs.
 int run_cpu_rank(const Args& a, ShmGroup& g, int rank) {
+  W3D_REQUIRE(a.resume.empty(), "--resume runs on one CPU process (--cpu) or on the GPU path, not the CPU ranks");
   try {
     CpuRankSolver s(a.prob, g, rank, a.check_every, a.threads);
     // fault injection: W3D_FAULT_RANK=r makes rank r fail before its first exchange
@@ -444,6 +539,8 @@ int run_cpu_rank(const Args& a, ShmGroup& g, int rank) {
       }
     }
     if (!a.dump.empty()) write_dump(a.dump, a.prob, s.layout(), s.field(0), rank, g.world(), d);
+    if (!a.checkpoint.empty())
+      write_checkpoint(a.checkpoint, a.prob, s.layout(), s.field(0), s.field(1), rank, g.world(), d);
     return r.finite ? 0 : 3;
   } catch (...) {
     g.abort();  // the other ranks leave their barriers with an error instead of waiting for the timeout
@@ -480,6 +577,11 @@ SolverOptions options_from(const Args& a, bool fake) {
 
 int run_group(const Args& a, const SolverOptions& o, const hipDeviceProp_t& prop) {
   GpuGroup g(a.prob, o, a.group, a.group_transport);
+  if (!a.resume.empty()) {
+    std::vector<double> prev, cur;
+    const int n0 = load_checkpoint(a.resume, a.prob, prev, cur);
+    g.set_state(prev.data(), cur.data(), n0);
+  }
   RunResult r;
   double best = 1e30, sum = 0;
   for (int i = 0; i < a.warmup + a.repeat; ++i) {
@@ -501,6 +603,10 @@ int run_group(const Args& a, const SolverOptions& o, const hipDeviceProp_t& prop
   if (!a.dump.empty())
     for (int q = 0; q < g.world(); ++q)
       write_dump(a.dump, a.prob, g.rank(q).layout(), g.rank(q).download(0), q, g.world(), d);
+  if (!a.checkpoint.empty())
+    for (int q = 0; q < g.world(); ++q)
+      write_checkpoint(a.checkpoint, a.prob, g.rank(q).layout(), g.rank(q).download(0), g.rank(q).download(1), q,
+                       g.world(), d);
   if (!a.json.empty()) {
     std::vector<int> cc = g.comm_counts();
     std::ofstream j(a.json);
@@ -616,6 +722,11 @@ int run_gpu(const Args& a) {
     s = std::make_unique<GpuSolver>(a.prob, base, rank, world, comm);
   }
 
+  if (!a.resume.empty()) {
+    std::vector<double> prev, cur;
+    const int n0 = load_checkpoint(a.resume, a.prob, prev, cur);
+    s->set_state(prev.data(), cur.data(), n0);
+  }
   RunResult r;
   double best = 1e30, sum = 0, first = 0;
   for (int i = 0; i < a.warmup + a.repeat; ++i) {
@@ -720,6 +831,8 @@ int run_gpu(const Args& a) {
         << ", \"compute_ms\": " << u.compute_ms << ", \"check_ms\": " << u.check_ms << "}\n";
   }
   if (!a.dump.empty()) write_dump(a.dump, a.prob, s->layout(), s->download(0), rank, world, d);
+  if (!a.checkpoint.empty())
+    write_checkpoint(a.checkpoint, a.prob, s->layout(), s->download(0), s->download(1), rank, world, d);
   return r.finite ? 0 : 3;
 }
 

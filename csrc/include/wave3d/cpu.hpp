@@ -18,6 +18,12 @@ struct LBox {
 
 inline LBox compute_box(const Layout& l) { return LBox{l.cx0, l.cx1, l.cy0, l.cy1, l.cz0, l.cz1}; }
 
+// Resume / loaded-field start: the rank's padded local array (owned nodes and every ghost layer that lies inside the
+// domain; ghosts beyond the global boundary and the row padding 0) from a GLOBAL (N+1)³ C-order field. With ghosts
+// of any depth filled from the global field, the first pass after a resume needs no halo exchange.
+void global_to_local(const Layout& l, const double* global, double* local);
+
+
 // Error accumulator: L∞ and Σe² over the updated (interior) nodes.
 struct ErrAcc {
   double max = 0.0;
@@ -64,6 +70,9 @@ class CpuSolver {
  public:
   CpuSolver(const Problem& p, int check_every = 2, int threads = 0);
   CpuResult run();
+  // Start every following run() at step n0 from u^{n0−1} = prev and u^{n0} = cur (global (N+1)³ fields) instead of
+  // the analytic initial condition: the leapfrog continues to K and checks the steps after n0.
+  void set_state(const double* prev_global, const double* cur_global, int n0);
   // u^K (which = 0) or u^{K-1} (which = 1), padded local layout (single rank = whole domain).
   const std::vector<double>& field(int which) const { return which == 0 ? u_[final_] : u_[1 - final_]; }
   const Layout& layout() const { return lay_; }
@@ -76,6 +85,8 @@ class CpuSolver {
   std::vector<double> u_[2];
   std::vector<double> s_;
   int final_ = 1;
+  int resume_n_ = 0;                     // > 0: start step of a resumed run
+  std::vector<double> resume_[2];        // local u^{n0−1}, u^{n0}
 };
 
 }  // namespace wave3d

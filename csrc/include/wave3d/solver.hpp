@@ -116,6 +116,11 @@ class GpuSolver {
   // Per-phase event timers for the following run() calls (those launch eagerly; the captured graph is kept for when
   // the timers are switched off again): a phase breakdown of exactly the schedule the graph replays.
   void set_timers(bool on) { opt_.timers = on; }
+  // Loaded-field start (resume): every following run() starts at step n0 from u^{n0−1} = prev and
+  // u^{n0} = cur (GLOBAL (N+1)³ C-order fields; each rank takes its box and all its ghost layers from them, so the
+  // first pass needs no exchange) and continues the same schedule kinds to K, checking the steps after n0. The
+  // state is uploaded at the start of each run (eager launches, no graph).
+  void set_state(const double* prev_global, const double* cur_global, int n0);
 
   // Host copy of the local array holding u^K (which = 0) or u^{K−1} (which = 1), full padded layout.
   std::vector<double> download(int which) const;
@@ -242,6 +247,8 @@ class GpuSolver {
   int start_n_ = 1;                           // first leapfrog step after the init kernel
   bool analytic_ = false;                     // the first unit computes u⁰, u¹ itself (no init kernel)
   std::vector<char> is_check_;
+  int resume_n_ = 0;                  // > 0: runs start at this step from resume_[0..1]
+  std::vector<double> resume_[2];     // local (padded) u^{n0−1}, u^{n0}
   hipGraphExec_t graph_exec_ = nullptr;
   int runs_ = 0;  // completed run() calls (RCCL ranks capture the graph only after one eager solve)
   int final_buf_ = 0;            // buffer index holding u^K after a solve
@@ -289,6 +296,7 @@ class GpuGroup {
   bool graph_enabled() const { return graph_; }
   // RCCL communicators in use and the rank count each reports (rccl-self: world one-rank communicators)
   std::vector<int> comm_counts() const;
+  void set_state(const double* prev_global, const double* cur_global, int n0);  // every rank (GpuSolver::set_state)
 
  private:
   void enqueue();

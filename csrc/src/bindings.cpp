@@ -277,7 +277,11 @@ PYBIND11_MODULE(_C, m) {
              return darr(static_cast<py::ssize_t>(v.size()), v.data());
            })
       .def_property_readonly("layout", &CpuSolver::layout)
-      .def("check_steps", &CpuSolver::check_steps);
+      .def("check_steps", &CpuSolver::check_steps)
+      .def("set_state", [](CpuSolver& s, const darr& prev, const darr& cur, int n0) {
+        const i64 n = s.layout().N + 1;
+        s.set_state(ro_ptr(prev, n * n * n, "prev"), ro_ptr(cur, n * n * n, "cur"), n0);
+      }, py::arg("prev"), py::arg("cur"), py::arg("step"));
 
   // ---------------- GPU ----------------
   m.def("gpu_device_count", []() {
@@ -462,6 +466,10 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("halo", &GpuSolver::halo)
       .def_property_readonly("rank", &GpuSolver::rank)
       .def_property_readonly("world", &GpuSolver::world)
+      .def("set_state", [](GpuSolver& s, const darr& prev, const darr& cur, int n0) {
+        const i64 n = s.problem().N + 1;
+        s.set_state(ro_ptr(prev, n * n * n, "prev"), ro_ptr(cur, n * n * n, "cur"), n0);
+      }, py::arg("prev"), py::arg("cur"), py::arg("step"))
       .def("shell_boxes", &GpuSolver::shell_boxes)
       .def("interior_box", &GpuSolver::interior_box)
       .def("check_steps", &GpuSolver::check_steps)
@@ -494,6 +502,10 @@ PYBIND11_MODULE(_C, m) {
       .def("dims", [](GpuGroup& g) { return g.rank(0).dims(); })
       .def("mode", [](GpuGroup& g) { return g.rank(0).mode(); })
       .def("comm_counts", &GpuGroup::comm_counts)
+      .def("set_state", [](GpuGroup& g, const darr& prev, const darr& cur, int n0) {
+        const i64 n = g.rank(0).problem().N + 1;
+        g.set_state(ro_ptr(prev, n * n * n, "prev"), ro_ptr(cur, n * n * n, "cur"), n0);
+      }, py::arg("prev"), py::arg("cur"), py::arg("step"))
       .def_property_readonly("transport", &GpuGroup::transport)
       .def_property_readonly("graph_enabled", &GpuGroup::graph_enabled)
       .def_property_readonly("world", &GpuGroup::world);

@@ -2,6 +2,7 @@
 //
 // Reference programs: `wave` (sequential, readme.md:33-36) and `openmpwave`/`wave3dOMP` (report.pdf p.21 §5.2). Phase
 // timers follow the reference's CPU breakdown columns init / compute / (check) (report.pdf p.16 §4.4).
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 
@@ -23,6 +24,32 @@ CpuSolver::CpuSolver(const Problem& p, int check_every, int threads) : prob_(p),
   u_[0].assign(static_cast<size_t>(lay_.total), 0.0);
   u_[1].assign(static_cast<size_t>(lay_.total), 0.0);
   s_ = sin_table_ext(prob_);
+}
+
+void global_to_local(const Layout& l, const double* g, double* out) {
+  const i64 n1 = l.N + 1;
+  std::fill(out, out + l.total, 0.0);
+#pragma omp parallel for schedule(static)
+  for (i64 x = -l.xg; x < l.nx + l.xg; ++x) {
+    const i64 gx = l.gx0 + x;
+    if (gx < 0 || gx > l.N) continue;
+    for (i64 y = -l.yg; y < l.ny + l.yg; ++y) {
+      const i64 gy = l.gy0 + y;
+      if (gy < 0 || gy > l.N) continue;
+      const i64 z0 = imax(-l.zg, -l.gz0), z1 = imin(l.nz + l.zg, n1 - l.gz0);
+      if (z1 <= z0) continue;
+      std::copy(g + (gx * n1 + gy) * n1 + l.gz0 + z0, g + (gx * n1 + gy) * n1 + l.gz0 + z1, out + l.off(x, y, z0));
+    }
+  }
+}
+
+void CpuSolver::set_state(const double* prev, const double* cur, int n0) {
+  W3D_REQUIRE(n0 >= 1 && n0 < prob_.K, "resume step must be in [1, K)");
+  for (int k = 0; k < 2; ++k) {
+    resume_[k].assign(static_cast<size_t>(lay_.total), 0.0);
+    global_to_local(lay_, k == 0 ? prev : cur, resume_[k].data());
+  }
+  resume_n_ = n0;
 }
 
 std::vector<int> CpuSolver::check_steps() const {
@@ -48,16 +75,22 @@ CpuResult CpuSolver::run() {
     if (!std::isfinite(a.max) || !std::isfinite(a.sum)) r.finite = false;
   };
   const double t0 = now_s();
-  cpu_init_first(lay_, c, s, u_[0].data(), u_[1].data());
+  const int n_start = resume_n_ > 0 ? resume_n_ : 1;
+  if (resume_n_ > 0) {
+    u_[0] = resume_[0];
+    u_[1] = resume_[1];
+  } else {
+    cpu_init_first(lay_, c, s, u_[0].data(), u_[1].data());
+  }
   const double t1 = now_s();
   r.init_s = t1 - t0;
-  if (is_check[1]) {
+  if (is_check[1] && resume_n_ == 0) {
     ErrAcc a;
     cpu_error(lay_, u_[1].data(), box, s, time_factor(prob_, 1), &a);
     record(1, a);
   }
   int cur = 1, old = 0;
-  for (int n = 1; n <= prob_.K - 1; ++n) {
+  for (int n = n_start; n <= prob_.K - 1; ++n) {
     const double tc = now_s();
     if (is_check[static_cast<size_t>(n + 1)]) {
       ErrAcc a;

@@ -337,10 +337,21 @@ size_t GpuSolver::device_bytes() const {
          static_cast<size_t>(kTbRegions) * 4 * 3 * static_cast<size_t>(n_tb_) * sizeof(Partial);
 }
 
+void GpuSolver::set_state(const double* prev, const double* cur, int n0) {
+  W3D_REQUIRE(n0 >= 1 && n0 < prob_.K, "resume step must be in [1, K)");
+  W3D_REQUIRE(mode_ != Mode::kDeepTb || prob_.K - n0 >= 2, "resume: the multi-rank LDS passes need >= 2 steps left");
+  W3D_REQUIRE(mode_ != Mode::kDeep || (prob_.K - n0) % 2 == 0, "resume: two-step passes need an even step count left");
+  for (int k = 0; k < 2; ++k) {
+    resume_[k].assign(static_cast<size_t>(lay_.total), 0.0);
+    global_to_local(lay_, k == 0 ? prev : cur, resume_[k].data());
+  }
+  resume_n_ = n0;
+}
+
 std::vector<int> GpuSolver::check_steps() const {
   std::vector<int> v;
   const int ce = opt_.check_every;
-  for (int n = 1; n <= prob_.K; ++n)
+  for (int n = resume_n_ + 1; n <= prob_.K; ++n)
     if ((ce > 0 && n % ce == 0) || n == prob_.K) v.push_back(n);
   return v;
 }
@@ -534,8 +545,15 @@ void GpuSolver::phase_init() {
   marks_.clear();
   W3D_HIP(hipMemsetAsync(errlog_, 0, static_cast<size_t>(K + 1) * sizeof(Partial), s0_));
   // one rank on the LDS kernel: the first pass starts from the analytic u⁰, u¹ itself (no init kernel, no reads)
-  analytic_ = (mode_ == Mode::kFusedSingle || mode_ == Mode::kDeepTb) && analytic_ok();
-  if (analytic_) {
+  analytic_ = (mode_ == Mode::kFusedSingle || mode_ == Mode::kDeepTb) && analytic_ok() && resume_n_ == 0;
+  if (resume_n_ > 0) {  // loaded state: u^{n0−1} → buf 0, u^{n0} → buf 1 (ghosts included)
+    const size_t bytes = static_cast<size_t>(lay_.bytes());
+    timed(kPhaseInit, s0_, [&] {
+      W3D_HIP(hipMemcpyAsync(u_[0], resume_[0].data(), bytes, hipMemcpyHostToDevice, s0_));
+      W3D_HIP(hipMemcpyAsync(u_[1], resume_[1].data(), bytes, hipMemcpyHostToDevice, s0_));
+    });
+    start_n_ = resume_n_;
+  } else if (analytic_) {
     start_n_ = 1;
   } else if (opt_.init2 && K >= 2) {
     // u¹ -> buf 0, u² -> buf 1 analytically (no read pass), ghosts included; the first leapfrog step is n = 2
@@ -897,7 +915,7 @@ RunResult GpuSolver::run() {
   // first send/recv, which must not happen inside a stream capture; the capture follows on the second run
   if (world_ > 1 && !multistream_capture_safe()) opt_.graph = false;
   const bool capture_ok = !(world_ > 1 && comm_) || runs_ >= 1;
-  if (opt_.graph && !graph_exec_ && capture_ok && !opt_.timers) {
+  if (opt_.graph && !graph_exec_ && capture_ok && !opt_.timers && resume_n_ == 0) {
     // capture once (outside the timed region of later runs); fall back to eager launches if capture is refused
     hipGraph_t g = nullptr;
     bool ok = hipStreamBeginCapture(s0_, hipStreamCaptureModeThreadLocal) == hipSuccess;
@@ -919,7 +937,7 @@ RunResult GpuSolver::run() {
     }
   }
   const double t0 = now_s();
-  if (graph_exec_ && !opt_.timers)
+  if (graph_exec_ && !opt_.timers && resume_n_ == 0)
     W3D_HIP(hipGraphLaunch(graph_exec_, s0_));
   else
     enqueue_solve();
@@ -996,6 +1014,11 @@ GpuGroup::~GpuGroup() {
   for (hipEvent_t e : {fork_, all_packed_, all_pulled_})
     if (e) (void)hipEventDestroy(e);
   if (gs_) (void)hipStreamDestroy(gs_);
+}
+
+void GpuGroup::set_state(const double* prev, const double* cur, int n0) {
+  for (auto& r : ranks_) r->set_state(prev, cur, n0);
+  graph_ = false;  // (the state upload is a pageable host copy: eager runs)
 }
 
 std::vector<int> GpuGroup::comm_counts() const {
@@ -1114,7 +1137,7 @@ RunResult GpuGroup::run() {
     }
   }
   const double t0 = now_s();
-  if (exec_) {
+  if (exec_ && graph_) {
     W3D_HIP(hipGraphLaunch(exec_, gs_));
     trace("graph launch");
   } else {

@@ -8,7 +8,7 @@ Launch several ranks with torchrun (the `mpirun -np P` analogue):
     torchrun --nproc-per-node 4 --master-addr 127.0.0.1 -m mpi_cuda_amd 128 0.001 20 --backend cpu  # MPI analogue
 
 ``--checkpoint PREFIX`` dumps u^{K−1} and u^K (utils/dump.py format) so that ``--resume PREFIX`` can continue a run
-from step K to a larger K.
+from step K to a larger K on any backend and decomposition; the native CLI has the same flags.
 """
 from __future__ import annotations
 
@@ -45,7 +45,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--json", default="")
     ap.add_argument("--dump", default="", help="write u^K to PREFIX[.rankR].bin/.json")
     ap.add_argument("--checkpoint", default="", help="write u^{K-1}, u^K to PREFIX.prev / PREFIX.cur dumps")
-    ap.add_argument("--resume", default="", help="continue from a --checkpoint PREFIX (torch transport)")
+    ap.add_argument("--resume", default="", help="continue from a --checkpoint PREFIX (any backend/transport)")
     ap.add_argument("--force", action="store_true", help="run even if the CFL condition is violated")
     ap.add_argument("--quiet", action="store_true")
     return ap
@@ -73,8 +73,6 @@ def main(argv=None) -> int:
         backend = "hip" if torch.cuda.is_available() else "cpu"
     rank, world, local = init_process_group("gloo" if backend != "hip" or a.transport != "torch" else "nccl")
     transport = a.transport
-    if a.resume:
-        transport = "torch"
     kw = dict(backend=backend, transport=transport, decomp=a.decomp, overlap=not a.no_overlap,
               graph=not a.no_graph, threads=a.threads, force=a.force, temporal=1 if a.no_temporal else a.temporal, tb=not a.no_tb)
     if backend == "hip":
@@ -86,7 +84,7 @@ def main(argv=None) -> int:
     if a.resume:
         prev, meta = dumpio.load(a.resume + ".prev")
         cur, meta_c = dumpio.load(a.resume + ".cur")
-        s.native.set_state(torch.from_numpy(prev), torch.from_numpy(cur), int(meta_c["step"]))
+        s.set_state(prev, cur, int(meta_c["step"]))
     r = None
     times = []
     for i in range(a.warmup + a.repeat):

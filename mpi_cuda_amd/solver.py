@@ -177,6 +177,23 @@ class Solver:
                            {k: v for k, v in r.items() if k not in ("steps", "max_err", "rms_err", "solve_s",
                                                                     "finite")})
 
+    def set_state(self, prev, cur, step: int) -> None:
+        """Loaded-field start (resume): every following run() starts at ``step`` from u^{step-1} = prev and
+        u^{step} = cur (GLOBAL (N+1)³ float64 arrays or tensors, e.g. utils.dump.load of a checkpoint) and continues to
+        K, checking the steps after ``step``. Native backends take each rank's box and ghost layers from the global
+        fields (no exchange before the first pass); the result is bit-identical to an uninterrupted run."""
+        import numpy as np
+
+        if self.backend == "torch":
+            raise ValueError("the torch reference solver has no resume")
+        if self.transport == "torch":
+            to_t = (lambda a: a if isinstance(a, torch.Tensor) else torch.from_numpy(np.asarray(a)))
+            self._impl.set_state(to_t(prev), to_t(cur), int(step))
+            return
+        to_np = (lambda a: np.ascontiguousarray(a.cpu().numpy() if isinstance(a, torch.Tensor) else a,
+                                                dtype=np.float64).reshape(-1))
+        self._impl.set_state(to_np(prev), to_np(cur), int(step))
+
     @property
     def native(self):
         return self._impl

@@ -134,3 +134,21 @@ def test_mpi_program_under_external_launcher():
     assert lines == [l for l in seq.stdout.splitlines() if l.startswith("Step ")] and len(lines) == 3
     assert "max over 3 ranks" in outs[0][0]
     assert not os.path.exists(f"/dev/shm/wave3d-cpu-{job}")  # rank 0 unlinked the segment
+
+
+def test_cli_cpu_checkpoint_resume_bitexact(tmp_path):
+    """bin/wave3d --cpu: K=10 → --checkpoint → --resume to K=20 equals a direct K=20 run bit for bit (field dump) and
+    prints the same error lines for steps 12..20."""
+    import numpy as np
+
+    cli = os.path.join(ROOT, "bin", "wave3d")
+    run = lambda *a: subprocess.run([cli, *map(str, a)], check=True, capture_output=True, text=True,  # noqa: E731
+                                    cwd=tmp_path).stdout
+    run(40, 0.001, 10, 1, "--cpu", "--checkpoint", "c10")
+    resumed = run(40, 0.001, 20, 1, "--cpu", "--resume", "c10", "--dump", "r20")
+    direct = run(40, 0.001, 20, 1, "--cpu", "--dump", "d20")
+    assert np.array_equal(np.fromfile(tmp_path / "r20.bin"), np.fromfile(tmp_path / "d20.bin"))
+    steps = lambda out: [l for l in out.splitlines() if l.startswith("Step")]  # noqa: E731
+    assert steps(resumed) == [l for l in steps(direct) if int(l.split()[1].rstrip(",")) > 10]
+    meta = json.loads((tmp_path / "c10.prev.json").read_text())
+    assert meta["step"] == 9 and json.loads((tmp_path / "c10.cur.json").read_text())["step"] == 10

@@ -56,6 +56,9 @@ struct Args {
   bool autotune = false;               // --autotune: time the multi-rank schedule candidates, keep the fastest
   bool phases = false;                 // --phases: per-phase breakdown from a traced solve of the timed schedule
   std::string group_transport = "rccl-self";
+  std::string transport = "rccl";      // --transport rccl | push (slab LDS passes: halos pushed by the passes)
+  bool push_cp_wait = false;           // --push-cp-wait: push waits by the command processor (eager launches)
+  bool no_rccl = false;                // --no-rccl: ranks without a communicator (push rehearsal on one shared GPU)
   int t2_rows = 0, t2_target = -1, deep_min = -1, t2_occ = -1, tb_min = -1;
   bool force = false;
   int repeat = 1;
@@ -116,7 +119,12 @@ constexpr Personality kPersonalities[] = {
                "  --fake-rank R/P    perf study: time rank R of a P-rank decomposition alone on one GPU, no transport\n"
                "  --group P          all P ranks of the decomposition in this process on one GPU (rehearsal of the\n"
                "                     multi-rank path; --group-transport rccl-self (default: RCCL send/recv, each rank\n"
-               "                     over a one-rank communicator) or loopback (device copies))\n"
+               "                     over a one-rank communicator), loopback (device copies) or push)\n"
+               "  --transport T      rccl (default) | push: slab LDS passes store their face planes straight into the\n"
+               "                     neighbours' fine-grained staging over xGMI and signal them with flags (no exchange)\n"
+               "  --push-cp-wait     push: wait for the neighbours with hipStreamWaitValue32 (eager) instead of in-kernel\n"
+               "  --no-rccl          ranks without an RCCL communicator (push only; IPC handles through files; error\n"
+               "                     logs per rank): the multi-process push rehearsal on one shared GPU\n"
                "  --t2-rows R / --t2-target W   fused two-step kernel: rows per wave, x-chunking target (waves)\n"
                "  --repeat R / --warmup W   timed / untimed solves (report min and mean)\n"
                "  --bench-steps K    then K back-to-back solves between two sync+barriers (max over ranks)\n"
@@ -190,6 +198,9 @@ Args parse(int argc, char** argv) {
     else if (s == "--autotune") a.autotune = true;
     else if (s == "--phases") a.phases = true;
     else if (s == "--group-transport") a.group_transport = next();
+    else if (s == "--transport") a.transport = next();
+    else if (s == "--push-cp-wait") a.push_cp_wait = true;
+    else if (s == "--no-rccl") a.no_rccl = true;
     else if (s == "--repeat") a.repeat = std::stoi(next());
     else if (s == "--warmup") a.warmup = std::stoi(next());
     else if (s == "--tile-rows") a.tile_rows = std::stoi(next());
@@ -563,6 +574,9 @@ SolverOptions options_from(const Args& a, bool fake) {
   if (a.tb_threads > 0) o.tiling_tb.threads = a.tb_threads;
   o.init2 = a.init2;
   o.fake_comm = fake;
+  o.push = a.transport == "push";
+  // (ranks without a communicator have no end-of-solve collective: their flags must run on, CP waits)
+  o.push_cp_wait = a.push_cp_wait || a.no_rccl;
   if (a.t2_rows > 0) o.tiling2.rows = a.t2_rows;
   if (a.deep_min >= 0) o.deep_min_planes = a.deep_min;
   if (a.tb_min >= 0) o.tb_min_planes = a.tb_min;
@@ -629,12 +643,48 @@ struct Candidate {
   const char* decomp;
   int temporal;
   bool overlap;
+  bool push = false;  // slab LDS passes with the push transport (faces forwarded by the passes, flags)
 };
 constexpr Candidate kCandidates[] = {
-    {"slab-S4", "slab", 4, true},   {"slab-S4-seq", "slab", 4, false}, {"slab-S3", "slab", 3, true},
-    {"slab-S2", "slab", 2, true},   {"slab-S1", "slab", 1, true},      {"block-S4", "block", 4, true},
-    {"block-S3", "block", 3, true}, {"block-S1", "block", 1, true},
+    {"slab-S4", "slab", 4, true},          {"slab-S4-seq", "slab", 4, false},
+    {"slab-S4-push", "slab", 4, true, true}, {"slab-S4-push-seq", "slab", 4, false, true},
+    {"slab-S3", "slab", 3, true},          {"slab-S2", "slab", 2, true},
+    {"slab-S1", "slab", 1, true},          {"block-S4", "block", 4, true},
+    {"block-S3", "block", 3, true},        {"block-S1", "block", 1, true},
 };
+
+// Every rank's bytes through files next to the rendezvous file (ranks without a communicator: --no-rccl). Each rank
+// publishes <rdzv>.push<rank> atomically and reads the others' (written after this process started).
+std::vector<std::string> file_allgather(int rank, int world, const std::string& mine) {
+  static const double t_start = static_cast<double>(std::time(nullptr));
+  auto path = [](int r) { return rdzv_path() + ".push" + std::to_string(r); };
+  {
+    const std::string tmp = path(rank) + ".tmp";
+    std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
+    f.write(mine.data(), static_cast<std::streamsize>(mine.size()));
+    if (!f) fail("cannot write " + tmp);
+    f.close();
+    if (std::rename(tmp.c_str(), path(rank).c_str()) != 0) fail("cannot publish " + path(rank));
+  }
+  std::vector<std::string> all(static_cast<size_t>(world));
+  const double t0 = now_s();
+  for (int r = 0; r < world; ++r) {
+    for (;;) {
+      struct stat st {};
+      if (stat(path(r).c_str(), &st) == 0 && static_cast<double>(st.st_mtime) >= t_start - 60.0) {
+        std::ifstream f(path(r), std::ios::binary);
+        std::string b((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+        if (b.size() == mine.size()) {
+          all[static_cast<size_t>(r)] = b;
+          break;
+        }
+      }
+      if (now_s() - t0 > 120.0) fail("timed out waiting for " + path(r));
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    }
+  }
+  return all;
+}
 
 int run_gpu(const Args& a) {
   static const char* const kRank[] = {"RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID", nullptr};
@@ -660,7 +710,7 @@ int run_gpu(const Args& a) {
 
   std::shared_ptr<Comm> comm;
   const double t_comm0 = now_s();
-  if (world > 1 && !fake) {
+  if (world > 1 && !fake && !a.no_rccl) {
     W3D_REQUIRE(local < ndev || std::getenv("W3D_SHARE_GPUS"),
                 "rank " + std::to_string(rank) + " has local rank " + std::to_string(local) + " but only " +
                     std::to_string(ndev) + " GPU(s) are visible (RCCL needs one GPU per rank)");
@@ -680,17 +730,33 @@ int run_gpu(const Args& a) {
   };
   auto max_over_ranks = [&](double v) { return comm ? comm_allreduce(*comm, v, true) : v; };
 
+  W3D_REQUIRE(!a.no_rccl || world == 1 || fake || (a.transport == "push" && !a.autotune),
+              "--no-rccl: ranks without a communicator can only run the push transport (no autotune)");
+  // push transport: connect the slab neighbours (IPC handles through RCCL, or files without a communicator; a fake
+  // rank forwards into its own staging and waits for its own signals: the cost of the push without peers)
+  auto connect = [&](GpuSolver& g) {
+    if (!g.push()) return;
+    if (fake)
+      g.connect_push_self();
+    else
+      g.connect_push(comm ? comm_allgather_bytes(*comm, g.push_handles())
+                          : file_allgather(rank, world, g.push_handles()));
+  };
   std::unique_ptr<GpuSolver> s;
-  std::string sched = a.decomp + "-S" + std::to_string(a.temporal) + (a.overlap ? "" : "-seq");
+  std::string sched = a.decomp + "-S" + std::to_string(a.temporal) + (a.overlap ? "" : "-seq") +
+                      (a.transport == "push" ? "-push" : "");
   std::vector<std::pair<std::string, double>> tuned;
   if (a.autotune && (world > 1 || a.fake_rank < 0)) {
     double best_t = 1e30;
+    std::vector<double> ref_log;
     for (const Candidate& c : kCandidates) {
       if (std::string(c.decomp) == "block" && world < 4) continue;  // (2 ranks: "block" is the slab)
       SolverOptions o = base;
       o.decomp = c.decomp;
       o.temporal = c.temporal;
       o.overlap = c.overlap;
+      o.push = c.push;
+      if (c.push && world < 2) continue;
       std::unique_ptr<GpuSolver> cand;
       std::string err;
       try {
@@ -702,9 +768,19 @@ int run_gpu(const Args& a) {
         if (!err.empty()) std::fprintf(stderr, "[wave3d rank %d] candidate %s rejected: %s\n", rank, c.name, err.c_str());
         continue;
       }
+      connect(*cand);  // (collective when the candidate pushes: every rank built it)
       double t = 1e30;
-      cand->run();  // eager: RCCL peer connections
-      cand->run();  // graph capture
+      RunResult r0 = cand->run();  // eager: RCCL peer connections
+      r0 = cand->run();            // graph capture
+      // every schedule computes bit-identical fields: a candidate whose error log differs from the first accepted
+      // one's (a transport that delivered wrong ghosts) is rejected on every rank, whatever its speed
+      bool same = r0.finite && (ref_log.empty() || r0.max_err == ref_log);
+      if (!agree(same)) {
+        std::fprintf(stderr, "[wave3d rank %d] candidate %s rejected: its error log differs from the reference\n", rank,
+                     c.name);
+        continue;
+      }
+      if (ref_log.empty()) ref_log = r0.max_err;
       for (int k = 0; k < 3; ++k) {
         if (comm) comm_barrier(*comm);
         t = std::min(t, cand->run().solve_s);
@@ -720,6 +796,7 @@ int run_gpu(const Args& a) {
     W3D_REQUIRE(s != nullptr, "autotune: no candidate schedule could be built");
   } else {
     s = std::make_unique<GpuSolver>(a.prob, base, rank, world, comm);
+    connect(*s);
   }
 
   if (!a.resume.empty()) {
@@ -805,7 +882,8 @@ int run_gpu(const Args& a) {
         << ", \"hip_runtime\": " << hipv << ", \"gcell_per_s\": " << jnum(gcell)
         << ", \"graph\": " << (s->options().graph ? "true" : "false") << ", \"overlap\": "
         << (s->options().overlap ? "true" : "false") << ", \"temporal\": " << s->options().temporal
-        << ", \"schedule\": " << jstr(sched) << ", \"mode\": " << jstr(s->mode()) << ", \"device\": "
+        << ", \"schedule\": " << jstr(sched) << ", \"mode\": " << jstr(s->mode())
+        << ", \"transport\": " << jstr(s->push() ? "push" : world > 1 ? "rccl" : "none") << ", \"device\": "
         << jstr(prop.gcnArchName) << ", \"bench_steps\": " << a.bench_steps << ", \"bench_s\": " << jnum(bench_s)
         << ", \"warmup\": " << a.warmup << ", \"finite\": " << (r.finite ? "true" : "false") << ", \"autotune_s\": {";
       for (size_t i = 0; i < tuned.size(); ++i) j << (i ? ", " : "") << jstr(tuned[i].first) << ": " << jnum(tuned[i].second);
@@ -833,6 +911,7 @@ int run_gpu(const Args& a) {
   if (!a.dump.empty()) write_dump(a.dump, a.prob, s->layout(), s->download(0), rank, world, d);
   if (!a.checkpoint.empty())
     write_checkpoint(a.checkpoint, a.prob, s->layout(), s->download(0), s->download(1), rank, world, d);
+  if (s->push() && !comm && !fake) std::remove((rdzv_path() + ".push" + std::to_string(rank)).c_str());
   return r.finite ? 0 : 3;
 }
 

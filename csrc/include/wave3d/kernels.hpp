@@ -83,18 +83,48 @@ struct LeapfrogTbTiling {
   int target_blocks = 256; // fewer (y,z) tiles than this: split x into chunks (one workgroup per CU at 1 WG/CU)
   int min_chunk = 16;      // ... of at least this many planes (each chunk recomputes S−1 planes on both sides)
 };
+// Slab peer-push transport of an LDS pass (x faces only; every slab rank has the same plane geometry, so a plane's
+// in-plane offsets are the same on both sides). The pass
+//   * marches the upper face segment [x1 − T, x1) first, then [x0, x1 − T) (faces_first), so both face regions are
+//     produced at the start of the pass;
+//   * stores u^{n+S} of planes [0, T) / [nx − T, nx) and u^{n+S−1} of planes [0, T−1) / [nx − T + 1, nx) a second time,
+//     straight into the lower / upper neighbour's staging over xGMI (fwd2 / fwd1: the neighbour's staging plane 0 of
+//     the matching side and pass parity; nullptr: no neighbour);
+//   * reads its own ghost planes [−T, 0) / [nx, nx + T) of u^n and u^{n−1} from its staging (gcur / gprev, plane 0 =
+//     ghost plane −T resp. nx) instead of the field buffers;
+//   * waits (wait_epoch > 0) for both neighbours' flags to reach wait_epoch before its first load, and raises its slot
+//     in both neighbours' flags (rflag) to signal_epoch once every workgroup's stores are visible (the workgroup that
+//     brings `done` to done_target).
+struct TbPush {
+  int on = 0, faces_first = 0;
+  int T = 0;                          // ghost depth (planes) = the deepest pass
+  int nx = 0;                         // this rank's planes
+  double* fwd1[2] = {nullptr, nullptr};        // [lo, hi] neighbour staging for u^{n+S−1}
+  double* fwd2[2] = {nullptr, nullptr};        // ... for u^{n+S}
+  const double* gprev[2] = {nullptr, nullptr}; // own staging holding the ghost planes of u^{n−1} [lo, hi]
+  const double* gcur[2] = {nullptr, nullptr};  // ... of u^n
+  unsigned* flags = nullptr;          // own flags: [0] raised by the lower neighbour, [1] by the upper
+  unsigned* rflag[2] = {nullptr, nullptr};     // this rank's slot in the lower / upper neighbour's flags
+  int wait_side[2] = {0, 0};
+  unsigned wait_epoch = 0, signal_epoch = 0;
+  unsigned* done = nullptr;           // workgroups done (local counter, zeroed per solve)
+  unsigned done_target = 0;
+  unsigned* status = nullptr;         // set to 1 when a wait timed out
+  unsigned long long spin_ticks = 0;  // wait bound (100 MHz wall clock)
+};
+
 // Stage-real ranges of an LDS pass: per axis, where the intermediate levels hold real values (S−1 nodes into the
 // S-deep ghosts towards neighbouring ranks); lo > hi: the axis default (x: compute box, y/z: no restriction).
 inline LBox tb_default_real() { return LBox{1, 0, 1, 0, 1, 0}; }
 // Raise the dynamic-LDS limit of every instantiation (call before capturing launches into a graph).
-void leapfrog_tb_prepare();
+void leapfrog_tb_prepare(bool push = false);  // push: also the push-transport instantiations
 size_t leapfrog_tb_lds_bytes(int stages);
 int leapfrog_tb_partials(const Layout& l, const LBox& box, const LeapfrogTbTiling& t);
 void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
                         double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
                         Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream,
                         const LBox& real = tb_default_real(), bool analytic_start = false, int level_stride = 0,
-                        int grid_blocks = 0);
+                        int grid_blocks = 0, const TbPush* push = nullptr);
 
 // Error of a stored field vs φ·ct over `box` (step 1 / standalone check). Writes leapfrog-compatible partials and
 // returns how many.

@@ -53,6 +53,15 @@ struct SolverOptions {
   // Slab ranks use the LDS multi-step passes (deep-tb) when every rank owns at least this many x-planes (and at least
   // 2·temporal: each pass first computes the `steps` planes next to each neighbour, the shells that are sent).
   int tb_min_planes = 16;
+  // Slab LDS passes (deep-tb) only: the "push" halo transport. Each pass stores the face planes its neighbours read as
+  // ghosts a second time, straight into their fine-grained staging over xGMI (TbPush, kernels.hpp): no exchange phase,
+  // no RCCL kernels competing for CUs, no shell launches; with `overlap` the pass produces both face regions first so
+  // the remote stores drain while it marches on. Cross-rank order: flags in uncached memory, raised at the end of a
+  // pass and waited for at the start of the next one (in the kernel; push_cp_wait: by the command processor with
+  // hipStreamWaitValue32 — eager launches only, for ranks that share one GPU). Peers are connected with
+  // connect_push() (multi-process: IPC handles) or by a GpuGroup.
+  bool push = false;
+  bool push_cp_wait = false;
 };
 
 // Summed device time per phase of the last run() (SolverOptions::timers). compute = interior / whole-box / fused
@@ -139,6 +148,12 @@ class GpuSolver {
   // "single-step" | "fused-single" (temporal blocking, one rank) | "deep-tb" (LDS multi-step passes, slab ranks)
   // | "deep-halo" (two-step passes, slab ranks)
   std::string mode() const;
+  // push transport: this rank's staging + flag IPC handles (opaque bytes), and connecting to the neighbours from
+  // every rank's handles (index = rank); GpuGroup ranks are connected in-process instead
+  bool push() const { return push_; }
+  std::string push_handles() const;
+  void connect_push(const std::vector<std::string>& all);
+  void connect_push_self();  // perf study (fake rank): forward into the own staging, wait for the own signals
 
  private:
   friend class GpuGroup;
@@ -230,6 +245,7 @@ class GpuSolver {
   Partial* errall_ = nullptr;    // [world][K+1]
   std::vector<double> ct_;       // cos(a_t n τ)
   hipStream_t s0_ = nullptr, s1_ = nullptr;
+  bool own_s0_ = true;  // false: a GpuGroup "push" rank on the group's shared compute stream
   hipEvent_t ev_shell_ = nullptr, ev_halo_ = nullptr, ev_packed_ = nullptr;
   int n_full_ = 0, n_shell_ = 0, n_int_ = 0, n_fused_ = 0;  // error partials of each launch kind
   int n_tb_ = 0;                                            // ... per level of a k_leapfrog_tb pass
@@ -266,6 +282,18 @@ class GpuSolver {
   void timed(int phase, hipStream_t st, F&& f);
   void collect_phases(RunResult& r);
   void poison(hipStream_t st);
+  // push transport (slab deep-tb)
+  bool push_ = false;
+  double* stg_ = nullptr;       // [parity][field (0: u^{n+S−1}, 1: u^{n+S})][side (0: lo ghosts, 1: hi)][T planes]
+  unsigned* flags_ = nullptr;   // uncached: [0] raised by the lower neighbour, [1] by the upper, [4] timeout, [8] done
+  double* peer_stg_[2] = {nullptr, nullptr};   // neighbours' staging (lo, hi)
+  unsigned* peer_flags_[2] = {nullptr, nullptr};
+  bool peer_ipc_[2] = {false, false};          // opened with hipIpcOpenMemHandle (closed in the destructor)
+  int push_epoch_ = 0;                         // passes of the earlier solves (push_cp_wait: epochs run on)
+  i64 stg_off(int par, int field, int side) const { return ((par * 2 + field) * 2 + side) * lay_.xg * lay_.plane; }
+  void connect_push_peer(int side, double* stg, unsigned* flags, bool ipc);
+  void push_finish(hipStream_t st);  // end of a solve: zero this rank's flags (after its last wait)
+  void push_check();                 // after a solve: fail if a wait timed out
 };
 
 }  // namespace wave3d
@@ -314,6 +342,8 @@ class GpuGroup {
 
 // Host-scalar collectives over the RCCL communicator (timer max-reduction, barriers). Blocking.
 double comm_allreduce(const Comm& c, double v, bool max_op);
+// Every rank's bytes (equal sizes), in rank order, through ncclAllGather. Blocking.
+std::vector<std::string> comm_allgather_bytes(const Comm& c, const std::string& mine);
 int rccl_version();  // ncclGetVersion of the RCCL resolved at run time
 // Whether this process's HIP runtime captures the multi-rank (multi-stream) schedules correctly (HIP >= 7.2).
 bool multistream_capture_safe();

@@ -30,721 +30,14 @@
 // passes, deeper prefetch, half tiles, branch-free selects, a conflict-free position order) are documented with their
 // numbers in profiles/r1_tb_queue_experiments.md. The pass
 // semantics (which plane of which level each stage reads) are mirrored by tools/tb_emulate.py (CPU tests).
-#include <hip/hip_runtime.h>
-
-#include <string>
-#include <type_traits>
-
-#include "wave3d/kernels.hpp"
-#include "wave3d/stencil.hpp"
+#include "wave3d/leapfrog_tb_kernel.hpp"
 
 namespace wave3d {
 
-namespace {
+using namespace tbk;
 
-constexpr int kTile = 32;  // tile edge (y and z)
-
-__device__ __forceinline__ void wave_reduce(double& m, double& s) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    const double om = __shfl_xor(m, o, 64);
-    const double os = __shfl_xor(s, o, 64);
-    m = om > m ? om : m;
-    s = s + os;
-  }
-}
-
-struct TbParams {
-  const double* prev;  // u^{n−1}
-  const double* cur;   // u^n
-  double* out1;        // u^{n+S−1}
-  double* out2;        // u^{n+S}
-  const double* s;     // sin table, global index −1..N+1
-  Partial* partials;   // stage k's block of nblocks partials at (k−1)·lstride (checked stages only)
-  i64 plane, pitch, zs;
-  int x0, x1;          // output x range (local)
-  int xlen, nxc;       // x chunk length and chunk count (block c marches [x0 + c·xlen, min(x1, x0 + (c+1)·xlen)))
-  int sx0, sx1;        // x range where stage outputs are real (outside: Dirichlet 0)
-  int ax0, ax1;        // allocated x range (local planes that may be read)
-  int sy0, sy1, sz0, sz1;  // y / z ranges where stage outputs are real (3-D block ranks; whole planes: everything)
-  int ay0, ay1, az0, az1;  // allocated y / z ranges (ghosts included)
-  int zero_off;            // in-plane offset of the zero slot (Layout::zero_off)
-  int yg, zg;              // y / z ghost depths (in-plane offsets count from the plane start)
-  int N, gx0, gy0, gz0;
-  int y0, y1, z0, z1;  // output (y, z) range (local)
-  double ihx2, ihy2, ihz2, tau2, half_tau2;
-  double ct[4];        // time factor of u^{n+k} (k = 1..S) for the check
-  int check_mask;      // bit k−1: check u^{n+k}
-  int nty, ntz, nblocks, xcd_remap;
-  int lstride;         // partials between consecutive levels (≥ nblocks; larger when several launches share a level)
-  int bby, bbz;        // > 0: each XCD's tiles form a bby × bbz block of the tile grid (else two-row strips)
-};
-
-template <int S, int T, int NT>
-struct TbGeom {
-  static constexpr int H1 = T + 2 * (S - 1);  // stage-1 region edge: the thread-owned positions
-  static constexpr int NP = H1 * H1;
-  static constexpr int Q = (NP + NT - 1) / NT;  // positions per thread
-  static constexpr int W0 = T + 2 * S;          // u^n region edge = LDS plane edge (all levels share the indexing)
-  static constexpr int PL = W0 * W0;
-  static constexpr int NR = PL - NP;            // u^n halo ring (not thread-owned)
-  // plane stride in LDS: the plane plus a pad holding a dummy node (and its 4 neighbours) for lanes without a position
-  static constexpr int PLP = PL + 2 * W0 + 2;
-  static constexpr int DUMMY = PL + W0 + 1;
-  static constexpr int QR = (NR + NT - 1) / NT;
-  // levels 0..S−1 × 2 parity slots; the analytic start adds a φ level (two parity slots) after them
-  static constexpr int lds_doubles(bool init = false) { return (S + (init ? 1 : 0)) * 2 * PLP; }
-};
-
-// + sin tables (error check, analytic start): y and z over the u^n region ± 1, x over the planes the pass touches ± 1.
-// In LDS because a global load of the per-plane x factor would be a vector load (the table may alias the outputs, so
-// no scalar load) whose wait drains the prefetch queue. nxo = tb_nx_table(x1 − x0) or 0 (no table needed).
-template <int S, int T, int NT, bool INIT = false>
-constexpr size_t tb_lds_bytes(int nxo = 0) {
-  return (static_cast<size_t>(TbGeom<S, T, NT>::lds_doubles(INIT)) + (2 + 2 * S) * (T + 2 * S + 2) +
-          static_cast<size_t>(nxo)) *
-         sizeof(double);
-}
-template <int S>
-constexpr int tb_nx_table(int nx_box) {
-  return nx_box + 2 * S + 4;
-}
-
-// CM: compile-time superset of the levels that may be checked (bit k−1 ↔ u^{n+k}); levels outside it carry no error
-// accumulators or check code (registers: the S = 4 kernel sits at the 128-VGPR limit of 4 waves per SIMD).
-// INIT: analytic start at n = 1 — u^{n−1} = u⁰ = φ and u^n = u¹ = u⁰ + τ²/2·Δ_h u⁰ are computed from the sin tables
-// (k_init_first's formulas and operation order) instead of loaded: the pass reads nothing from HBM.
-// CH: x-chunked launch (small boxes). Without it the block's x range is the kernel argument itself, which the compiler
-// re-reads instead of keeping live (measured: a computed range costs the S = 4 kernel 5 % in extra spills).
-template <int S, int T, int NT, int CM, bool INIT, bool CH>
-__global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
-  using G = TbGeom<S, T, NT>;
-  constexpr int Q = G::Q, QR = G::QR, H1 = G::H1, W0 = G::W0, PLP = G::PLP;
-  constexpr int kOwn = 1 << 30;   // gof flag: tile node inside the output box
-  constexpr int kReal = 1 << 29;  // gof flag: stage values are real at this node (interior ∩ stage-real range)
-  constexpr int kLd = 1 << 28;    // gof flag: node inside the global interior and the allocation (loaded)
-  constexpr int kOff = kLd - 1;   // gof bits of the in-plane offset
-  extern __shared__ double lds[];
-  const int tid = static_cast<int>(threadIdx.x);
-  int blk = static_cast<int>(blockIdx.x);
-  if (p.xcd_remap) blk = (blk & 7) * (p.nblocks >> 3) + (blk >> 3);
-  const int ntiles = p.nty * p.ntz;
-  const bool active = blk < ntiles * (CH ? p.nxc : 1);
-  // chunk-major: consecutive blocks (one XCD after the remap) are neighbouring tiles of one x chunk
-  const int chunk = (CH && active) ? blk / ntiles : 0;
-  if constexpr (CH) blk -= chunk * ntiles;
-  int tzi = active ? blk % p.ntz : 0, tyi = active ? blk / p.ntz : 0;
-  if (p.bby > 0) {  // XCD x (= blk / per after the remap) owns block x of the tile grid: halo re-reads stay in its L2
-    const int per = p.bby * p.bbz, x = blk / per, w = blk - x * per, nbz = p.ntz / p.bbz;
-    tyi = (x / nbz) * p.bby + w / p.bbz;
-    tzi = (x - (x / nbz) * nbz) * p.bbz + (w - (w / p.bbz) * p.bbz);
-  }
-  const int ty0 = p.y0 + tyi * T, tz0 = p.z0 + tzi * T;
-  const int x0 = CH ? p.x0 + chunk * p.xlen : p.x0;  // this block's output x range
-  const int x1 = CH ? imin(p.x1, x0 + p.xlen) : p.x1;
-  const int N = p.N;
-  const i64 P = p.plane;
-  // in-plane offsets count from the plane's first element (always ≥ 0, also for the y/z ghosts of block ranks):
-  // node (y, z) at (y + yg)·pitch + z + zg + zs; the field pointers are offset by (xg − 1) planes only
-  const int R = static_cast<int>(p.pitch), ya = p.yg, za = p.zg + static_cast<int>(p.zs);
-  const double tau2 = p.tau2;  // = τ²/h² (the coefficient of d2sum)
-  auto inside = [&](int g) { return static_cast<unsigned>(g - 1) < static_cast<unsigned>(N - 1); };
-  auto in_rng = [](int v, int lo, int hi) { return static_cast<unsigned>(v - lo) < static_cast<unsigned>(hi - lo); };
-
-  double emax[S], esum[S];
-#pragma unroll
-  for (int k = 0; k < S; ++k) emax[k] = esum[k] = 0.0;
-
-  if (active) {
-    // ---- per-thread descriptors of the owned positions (stage-1 region coordinates a, b ∈ [0, H1))
-    const int zero_off = p.zero_off;
-    int lid[Q];   // LDS index (u^n-region coordinates a+1, b+1); the pad's dummy node for lanes without a position
-    int gof[Q];   // in-plane offset to load (zero node outside the interior) | kReal | kOwn
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int idx = tid + q * NT;
-      const int a = idx / H1, b = idx - (idx / H1) * H1;
-      const int y = ty0 - (S - 1) + a, z = tz0 - (S - 1) + b;
-      const bool valid = idx < G::NP;
-      // u^n / u^{n−1} are loaded wherever the rank holds them (its neighbours' ghost values included); the stage
-      // values are real only in the stage-real range (S−1 into the ghosts)
-      const bool ld = valid && inside(p.gy0 + y) && inside(p.gz0 + z) && in_rng(y, p.ay0, p.ay1) &&
-                      in_rng(z, p.az0, p.az1);
-      const bool real = ld && in_rng(y, p.sy0, p.sy1) && in_rng(z, p.sz0, p.sz1);
-      const bool own = real && a >= S - 1 && a < S - 1 + T && b >= S - 1 && b < S - 1 + T && y < p.y1 && z < p.z1;
-      lid[q] = valid ? (a + 1) * W0 + (b + 1) : G::DUMMY;
-      gof[q] = ld ? (((y + ya) * R + z + za) | kLd | (real ? kReal : 0) | (own ? kOwn : 0)) : zero_off;
-    }
-    // wave-uniform stage masks: bit k−1 of wsm[q] is set when some lane of this wave's position set q lies inside stage
-    // k's region (rows [k−1, H1−k+1) of the stage-1 region); other (wave, q, stage) combinations are skipped with a
-    // scalar branch (at 32² tiles and S = 4, 9 of 16 waves hold no position at all in their second set)
-    int wsm[Q];
-    {
-      const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const int first = wbase + q * NT, last = imin(first + 63, G::NP - 1);
-        int m = 0;
-        if (first < G::NP) {
-          const int rlo = first / H1, rhi = last / H1;
-#pragma unroll
-          for (int k = 1; k <= S; ++k)
-            if (rhi >= k - 1 && rlo < H1 - (k - 1)) m |= 1 << (k - 1);
-        }
-        wsm[q] = __builtin_amdgcn_readfirstlane(m);
-      }
-    }
-    // u^n halo ring: LDS index (dummy: no ring node) and global offset (zero node outside the interior)
-    int lrid[QR], grof[QR];
-#pragma unroll
-    for (int r = 0; r < QR; ++r) {
-      const int ridx = tid + r * NT;
-      int a0 = 0, b0 = 0;
-      if (ridx < W0) {
-        b0 = ridx;
-      } else if (ridx < 2 * W0) {
-        a0 = W0 - 1;
-        b0 = ridx - W0;
-      } else if (ridx < 3 * W0 - 2) {
-        a0 = 1 + ridx - 2 * W0;
-      } else {
-        a0 = 1 + ridx - (3 * W0 - 2);
-        b0 = W0 - 1;
-      }
-      const int y = ty0 - S + a0, z = tz0 - S + b0;
-      const bool valid = ridx < G::NR;
-      lrid[r] = valid ? a0 * W0 + b0 : G::DUMMY;
-      grof[r] = (valid && inside(p.gy0 + y) && inside(p.gz0 + z) && in_rng(y, p.ay0, p.ay1) && in_rng(z, p.az0, p.az1))
-                    ? ((y + ya) * R + z + za) | kLd
-                    : zero_off;
-    }
-    // sin tables: syw[j] = s[y] for y = ty0 − S − 1 + j (the u^n region ± 1), szw likewise, sxw[i] = s[x] for
-    // x = x0 − S − 1 + i; indices clamped into −1..N+1 (only nodes of the interior, and their neighbours, use them)
-    constexpr int NYW = T + 2 * S + 2;
-    double* syw = lds + G::lds_doubles(INIT);
-    double* szw = syw + NYW;
-    double* rowt = szw + NYW;  // per checked level, two plane-parity slots of NYW row factors s_x·s_y
-    double* sxw = rowt + 2 * S * NYW;
-    if (p.check_mask || INIT) {
-      auto sc = [&](int g) { return p.s[g < -1 ? -1 : g > N + 1 ? N + 1 : g]; };
-      for (int t = tid; t < NYW; t += NT) {
-        syw[t] = sc(p.gy0 + ty0 - S - 1 + t);
-        szw[t] = sc(p.gz0 + tz0 - S - 1 + t);
-      }
-      for (int i = tid; i < tb_nx_table<S>(x1 - x0); i += NT) sxw[i] = sc(p.gx0 + x0 - S - 1 + i);
-      __syncthreads();
-    }
-    // table indices of an LDS position li (u^n-region coordinates): y ↔ li / W0 + 1, z ↔ li % W0 + 1 (the pad's dummy
-    // node is clamped into the table)
-    auto ytab = [&](int li) { return imin(li / W0 + 1, W0); };
-    auto ztab = [&](int li) { return li - (li / W0) * W0 + 1; };
-    const int xtab0 = S + 1 - x0;  // x ↔ sxw[x + xtab0]
-    // analytic u⁰ = φ and u¹ at plane x, LDS position li (INIT)
-    auto phi_at = [&](int x, int li) {
-      return (sxw[x + xtab0] * syw[ytab(li)]) * szw[ztab(li)];
-    };
-    auto u1_at = [&](int x, int li, bool real_yz) {
-      const int xi = x + xtab0, ya = ytab(li), zb = ztab(li);
-      const double sxc = sxw[xi], sy = syw[ya], sz = szw[zb];
-      const double cy = sxc * sy;
-      const double c = cy * sz;
-      const double lap = d2sum(c, (sxw[xi - 1] * sy) * sz, (sxw[xi + 1] * sy) * sz, (sxc * syw[ya - 1]) * sz,
-                              (sxc * syw[ya + 1]) * sz, cy * szw[zb - 1], cy * szw[zb + 1]);
-      return (real_yz && inside(p.gx0 + x)) ? first_step(c, lap, p.half_tau2) : 0.0;
-    };
-
-    // ---- register queues: plane x of level j at slot (x − i0) & 3; u^{n−1} and the ring: slot (x − i0) & 1
-    // Stages also run on the positions outside their (shrinking) region: those values are never read by a node
-    // inside the region (its neighbours lie in the previous stage's region), and skipping them per lane costs more
-    // exec-mask branching than the arithmetic. Zero-initialised so every value is defined.
-    double L[S][Q][4] = {};  // L[0] = u^n, L[k] = u^{n+k} (k < S)
-    double Lm[Q][2] = {};    // u^{n−1}
-    double Rg[QR][2] = {};   // u^n ring
-    const int i0 = x0 - S + 1, i1 = x1 + S - 2;
-    auto lds_plane = [&](int j, int par) { return lds + (j * 2 + par) * PLP; };
-
-    // plane x of u^n: owned positions into L[0][q][slot], ring into Rg[r][rs]
-    const int wbase_r = __builtin_amdgcn_readfirstlane(tid & ~63);
-    auto load_cur = [&](auto slot_c, auto rs_c, int x) {
-      constexpr int slot = decltype(slot_c)::value, rs = decltype(rs_c)::value;
-      if constexpr (INIT) {
-#pragma unroll
-        for (int q = 0; q < Q; ++q)
-          if (wsm[q]) L[0][q][slot] = u1_at(x, lid[q], gof[q] & kLd);
-#pragma unroll
-        for (int r = 0; r < QR; ++r)
-          if (wbase_r + r * NT < G::NR) Rg[r][rs] = u1_at(x, lrid[r], grof[r] & kLd);
-      } else {
-        const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;  // always an allocated plane
-        const double* base = p.cur + static_cast<i64>(xs + 1) * P;
-#pragma unroll
-        for (int q = 0; q < Q; ++q)
-          if (wsm[q]) L[0][q][slot] = base[gof[q] & kOff];
-#pragma unroll
-        for (int r = 0; r < QR; ++r) Rg[r][rs] = base[grof[r] & kOff];
-      }
-    };
-    auto load_prev = [&](auto slot_c, int x) {
-      constexpr int slot = decltype(slot_c)::value;
-      if constexpr (INIT) {
-#pragma unroll
-        for (int q = 0; q < Q; ++q)
-          if (wsm[q]) Lm[q][slot] = phi_at(x, lid[q]);
-      } else {
-        const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
-        const double* base = p.prev + static_cast<i64>(xs + 1) * P;
-#pragma unroll
-        for (int q = 0; q < Q; ++q)
-          if (wsm[q]) Lm[q][slot] = base[gof[q] & kOff];
-      }
-    };
-    auto commit_cur = [&](auto slot_c, auto rs_c, int par) {
-      constexpr int slot = decltype(slot_c)::value, rs = decltype(rs_c)::value;
-      double* d = lds_plane(0, par);
-#pragma unroll
-      for (int q = 0; q < Q; ++q)
-        if (wsm[q]) d[lid[q]] = L[0][q][slot];
-#pragma unroll
-      for (int r = 0; r < QR; ++r) d[lrid[r]] = Rg[r][rs];
-    };
-
-    // ---- analytic start, φ stage: φ = (s_x·s_y)·s_z is computed once per node and plane (2 products with the
-    // node's y/z factors held in registers) into a φ plane of LDS (two parity slots after the S levels); u¹ of the
-    // owned positions is then first_step(φ, Δ_h φ) with the y/z neighbours from that plane and the x neighbours from
-    // the thread's own entries of both φ slots. Every neighbour value is the product u1_at forms for it, so u¹ is
-    // bit-identical to k_init_first's; 2 products + 4 LDS reads instead of 12 products + 9 table reads per node.
-    // The halo ring (no φ neighbours beyond it in LDS) keeps u1_at.
-    // (S = 4: the queues leave no room for them — the factors are re-read from the LDS tables per use instead)
-    constexpr bool kFacReg = S < 4;
-    double fy[Q], fz[Q], fyr[QR], fzr[QR];
-    // (the check's z factor of a position is re-read from the LDS table per use: keeping it in a register per position
-    // spills at S = 4 since the y/z stage-real ranges of the block ranks were added)
-    auto fyq = [&](int q) { return kFacReg ? fy[q] : syw[ytab(lid[q])]; };
-    auto fzq = [&](int q) { return kFacReg ? fz[q] : szw[ztab(lid[q])]; };
-    auto fyrr = [&](int r) { return kFacReg ? fyr[r] : syw[ytab(lrid[r])]; };
-    auto fzrr = [&](int r) { return kFacReg ? fzr[r] : szw[ztab(lrid[r])]; };
-    if constexpr (INIT && kFacReg) {
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        fy[q] = syw[ytab(lid[q])];
-        fz[q] = szw[ztab(lid[q])];
-      }
-#pragma unroll
-      for (int r = 0; r < QR; ++r) {
-        fyr[r] = syw[ytab(lrid[r])];
-        fzr[r] = szw[ztab(lrid[r])];
-      }
-    }
-    auto lds_phi = [&](int par) { return lds + (S * 2 + par) * PLP; };
-    // φ of plane x (owned positions and ring) into φ slot `par`
-    auto phi_plane = [&](int x, int par) {
-      double* d = lds_phi(par);
-      const double sx = sxw[x + xtab0];
-#pragma unroll
-      for (int q = 0; q < Q; ++q)
-        if (wsm[q]) d[lid[q]] = (sx * fyq(q)) * fzq(q);
-#pragma unroll
-      for (int r = 0; r < QR; ++r)
-        if (wbase_r + r * NT < G::NR) d[lrid[r]] = (sx * fyrr(r)) * fzrr(r);
-    };
-    // iteration i of the analytic pass (F = (i − i0) & 3): u¹ of plane i+2 into L[0] slot (F+2)&3 / Rg slot (F+2)&1,
-    // u⁰ = φ of plane i+1 into Lm slot (F+1)&1; φ of plane i+3 into its slot. φ slot (i+2)&1 was completed in the
-    // previous iteration (behind this iteration's barrier); slot (i+3)&1 still holds this thread's φ(i+1) entries,
-    // read before they are overwritten.
-    auto init_iter = [&](auto fc, int i) {
-      constexpr int F = decltype(fc)::value;
-      double* p3 = lds_phi((F + 3) & 1);
-      const double* p2 = lds_phi((F + 2) & 1);
-      const double sx3 = sxw[i + 3 + xtab0];
-      const bool xin = inside(p.gx0 + i + 2);
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        if (!wsm[q]) continue;  // wave-uniform
-        const int li = lid[q];
-        const double f1 = p3[li];                    // φ(i+1), own entry
-        const double f3 = (sx3 * fyq(q)) * fzq(q);   // φ(i+3)
-        p3[li] = f3;
-        const double c = p2[li];                     // φ(i+2)
-        const double lap = d2sum(c, f1, f3, p2[li - W0], p2[li + W0], p2[li - 1], p2[li + 1]);
-        L[0][q][(F + 2) & 3] = ((gof[q] & kLd) && xin) ? first_step(c, lap, p.half_tau2) : 0.0;
-        Lm[q][(F + 1) & 1] = f1;
-      }
-#pragma unroll
-      for (int r = 0; r < QR; ++r) {
-        if (wbase_r + r * NT < G::NR) {
-          p3[lrid[r]] = (sx3 * fyrr(r)) * fzrr(r);
-          Rg[r][(F + 2) & 1] = u1_at(i + 2, lrid[r], grof[r] & kLd);
-        }
-      }
-    };
-
-    // stage k at plane xp; D = (xp − i0) & 3 (static), parity of xp = D & 1
-    // BK (bulk): plane xp is real and owned for every stage (the x tests are compile-time true)
-    auto stage = [&](auto kc, auto dc, auto bkc, int xp) {
-      constexpr int k = decltype(kc)::value, D = decltype(dc)::value;
-      constexpr bool BK = decltype(bkc)::value;
-      constexpr int sm = (D + 3) & 3, s0 = D, sp = (D + 1) & 3;
-      const double* nb = lds_plane(k - 1, D & 1);
-      double* dst = lds_plane(k < S ? k : 0, D & 1);
-      const bool xreal = BK || (xp >= p.sx0 && xp < p.sx1 && inside(p.gx0 + xp));
-      const bool xown = BK || (xp >= x0 && xp < x1);
-      constexpr bool kChk = (CM >> (k - 1)) & 1;
-      const bool chk = kChk && ((p.check_mask >> (k - 1)) & 1);
-      double* outp = (k == S ? p.out2 : p.out1) + static_cast<i64>(xp + 1) * P;
-      // the check's (s_x·s_y) row factor of plane xp, tabulated one iteration ahead (row_tables), slot F & 1
-      const double* rowk = rowt + ((k - 1) * 2 + ((D + k - 1) & 1)) * NYW;
-      (void)xown;
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        if (!((wsm[q] >> (k - 1)) & 1)) continue;  // wave-uniform
-        const int li = lid[q];
-        const double c = L[k - 1][q][s0];
-        const double lap = d2sum(c, L[k - 1][q][sm], L[k - 1][q][sp], nb[li - W0], nb[li + W0], nb[li - 1], nb[li + 1]);
-        double o;
-        if constexpr (k == 1)
-          o = Lm[q][D & 1];
-        else
-          o = L[k - 2][q][s0];
-        const int g = gof[q];
-        const double v = (xreal && (gof[q] & kReal)) ? leapfrog(c, o, lap, tau2) : 0.0;
-        if constexpr (k < S) {
-          L[k][q][s0] = v;
-          dst[li] = v;
-        }
-        const bool own = xown && (g & kOwn);
-        if constexpr (k >= S - 1) {
-          if (own && xreal) {
-            __builtin_nontemporal_store(v, outp + (g & kOff));
-          }
-        }
-        if constexpr (kChk) {
-          if (chk && own && xreal) {
-            const double e = fabs(v - (rowk[ytab(li)] * szw[ztab(li)]) * p.ct[k - 1]);
-            emax[k - 1] = fmax(e, emax[k - 1]);  // = (e > m ? e : m) for every non-NaN e; a NaN shows in the sum
-            esum[k - 1] += e * e;
-          }
-        }
-      }
-    };
-
-    // check row factors: rowt[k][slot][j] = s_x(plane of stage k) · s_y(j), the first product of the check's
-    // ((s_x·s_y)·s_z)·ct (same operands and order: bit-identical), tabulated once per plane by the first NYW threads
-    // instead of once per node; iteration i fills slot ((i − i0) + 1) & 1 for the planes its successor checks
-    auto row_tables = [&](int i, int slot) {
-      if constexpr (CM != 0) {
-        if (p.check_mask && tid < NYW) {
-#pragma unroll
-          for (int k = 1; k <= S; ++k)
-            if (((CM & p.check_mask) >> (k - 1)) & 1)
-              rowt[((k - 1) * 2 + slot) * NYW + tid] = sxw[imax(i - (k - 1) + xtab0, 0)] * syw[tid];
-        }
-      }
-    };
-
-    // iteration i with phase F = (i − i0) & 3
-    auto iteration = [&](auto fc, auto bkc, int i) {
-      constexpr int F = decltype(fc)::value;
-      constexpr bool BK = decltype(bkc)::value;
-      __syncthreads();  // every read of the slots overwritten below (iteration i−1) is done; i−1's writes visible
-      row_tables(i + 1, (F + 1) & 1);
-      commit_cur(std::integral_constant<int, (F + 1) & 3>{}, std::integral_constant<int, (F + 1) & 1>{},
-                 (F + 1) & 1);  // u^n plane i+1 → LDS (loaded one iteration ago)
-      if constexpr (INIT) {
-        init_iter(fc, i);
-      } else {
-        load_cur(std::integral_constant<int, (F + 2) & 3>{}, std::integral_constant<int, (F + 2) & 1>{}, i + 2);
-        load_prev(std::integral_constant<int, (F + 1) & 1>{}, i + 1);
-      }
-#define W3D_TB_STAGE(K)                                                                                          \
-  if constexpr (K <= S) {                                                                                        \
-    const int xp = i - (K - 1);                                                                                  \
-    if (BK || (xp >= x0 - (S - K) && xp < x1 + (S - K)))                                                         \
-      stage(std::integral_constant<int, K>{}, std::integral_constant<int, (F - (K - 1) + 8) & 3>{}, bkc, xp);    \
-  }
-      W3D_TB_STAGE(1)
-      W3D_TB_STAGE(2)
-      W3D_TB_STAGE(3)
-      W3D_TB_STAGE(4)
-#undef W3D_TB_STAGE
-    };
-
-    // prologue: u^n planes i0−1, i0 (registers; plane i0 also to LDS), plane i0+1 and u^{n−1} plane i0 in flight
-    load_cur(std::integral_constant<int, 3>{}, std::integral_constant<int, 1>{}, i0 - 1);
-    load_cur(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, i0);
-    commit_cur(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0);
-    load_cur(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, i0 + 1);
-    load_prev(std::integral_constant<int, 0>{}, i0);
-    row_tables(i0, 0);
-    if constexpr (INIT) {  // φ planes i0+1 (slot 1: read back as the x neighbour at i0) and i0+2 (slot 0)
-      phi_plane(i0 + 1, 1);
-      phi_plane(i0 + 2, 0);
-    }
-    // bulk iterations: every stage's plane i − (k−1) lies in [blo, bhi) (owned, real, inside the global interior),
-    // so the per-stage x tests vanish; measured: the scalar unit (exec masks, compares, address math) was as busy as
-    // the vector unit. Blocks of 4 iterations keep the register-queue slots static.
-    using Gen = std::false_type;
-    using Bulk = std::true_type;
-    if constexpr (INIT) {
-      // the analytic-start pass runs general blocks only: its register footprint leaves no room for a second copy
-      for (int ib = i0; ib <= i1; ib += 4) {
-        iteration(std::integral_constant<int, 0>{}, Gen{}, ib);
-        if (ib + 1 > i1) break;
-        iteration(std::integral_constant<int, 1>{}, Gen{}, ib + 1);
-        if (ib + 2 > i1) break;
-        iteration(std::integral_constant<int, 2>{}, Gen{}, ib + 2);
-        if (ib + 3 > i1) break;
-        iteration(std::integral_constant<int, 3>{}, Gen{}, ib + 3);
-      }
-    } else {
-      // head blocks (general) until the first block inside the bulk range, bulk blocks, then the general tail
-      const int blo = imax(imax(x0, p.sx0), 1 - p.gx0) + (S - 1);
-      const int bhi = imin(imin(x1, p.sx1), N - p.gx0);
-      int ib = i0;
-      const int nhead = blo > i0 ? (blo - i0 + 3) / 4 : 0;
-      for (int b = 0; b < nhead && ib + 3 <= i1; ++b, ib += 4) {
-        iteration(std::integral_constant<int, 0>{}, Gen{}, ib);
-        iteration(std::integral_constant<int, 1>{}, Gen{}, ib + 1);
-        iteration(std::integral_constant<int, 2>{}, Gen{}, ib + 2);
-        iteration(std::integral_constant<int, 3>{}, Gen{}, ib + 3);
-      }
-      for (; ib + 3 < bhi; ib += 4) {
-        iteration(std::integral_constant<int, 0>{}, Bulk{}, ib);
-        iteration(std::integral_constant<int, 1>{}, Bulk{}, ib + 1);
-        iteration(std::integral_constant<int, 2>{}, Bulk{}, ib + 2);
-        iteration(std::integral_constant<int, 3>{}, Bulk{}, ib + 3);
-      }
-      for (; ib <= i1; ib += 4) {
-        iteration(std::integral_constant<int, 0>{}, Gen{}, ib);
-        if (ib + 1 > i1) break;
-        iteration(std::integral_constant<int, 1>{}, Gen{}, ib + 1);
-        if (ib + 2 > i1) break;
-        iteration(std::integral_constant<int, 2>{}, Gen{}, ib + 2);
-        if (ib + 3 > i1) break;
-        iteration(std::integral_constant<int, 3>{}, Gen{}, ib + 3);
-      }
-    }
-  }
-
-  if (p.partials == nullptr) return;
-  __shared__ double red_m[NT / 64], red_s[NT / 64];
-#pragma unroll
-  for (int k = 0; k < S; ++k) {
-    if (!((CM >> k) & 1) || !((p.check_mask >> k) & 1)) continue;
-    double m = emax[k], sm = esum[k];
-    wave_reduce(m, sm);
-    __syncthreads();
-    if ((tid & 63) == 0) {
-      red_m[tid >> 6] = m;
-      red_s[tid >> 6] = sm;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      double mm = red_m[0], ss = red_s[0];
-      for (int w = 1; w < NT / 64; ++w) {
-        mm = red_m[w] > mm ? red_m[w] : mm;
-        ss += red_s[w];
-      }
-      p.partials[k * p.lstride + static_cast<int>(blockIdx.x)] = make_double2(mm, ss);
-    }
-  }
-}
-
-struct TbPlan {
-  TbParams prm{};
-  int nblocks = 0;
-};
-
-// `real`: per axis, the local range where stage values are real (outside: Dirichlet 0 / unused); an axis with lo > hi
-// takes the default (x: the compute box; y, z: the whole allocation, i.e. no restriction besides the global interior).
-TbPlan make_plan_tb(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, LBox real) {
-  W3D_REQUIRE(t.stages >= 2 && t.stages <= 4, "leapfrog_tb: stages must be 2, 3 or 4");
-  W3D_REQUIRE(t.threads == 512 || t.threads == 1024, "leapfrog_tb: threads must be 512 or 1024");
-  const LBox full = compute_box(l);
-  if (real.x0 > real.x1) {
-    real.x0 = full.x0;
-    real.x1 = full.x1;
-  }
-  if (real.y0 > real.y1) {
-    real.y0 = -l.yg;
-    real.y1 = l.ny + l.yg;
-  }
-  if (real.z0 > real.z1) {
-    real.z0 = -l.zg;
-    real.z1 = l.nz + l.zg;
-  }
-  W3D_REQUIRE(b.x0 >= full.x0 && b.x1 <= full.x1 && b.y0 >= full.y0 && b.y1 <= full.y1 && b.z0 >= full.z0 &&
-                  b.z1 <= full.z1,
-              "leapfrog_tb box outside the compute box");
-  W3D_REQUIRE(l.N < (1 << 20) && l.plane < (1 << 28), "leapfrog_tb: plane too large for 28-bit in-plane offsets");
-  const i64 S = t.stages;
-  // per axis: u^{n+k} (k < S) is read up to S−k nodes beyond the box, so its values there must be real (the `real`
-  // range) unless they lie beyond the global boundary (structural zeros); u^n is read S nodes beyond the box, within
-  // the allocation (ghost depth g) unless beyond the global boundary
-  auto axis_ok = [&](i64 b0, i64 b1, i64 r0, i64 r1, i64 g0, i64 n, i64 g, const char* ax) {
-    const bool lo_ok = r0 <= b0 - (S - 1) || g0 + r0 <= 1;
-    const bool hi_ok = r1 >= b1 + (S - 1) || g0 + r1 >= l.N;
-    W3D_REQUIRE(lo_ok && hi_ok, std::string("leapfrog_tb: stage-1 range does not cover the box halo in ") + ax);
-    W3D_REQUIRE(g0 + b0 - S <= 0 || b0 - S >= -g, std::string("leapfrog_tb: halo deeper than the ghosts in ") + ax);
-    W3D_REQUIRE(g0 + b1 + S - 1 >= l.N || b1 + S - 1 < n + g,
-                std::string("leapfrog_tb: halo deeper than the ghosts in ") + ax);
-    W3D_REQUIRE(r0 >= -g && r1 <= n + g, std::string("leapfrog_tb: real range outside the allocation in ") + ax);
-  };
-  axis_ok(b.x0, b.x1, real.x0, real.x1, l.gx0, l.nx, l.xg, "x");
-  axis_ok(b.y0, b.y1, real.y0, real.y1, l.gy0, l.ny, l.yg, "y");
-  axis_ok(b.z0, b.z1, real.z0, real.z1, l.gz0, l.nz, l.zg, "z");
-  TbPlan pl;
-  TbParams& p = pl.prm;
-  p.plane = l.plane;
-  p.pitch = l.pitch;
-  p.zs = l.zs;
-  p.x0 = static_cast<int>(b.x0);
-  p.x1 = static_cast<int>(b.x1);
-  p.xlen = static_cast<int>(imax(1, b.x1 - b.x0));
-  p.nxc = 1;
-  p.sx0 = static_cast<int>(real.x0);
-  p.sx1 = static_cast<int>(real.x1);
-  p.ax0 = static_cast<int>(-l.xg);
-  p.ax1 = static_cast<int>(l.nx + l.xg);
-  p.sy0 = static_cast<int>(real.y0);
-  p.sy1 = static_cast<int>(real.y1);
-  p.sz0 = static_cast<int>(real.z0);
-  p.sz1 = static_cast<int>(real.z1);
-  p.ay0 = static_cast<int>(-l.yg);
-  p.ay1 = static_cast<int>(l.ny + l.yg);
-  p.az0 = static_cast<int>(-l.zg);
-  p.az1 = static_cast<int>(l.nz + l.zg);
-  p.zero_off = static_cast<int>(l.zero_off());
-  p.yg = static_cast<int>(l.yg);
-  p.zg = static_cast<int>(l.zg);
-  p.N = static_cast<int>(l.N);
-  p.gx0 = static_cast<int>(l.gx0);
-  p.gy0 = static_cast<int>(l.gy0);
-  p.gz0 = static_cast<int>(l.gz0);
-  p.y0 = static_cast<int>(b.y0);
-  p.y1 = static_cast<int>(b.y1);
-  p.z0 = static_cast<int>(b.z0);
-  p.z1 = static_cast<int>(b.z1);
-  if (b.x1 <= b.x0 || b.y1 <= b.y0 || b.z1 <= b.z0) return pl;
-  p.nty = static_cast<int>(ceil_div(b.y1 - b.y0, kTile));
-  p.ntz = static_cast<int>(ceil_div(b.z1 - b.z0, kTile));
-  const int tiles = p.nty * p.ntz;
-  // x chunks when the tile grid alone leaves CUs idle (3-D block boxes): at least min_chunk planes per chunk
-  if (t.target_blocks > tiles) {
-    const i64 nxb = b.x1 - b.x0;
-    const i64 want = imin(ceil_div(t.target_blocks, tiles), imax(1, nxb / imax(1, t.min_chunk)));
-    p.xlen = static_cast<int>(ceil_div(nxb, imax(1, want)));
-    p.nxc = static_cast<int>(ceil_div(nxb, p.xlen));
-  }
-  const int blocks = tiles * p.nxc;
-  pl.nblocks = t.xcd_remap ? static_cast<int>(round_up(blocks, 8)) : blocks;
-  p.nblocks = pl.nblocks;
-  p.xcd_remap = t.xcd_remap ? 1 : 0;
-  // blocked XCD ownership when the tile grid splits into 8 equal blocks (one per XCD), the squarest such block
-  p.bby = p.bbz = 0;
-  if (t.xcd_remap && t.xcd_blocks && p.nxc == 1 && tiles == pl.nblocks && tiles % 8 == 0) {
-    const int per = tiles / 8;
-    int best = 1 << 30;
-    for (int by = 1; by <= per; ++by) {
-      if (per % by) continue;
-      const int bz = per / by;
-      if (p.nty % by || p.ntz % bz) continue;
-      const int perim = by + bz;
-      if (perim < best) {
-        best = perim;
-        p.bby = by;
-        p.bbz = bz;
-      }
-    }
-  }
-  return pl;
-}
-
-template <int NT>
-constexpr size_t max_dyn_lds() {
-  return 160 * 1024 - 2 * (NT / 64) * sizeof(double) - 64;  // minus the static reduction arrays (+ alignment)
-}
-
-// allow the dynamic LDS size once per instantiation (outside any stream capture: see leapfrog_tb_prepare): the CU's
-// 160 KiB minus the kernel's static LDS (the reduction arrays as the compiler laid them out, alignment included);
-// returns that limit
-template <int S, int NT, int CM, bool INIT, bool CH>
-size_t prepare_cfg() {
-  static_assert(tb_lds_bytes<S, kTile, NT, INIT>() <= max_dyn_lds<NT>(), "leapfrog_tb tile does not fit in LDS");
-  static const size_t limit = [] {
-    const void* fn = reinterpret_cast<const void*>(k_leapfrog_tb<S, kTile, NT, CM, INIT, CH>);
-    hipFuncAttributes fa{};
-    hipError_t e = hipFuncGetAttributes(&fa, fn);
-    if (e != hipSuccess) fail(std::string("leapfrog_tb attributes: ") + hipGetErrorString(e));
-    const size_t lim = 160 * 1024 - fa.sharedSizeBytes;
-    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lim));
-    if (e != hipSuccess) fail(std::string("leapfrog_tb LDS attribute: ") + hipGetErrorString(e));
-    return lim;
-  }();
-  return limit;
-}
-
-template <int S, int NT, int CM, bool INIT>
-void launch_cfg(const TbParams& p, int nblocks, hipStream_t st) {
-  const size_t shmem = tb_lds_bytes<S, kTile, NT, INIT>((p.check_mask || INIT) ? tb_nx_table<S>(p.xlen) : 0);
-  if (p.nxc > 1) {
-    const size_t lim = prepare_cfg<S, NT, CM, INIT, true>();
-    W3D_REQUIRE(shmem <= lim, "leapfrog_tb: too many planes for the LDS sin table");
-    hipLaunchKernelGGL((k_leapfrog_tb<S, kTile, NT, CM, INIT, true>), dim3(nblocks), dim3(NT), shmem, st, p);
-  } else {
-    const size_t lim = prepare_cfg<S, NT, CM, INIT, false>();
-    W3D_REQUIRE(shmem <= lim, "leapfrog_tb: too many planes for the LDS sin table");
-    hipLaunchKernelGGL((k_leapfrog_tb<S, kTile, NT, CM, INIT, false>), dim3(nblocks), dim3(NT), shmem, st, p);
-  }
-}
-
-// instantiated check supersets per S: none, even levels, odd levels, all (checks every 2nd step hit one parity)
-template <int S>
-constexpr int kFull = (1 << S) - 1;
-template <int S>
-constexpr int kEven = 0b1010 & kFull<S>;
-template <int S>
-constexpr int kOdd = 0b0101 & kFull<S>;
-
-template <int S, int NT, bool INIT>
-void launch_nt(const TbParams& p, int nblocks, hipStream_t st) {
-  const int m = p.check_mask;
-  if (m == 0)
-    launch_cfg<S, NT, 0, INIT>(p, nblocks, st);
-  else if ((m & ~kEven<S>) == 0)
-    launch_cfg<S, NT, kEven<S>, INIT>(p, nblocks, st);
-  else if ((m & ~kOdd<S>) == 0)
-    launch_cfg<S, NT, kOdd<S>, INIT>(p, nblocks, st);
-  else
-    launch_cfg<S, NT, kFull<S>, INIT>(p, nblocks, st);
-}
-
-// the analytic-start pass is built for 1024-thread workgroups only
-template <int S>
-void launch_s(const TbParams& p, int nblocks, const LeapfrogTbTiling& t, bool init, hipStream_t st) {
-  if (init)
-    launch_nt<S, 1024, true>(p, nblocks, st);
-  else if (t.threads == 1024)
-    launch_nt<S, 1024, false>(p, nblocks, st);
-  else
-    launch_nt<S, 512, false>(p, nblocks, st);
-}
-
-template <int S, int NT, bool INIT, bool CH>
-void prepare_ch() {
-  prepare_cfg<S, NT, 0, INIT, CH>();
-  prepare_cfg<S, NT, kEven<S>, INIT, CH>();
-  prepare_cfg<S, NT, kOdd<S>, INIT, CH>();
-  prepare_cfg<S, NT, kFull<S>, INIT, CH>();
-}
-template <int S, int NT, bool INIT>
-void prepare_nt() {
-  prepare_ch<S, NT, INIT, false>();
-  prepare_ch<S, NT, INIT, true>();
-}
-
-}  // namespace
-
-void leapfrog_tb_prepare() {
+void leapfrog_tb_prepare(bool push) {
+  if (push) prepare_push();
   prepare_nt<2, 512, false>();
   prepare_nt<3, 512, false>();
   prepare_nt<4, 512, false>();
@@ -772,12 +65,19 @@ int leapfrog_tb_partials(const Layout& l, const LBox& box, const LeapfrogTbTilin
 void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
                         double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
                         Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, const LBox& real,
-                        bool analytic_start, int level_stride, int grid_blocks) {
+                        bool analytic_start, int level_stride, int grid_blocks, const TbPush* push) {
   W3D_REQUIRE(out1 != out2 && (analytic_start || (prev != out1 && prev != out2 && cur != out1 && cur != out2)),
               "leapfrog_tb needs four distinct buffers");
   TbPlan pl = make_plan_tb(l, box, t, real);
   if (pl.nblocks == 0) return;
   TbParams& p = pl.prm;
+  if (push != nullptr && push->on) {
+    // the staging holds T planes per side in this rank's plane geometry; the forwarded planes are this rank's own
+    W3D_REQUIRE(push->T == l.xg && push->nx == l.nx && t.stages <= push->T && l.yg == 1 && l.zg == 1,
+                "leapfrog_tb push: slab ranks with T-deep x ghosts only");
+    W3D_REQUIRE(push->T >= 2 && l.nx >= push->T, "leapfrog_tb push: a rank needs at least T planes");
+    p.push = *push;
+  }
   // a padded grid (several launches sharing one level's partial slots, each of grid_blocks entries): the extra
   // workgroups have no tile and write (0, 0) partials, so every slot entry a reduction reads is written
   if (grid_blocks > 0) {
@@ -801,10 +101,16 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
   W3D_REQUIRE(level_stride == 0 || level_stride >= pl.nblocks, "leapfrog_tb: level stride below the block count");
   p.lstride = level_stride > 0 ? level_stride : pl.nblocks;
   for (int k = 0; k < 4; ++k) p.ct[k] = (ct != nullptr && k < t.stages) ? ct[k] : 0.0;
-  switch (t.stages) {
-    case 2: launch_s<2>(p, pl.nblocks, t, analytic_start, stream); break;
-    case 3: launch_s<3>(p, pl.nblocks, t, analytic_start, stream); break;
-    default: launch_s<4>(p, pl.nblocks, t, analytic_start, stream); break;
+  W3D_REQUIRE(!p.push.on || p.push.signal_epoch == 0 || p.push.done_target % static_cast<unsigned>(pl.nblocks) == 0,
+              "leapfrog_tb push: done_target must be a multiple of the grid (every pass of a solve: one full grid)");
+  if (p.push.on) {
+    launch_push(p, pl.nblocks, t.stages, analytic_start, stream);
+  } else {
+    switch (t.stages) {
+      case 2: launch_s<2, false>(p, pl.nblocks, t, analytic_start, stream); break;
+      case 3: launch_s<3, false>(p, pl.nblocks, t, analytic_start, stream); break;
+      default: launch_s<4, false>(p, pl.nblocks, t, analytic_start, stream); break;
+    }
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) fail(std::string("leapfrog_tb launch: ") + hipGetErrorString(e));

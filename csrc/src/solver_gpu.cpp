@@ -165,6 +165,10 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
       mode_ = Mode::kDeep;
   }
   block_tb_ = mode_ == Mode::kDeepTb && !slab;
+  if (opt_.push && world > 1) {
+    W3D_REQUIRE(mode_ == Mode::kDeepTb && !block_tb_, "push transport: slab LDS passes (deep-tb) only, not " + mode());
+    push_ = true;
+  }
   for (int attempt = 0; attempt < 2; ++attempt) {
     const i64 T = opt_.temporal;
     lay_ = make_layout(prob_, box, 16, mode_ == Mode::kDeep ? 2 : (mode_ == Mode::kDeepTb && dims_.px > 1) ? T : 1,
@@ -175,6 +179,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
     W3D_HIP(hipMemGetInfo(&free_b, &total_b));
     const double need2 = 2.0 * static_cast<double>(lay_.bytes()), headroom = 2.0e9;
     if (mode_ != Mode::kSingleStep && 2.0 * need2 + headroom > static_cast<double>(free_b)) {
+      W3D_REQUIRE(!push_, "push transport: four field buffers do not fit");
       mode_ = Mode::kSingleStep;
       block_tb_ = false;
       continue;
@@ -266,6 +271,16 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
     W3D_HIP(hipMalloc(&u_[b], static_cast<size_t>(lay_.bytes())));
     W3D_HIP(hipMemset(u_[b], 0, static_cast<size_t>(lay_.bytes())));
   }
+  if (push_) {
+    // staging in fine-grained memory (remote stores from the neighbours' passes stay coherent with this GPU's reads),
+    // flags in uncached memory (polled by the kernels and the command processor)
+    const size_t sb = static_cast<size_t>(8 * lay_.xg * lay_.plane) * sizeof(double);
+    W3D_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&stg_), sb, hipDeviceMallocFinegrained));
+    W3D_HIP(hipMemset(stg_, 0, sb));
+    W3D_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), 256, hipDeviceMallocUncached));
+    W3D_HIP(hipMemset(flags_, 0, 256));
+    if (opt_.push_cp_wait) opt_.graph = false;  // (stream memops are not captured into graphs)
+  }
   const std::vector<double> s = sin_table_ext(prob_);
   W3D_HIP(hipMalloc(&d_s_, s.size() * sizeof(double)));
   W3D_HIP(hipMemcpy(d_s_, s.data(), s.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -287,7 +302,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
     LeapfrogTbTiling t = opt_.tiling_tb;
     t.stages = opt_.temporal;  // partials per level do not depend on the stage count
     n_tb_ = leapfrog_tb_partials(lay_, full_, t);
-    leapfrog_tb_prepare();
+    leapfrog_tb_prepare(push_);
   }
   int n_deep = 0;
   for (const LBox& b : dshell_) {
@@ -326,7 +341,14 @@ GpuSolver::~GpuSolver() {
   if (ev_shell_) (void)hipEventDestroy(ev_shell_);
   if (ev_halo_) (void)hipEventDestroy(ev_halo_);
   if (ev_packed_) (void)hipEventDestroy(ev_packed_);
-  if (s0_) (void)hipStreamDestroy(s0_);
+  for (int k = 0; k < 2; ++k)
+    if (peer_ipc_[k]) {
+      (void)hipIpcCloseMemHandle(peer_stg_[k]);
+      (void)hipIpcCloseMemHandle(peer_flags_[k]);
+    }
+  if (stg_) (void)hipFree(stg_);
+  if (flags_) (void)hipFree(flags_);
+  if (s0_ && own_s0_) (void)hipStreamDestroy(s0_);
   if (s1_) (void)hipStreamDestroy(s1_);
 }
 
@@ -376,7 +398,7 @@ bool GpuSolver::post_exchange() const { return mode_ == Mode::kDeep || mode_ == 
 bool GpuSolver::late_exchange() const { return mode_ == Mode::kDeepTb && (!opt_.overlap || block_tb_); }
 
 bool GpuSolver::needs_exchange(int i) const {
-  if (!plan_.any()) return false;
+  if (!plan_.any() || push_) return false;  // (push: the passes deliver the ghosts themselves)
   return post_exchange() ? i + 1 < static_cast<int>(units_.size()) : i > 0;
 }
 
@@ -544,6 +566,12 @@ void GpuSolver::phase_init() {
   ev_next_ = 0;
   marks_.clear();
   W3D_HIP(hipMemsetAsync(errlog_, 0, static_cast<size_t>(K + 1) * sizeof(Partial), s0_));
+  if (push_) {
+    W3D_HIP(hipMemsetAsync(flags_ + 8, 0, sizeof(unsigned), s0_));  // workgroups done (the passes' signal counter)
+    // (in-process group only: there every rank's init precedes every pass, so no neighbour has written yet)
+    if (opt_.poison_ghosts && loopback_)
+      W3D_HIP(hipMemsetAsync(stg_, 0xFF, static_cast<size_t>(8 * lay_.xg * lay_.plane) * sizeof(double), s0_));
+  }
   // one rank on the LDS kernel: the first pass starts from the analytic u⁰, u¹ itself (no init kernel, no reads)
   analytic_ = (mode_ == Mode::kFusedSingle || mode_ == Mode::kDeepTb) && analytic_ok() && resume_n_ == 0;
   if (resume_n_ > 0) {  // loaded state: u^{n0−1} → buf 0, u^{n0} → buf 1 (ghosts included)
@@ -694,10 +722,57 @@ void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase) {
   W3D_REQUIRE(tb_slots_ < slots, "leapfrog_tb: too many launches in one unit");
   Partial* part = mask ? tb_partials_ + tb_region_ * (4 * slots * n_tb_) + tb_slots_ * n_tb_ : nullptr;
   const LBox real = mode_ == Mode::kDeepTb ? sreal_ : tb_default_real();
+  // push transport: pass j (1-based) forwards its faces into the neighbours' staging of parity j % 2, reads its ghosts
+  // from its own staging of parity (j − 1) % 2 (pass 1: from the field, filled by the init / the loaded state), waits
+  // for both neighbours' pass j − 1 and signals its own (all but the last pass: nobody waits for that one)
+  TbPush q;
+  if (push_) {
+    const int j = cur_unit_ + 1, npass = static_cast<int>(units_.size());
+    W3D_REQUIRE(peer_flags_[0] || !nb_lo_, "push transport: lower neighbour not connected");
+    W3D_REQUIRE(peer_flags_[1] || !nb_hi_, "push transport: upper neighbour not connected");
+    q.on = 1;
+    q.faces_first = opt_.overlap ? 1 : 0;
+    q.T = static_cast<int>(lay_.xg);
+    q.nx = static_cast<int>(lay_.nx);
+    q.flags = flags_;
+    q.status = flags_ + 4;
+    q.done = flags_ + 8;
+    // epochs: in-kernel waits (graph-replayable) use the pass index j of the solve, every pass but the last signals
+    // and the flags are reset at the end of the solve, before its closing collective (which every multi-process run
+    // with in-kernel waits has: the error all-gather); command-processor waits use a pass counter that runs on over
+    // the solves, every pass signals and pass 1 waits for the neighbours' last pass of the previous solve (no reset,
+    // no collective needed)
+    const bool mono = opt_.push_cp_wait;
+    const unsigned G = static_cast<unsigned>(mono ? push_epoch_ + j : j);
+    const unsigned wait = mono ? G - 1 : (j > 1 ? G - 1 : 0u);
+    q.wait_epoch = mono ? 0u : wait;
+    q.signal_epoch = (mono || j < npass) ? G : 0u;
+    q.done_target = q.signal_epoch ? static_cast<unsigned>(j * n_tb_) : 0u;
+    static const unsigned long long ticks = [] {
+      int khz = 100000;
+      (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
+      return static_cast<unsigned long long>(std::min(gpu_timeout_s(), 60.0) * 1e3 * khz);
+    }();
+    q.spin_ticks = ticks;
+    const int par = j % 2, rpar = (j - 1) % 2;
+    for (int side = 0; side < 2; ++side) {
+      if (!(side == 0 ? nb_lo_ : nb_hi_)) continue;
+      q.fwd1[side] = peer_stg_[side] + stg_off(par, 0, 1 - side);  // the neighbour's ghosts on the side facing us
+      q.fwd2[side] = peer_stg_[side] + stg_off(par, 1, 1 - side);
+      if (j > 1) {
+        q.gprev[side] = stg_ + stg_off(rpar, 0, side);
+        q.gcur[side] = stg_ + stg_off(rpar, 1, side);
+      }
+      q.rflag[side] = peer_flags_[side] + (1 - side);  // our slot in the neighbour's flags
+      q.wait_side[side] = 1;
+      if (mono && wait > 0)
+        W3D_HIP(hipStreamWaitValue32(s0_, flags_ + side, wait, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    }
+  }
   timed(phase, s0_, [&] {
     // (every launch fills its whole slot of n_tb_ partials: shell and interior boxes may have fewer x chunks)
     launch_leapfrog_tb(lay_, coef_, u_[old_], u_[cur_], u_[uf_[0]], u_[uf_[1]], box, d_s_ + 1, cts, mask, part, t,
-                       s0_, real, u.analytic, slots * n_tb_, n_tb_);
+                       s0_, real, u.analytic, slots * n_tb_, n_tb_, push_ ? &q : nullptr);
   });
   if (mask) ++tb_slots_;
 }
@@ -801,6 +876,8 @@ void GpuSolver::enqueue_solve() {
     if (late) unit_exchange_rccl(i);
   }
   flush_reduces();
+  if (push_) push_finish(s0_);
+  push_epoch_ += static_cast<int>(units_.size());
   final_buf_ = cur_;
   prev_buf_ = old_;
 }
@@ -892,6 +969,7 @@ void GpuSolver::gather_errors(RunResult& r) {
     W3D_HIP(hipMemcpyAsync(host.data(), errlog_, per * sizeof(Partial), hipMemcpyDeviceToHost, s0_));
   }
   wait_stream(s0_, comm_.get(), gpu_timeout_s());
+  push_check();
   const int nsrc = static_cast<int>(host.size() / per);
   const double n_int = static_cast<double>(prob_.N - 1);
   const double denom = n_int * n_int * n_int;
@@ -950,6 +1028,63 @@ RunResult GpuSolver::run() {
   return r;
 }
 
+// ------------------------------------------------------------------------------------------------------------------
+// push transport (slab LDS passes): peers, IPC, end of solve
+// ------------------------------------------------------------------------------------------------------------------
+std::string GpuSolver::push_handles() const {
+  W3D_REQUIRE(push_, "push_handles: this solver does not use the push transport");
+  hipIpcMemHandle_t h[2];
+  W3D_HIP(hipIpcGetMemHandle(&h[0], stg_));
+  W3D_HIP(hipIpcGetMemHandle(&h[1], flags_));
+  return std::string(reinterpret_cast<const char*>(h), sizeof h);
+}
+
+void GpuSolver::connect_push_peer(int side, double* stg, unsigned* flags, bool ipc) {
+  peer_stg_[side] = stg;
+  peer_flags_[side] = flags;
+  peer_ipc_[side] = ipc;
+}
+
+void GpuSolver::connect_push(const std::vector<std::string>& all) {
+  W3D_REQUIRE(push_, "connect_push: this solver does not use the push transport");
+  W3D_REQUIRE(static_cast<int>(all.size()) == world_, "connect_push: one handle set per rank expected");
+  for (int side = 0; side < 2; ++side) {
+    const int peer = neighbor_rank(dims_, rank_, 0, side);
+    if (peer < 0) continue;
+    const std::string& b = all[static_cast<size_t>(peer)];
+    hipIpcMemHandle_t h[2];
+    W3D_REQUIRE(b.size() == sizeof h, "connect_push: bad handle size from rank " + std::to_string(peer));
+    std::memcpy(h, b.data(), sizeof h);
+    void* stg = nullptr;
+    void* fl = nullptr;
+    W3D_HIP(hipIpcOpenMemHandle(&stg, h[0], hipIpcMemLazyEnablePeerAccess));
+    W3D_HIP(hipIpcOpenMemHandle(&fl, h[1], hipIpcMemLazyEnablePeerAccess));
+    connect_push_peer(side, static_cast<double*>(stg), static_cast<unsigned*>(fl), true);
+  }
+}
+
+void GpuSolver::connect_push_self() {
+  W3D_REQUIRE(push_, "connect_push_self: this solver does not use the push transport");
+  for (int side = 0; side < 2; ++side)
+    // (the signal raises peer_flags_[side] + (1 − side): aim it at flags_[side], the slot this side waits on)
+    if (neighbor_rank(dims_, rank_, 0, side) >= 0) connect_push_peer(side, stg_, flags_ + (2 * side - 1), false);
+}
+
+// After the last pass of a solve (which waited for both neighbours' last signals, the final values of this solve's
+// flags) the flags go back to 0, before this rank's end-of-solve collective: no neighbour can signal the next solve's
+// first pass before that collective has completed everywhere.
+void GpuSolver::push_finish(hipStream_t st) {
+  if (!opt_.push_cp_wait) W3D_HIP(hipMemsetAsync(flags_, 0, 2 * sizeof(unsigned), st));
+}
+
+void GpuSolver::push_check() {
+  if (!push_) return;
+  unsigned st = 0;
+  W3D_HIP(hipMemcpy(&st, flags_ + 4, sizeof st, hipMemcpyDeviceToHost));
+  W3D_REQUIRE(st == 0, "push transport: a pass timed out waiting for a neighbour's signal (rank " +
+                           std::to_string(rank_) + ")");
+}
+
 std::vector<double> GpuSolver::download(int which) const {
   std::vector<double> h(static_cast<size_t>(lay_.total));
   const double* src = u_[which == 0 ? final_buf_ : prev_buf_];
@@ -979,6 +1114,24 @@ double comm_allreduce(const Comm& c, double v, bool max_op) {
 
 void comm_barrier(const Comm& c) { (void)comm_allreduce(c, 0.0, false); }
 
+std::vector<std::string> comm_allgather_bytes(const Comm& c, const std::string& mine) {
+  const size_t n = mine.size(), w = static_cast<size_t>(c.world());
+  hipStream_t st = nullptr;
+  W3D_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  char* d = nullptr;
+  W3D_HIP(hipMalloc(&d, n * (w + 1)));
+  std::string all(n * w, '\0');
+  W3D_HIP(hipMemcpyAsync(d, mine.data(), n, hipMemcpyHostToDevice, st));
+  W3D_NCCL(ncclAllGather(d, d + n, n, ncclChar, static_cast<ncclComm_t>(c.raw()), st));
+  W3D_HIP(hipMemcpyAsync(all.data(), d + n, n * w, hipMemcpyDeviceToHost, st));
+  wait_stream(st, &c, gpu_timeout_s());
+  (void)hipFree(d);
+  (void)hipStreamDestroy(st);
+  std::vector<std::string> v;
+  for (size_t r = 0; r < w; ++r) v.push_back(all.substr(r * n, n));
+  return v;
+}
+
 int rccl_version() {
   int v = 0;
   (void)ncclGetVersion(&v);
@@ -992,12 +1145,36 @@ namespace wave3d {
 GpuGroup::GpuGroup(const Problem& prob, const SolverOptions& opt, int world, const std::string& transport)
     : transport_(transport) {
   W3D_REQUIRE(world >= 1, "world must be >= 1");
-  W3D_REQUIRE(transport == "loopback" || transport == "rccl-self",
-              "group transport must be loopback or rccl-self, not " + transport);
+  W3D_REQUIRE(transport == "loopback" || transport == "rccl-self" || transport == "push",
+              "group transport must be loopback, rccl-self or push, not " + transport);
+  SolverOptions o = opt;
+  o.push = transport == "push";
   for (int r = 0; r < world; ++r) {
     std::shared_ptr<Comm> c;
     if (transport == "rccl-self") c = std::make_shared<Comm>(0, 1, Comm::make_unique_id());
-    ranks_.push_back(std::make_unique<GpuSolver>(prob, opt, r, world, c, true));
+    ranks_.push_back(std::make_unique<GpuSolver>(prob, o, r, world, c, true));
+  }
+  if (o.push && world > 1) {
+    // the ranks' passes wait for each other in the kernel: on ONE GPU they must not run concurrently (a waiting pass
+    // could hold every CU while the pass it waits for cannot start), so every rank launches on rank 0's compute stream
+    // in schedule order (rank 0 unit i, rank 1 unit i, ...) and each wait is already satisfied when it is reached.
+    // The data path (forwarded faces in the neighbours' staging, ghosts read from the own staging, flags, counters,
+    // epochs, flag reset) is the multi-process one; peers are the other ranks' buffers instead of IPC mappings.
+    for (int r = 0; r < world; ++r) {
+      GpuSolver* s = ranks_[static_cast<size_t>(r)].get();
+      W3D_REQUIRE(s->push_, "push group: every rank must run the slab LDS passes (deep-tb)");
+      if (r > 0) {
+        (void)hipStreamDestroy(s->s0_);
+        s->s0_ = ranks_[0]->s0_;
+        s->own_s0_ = false;
+      }
+      for (int side = 0; side < 2; ++side) {
+        const int peer = neighbor_rank(s->dims_, r, 0, side);
+        if (peer < 0) continue;
+        GpuSolver* q = ranks_[static_cast<size_t>(peer)].get();
+        s->connect_push_peer(side, q->stg_, q->flags_, false);
+      }
+    }
   }
   graph_ = opt.graph && !opt.timers && !opt.debug_sync && (world == 1 || multistream_capture_safe());
   W3D_HIP(hipStreamCreateWithFlags(&gs_, hipStreamNonBlocking));
@@ -1074,6 +1251,11 @@ void GpuGroup::enqueue() {
     step("interior", i);
   }
   for (auto* s : rs) s->flush_reduces();
+  for (auto* s : rs)
+    if (s->push_) {
+      s->push_finish(s->s0_);
+      s->push_epoch_ += nu;
+    }
   step("flush", nu);
 }
 
@@ -1161,8 +1343,10 @@ RunResult GpuGroup::run() {
   }
   trace("gathers");
   wait_stream(gs_, rs[0]->comm_.get(), gpu_timeout_s());
-  for (auto* s : rs)
+  for (auto* s : rs) {
     if (s->comm_) s->comm_->check_async();
+    s->push_check();
+  }
   RunResult r;
   const double n_int = static_cast<double>(rs[0]->prob_.N - 1);
   for (int n : rs[0]->check_steps()) {

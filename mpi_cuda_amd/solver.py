@@ -12,6 +12,8 @@ hip        loopback    native GpuGroup: all ranks of a decomposition in THIS pro
                        (exercises the production multi-rank C++ path on a single GPU; tests)
 hip        rccl-self   native GpuGroup as above, halos moved by the production RCCL ncclSend/ncclRecv calls, each rank
                        over its own one-rank communicator (RCCL refuses 2 ranks of one communicator on one GPU)
+hip        push        native GpuGroup as above on the slab LDS passes, halos pushed by the passes themselves into the
+                       neighbours' fine-grained staging + flag signalling (the multi-process push transport's data path)
 cpu        native      C++ CpuSolver, OpenMP (the reference's sequential / OpenMP programs), world == 1
 cpu        torch       Python step loop, native OpenMP kernels, halos over torch.distributed gloo (MPI analogue)
 torch      -           plain PyTorch fp64 reference solver (oracle), world == 1
@@ -57,7 +59,8 @@ def _resolve(backend: str, transport: str, world: int) -> tuple[str, str]:
         backend = "hip" if torch.cuda.is_available() else "cpu"
     if transport == "auto":
         transport = {"hip": "rccl", "cpu": "native" if world == 1 else "torch", "torch": "none"}[backend]
-    ok = {("hip", "rccl"), ("hip", "torch"), ("hip", "loopback"), ("hip", "rccl-self"), ("cpu", "native"),
+    ok = {("hip", "rccl"), ("hip", "torch"), ("hip", "loopback"), ("hip", "rccl-self"), ("hip", "push"),
+          ("cpu", "native"),
           ("cpu", "torch"),
           ("torch", "none")}
     if (backend, transport) not in ok:
@@ -104,7 +107,7 @@ class Solver:
             self.device = torch.device("cuda", dev)
         else:
             self.device = torch.device("cpu")
-        if self.backend == "hip" and self.transport in ("loopback", "rccl-self"):
+        if self.backend == "hip" and self.transport in ("loopback", "rccl-self", "push"):
             opts = self._options(C, decomp, spec, overlap, graph, tiling, temporal, tiling2, init2, tb, tiling_tb)
             opts.timers, opts.debug_sync, opts.poison_ghosts = timers, debug_sync, poison_ghosts
             if deep_min_planes is not None:
@@ -202,7 +205,7 @@ class Solver:
         """The whole (N+1)³ field u^K (which=0) / u^{K-1} (which=1) on the CPU (single rank or loopback group)."""
         from .ops.stencil import grid_view
 
-        if self.transport not in ("loopback", "rccl-self"):
+        if self.transport not in ("loopback", "rccl-self", "push"):
             if self.world != 1:
                 raise RuntimeError("global_field needs world == 1 or the loopback transport")
             return self.owned_field(which)

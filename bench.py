@@ -220,7 +220,7 @@ def run_native(a, rank: int, world: int, local: int) -> int:
         par = (f"{sched.split('-')[0]}{world}" if multi else "single") if not a.cpu else f"cpu-ranks{world}"
         cfg = {
             "parallelism": par, "decomp": "x".join(map(str, dims)),
-            "transport": ("shm" if multi else "none") if a.cpu else ("rccl" if multi else "none"),
+            "transport": ("shm" if multi else "none") if a.cpu else (res.get("transport", "rccl") if multi else "none"),
             "runtime": "native bin/wave3d (C++/HIP/RCCL)" if not a.cpu else "native bin/wave3d --cpu (OpenMP ranks)",
             "graph": bool(res.get("graph", False)), "overlap": bool(res.get("overlap", False)) and multi,
             "temporal_blocking": int(res.get("temporal", 1)) > 1 and not a.cpu,

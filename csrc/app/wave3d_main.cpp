@@ -575,8 +575,8 @@ SolverOptions options_from(const Args& a, bool fake) {
   o.init2 = a.init2;
   o.fake_comm = fake;
   o.push = a.transport == "push";
-  // (ranks without a communicator have no end-of-solve collective: their flags must run on, CP waits)
-  o.push_cp_wait = a.push_cp_wait || a.no_rccl;
+  o.push_cp_wait = a.push_cp_wait;
+  o.push_no_collective = a.no_rccl;  // (no end-of-solve collective: the flag epochs run on, eager launches)
   if (a.t2_rows > 0) o.tiling2.rows = a.t2_rows;
   if (a.deep_min >= 0) o.deep_min_planes = a.deep_min;
   if (a.tb_min >= 0) o.tb_min_planes = a.tb_min;
@@ -768,19 +768,27 @@ int run_gpu(const Args& a) {
         if (!err.empty()) std::fprintf(stderr, "[wave3d rank %d] candidate %s rejected: %s\n", rank, c.name, err.c_str());
         continue;
       }
-      connect(*cand);  // (collective when the candidate pushes: every rank built it)
-      double t = 1e30;
-      RunResult r0 = cand->run();  // eager: RCCL peer connections
-      r0 = cand->run();            // graph capture
-      // every schedule computes bit-identical fields: a candidate whose error log differs from the first accepted
-      // one's (a transport that delivered wrong ghosts) is rejected on every rank, whatever its speed
-      bool same = r0.finite && (ref_log.empty() || r0.max_err == ref_log);
+      // every schedule computes bit-identical fields: a candidate that fails (e.g. a push wait timed out) or whose
+      // error log differs from the first accepted one's (a transport that delivered wrong ghosts) is rejected on
+      // every rank, whatever its speed
+      bool same = false;
+      RunResult r0;
+      try {
+        connect(*cand);     // (collective when the candidate pushes: every rank built it)
+        r0 = cand->run();   // eager: RCCL peer connections
+        r0 = cand->run();   // graph capture
+        same = r0.finite && (ref_log.empty() || r0.max_err == ref_log);
+        if (!same) err = "its error log differs from the reference schedule's";
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
       if (!agree(same)) {
-        std::fprintf(stderr, "[wave3d rank %d] candidate %s rejected: its error log differs from the reference\n", rank,
-                     c.name);
+        std::fprintf(stderr, "[wave3d rank %d] candidate %s rejected: %s\n", rank, c.name,
+                     err.empty() ? "failed on another rank" : err.c_str());
         continue;
       }
       if (ref_log.empty()) ref_log = r0.max_err;
+      double t = 1e30;
       for (int k = 0; k < 3; ++k) {
         if (comm) comm_barrier(*comm);
         t = std::min(t, cand->run().solve_s);

@@ -62,6 +62,9 @@ struct SolverOptions {
   // connect_push() (multi-process: IPC handles) or by a GpuGroup.
   bool push = false;
   bool push_cp_wait = false;
+  // push ranks without an end-of-solve collective (no RCCL communicator): the flag epochs run on over the solves
+  // instead of being reset (eager launches: every launch carries its own epochs)
+  bool push_no_collective = false;
 };
 
 // Summed device time per phase of the last run() (SolverOptions::timers). compute = interior / whole-box / fused

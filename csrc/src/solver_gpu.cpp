@@ -129,8 +129,8 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
       loopback_(loopback) {
   prob_.validate();
   W3D_REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
-  W3D_REQUIRE(world == 1 || comm_ || loopback_ || opt_.fake_comm,
-              "world > 1 needs an RCCL communicator (or the loopback group)");
+  W3D_REQUIRE(world == 1 || comm_ || loopback_ || opt_.fake_comm || (opt_.push && opt_.push_no_collective),
+              "world > 1 needs an RCCL communicator (or the loopback group, or the push transport without one)");
   dims_ = parse_dims(opt_.decomp, world, prob_.N);
   const Box box = rank_box(prob_, dims_, rank);
   W3D_REQUIRE(box.nx() >= 1 && box.ny() >= 1 && box.nz() >= 1,
@@ -255,7 +255,22 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   }
 
   // device memory
-  W3D_HIP(hipStreamCreateWithFlags(&s0_, hipStreamNonBlocking));
+  if (const char* cs = std::getenv("W3D_CU_SPLIT"); cs && !loopback_ && (std::strchr(cs, '/') || !std::strcmp(cs, "auto"))) {
+    // rehearsal of several ranks on ONE GPU with truly concurrent passes (W3D_CU_SPLIT=r/P, or auto = rank/world):
+    // this rank's compute stream only gets the r-th of P disjoint CU ranges, so a pass waiting in the kernel for a
+    // peer can never hold the CUs the peer's pass needs
+    const bool au = !std::strcmp(cs, "auto");
+    const int r = au ? rank : std::atoi(cs), P = au ? world : std::atoi(std::strchr(cs, '/') + 1);
+    int dev = 0, ncu = 0;
+    W3D_HIP(hipGetDevice(&dev));
+    W3D_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    W3D_REQUIRE(P >= 1 && r >= 0 && r < P && ncu >= P, "W3D_CU_SPLIT must be r/P with 0 <= r < P <= CUs");
+    std::vector<uint32_t> mask(static_cast<size_t>((ncu + 31) / 32), 0u);
+    for (int c = r * ncu / P; c < (r + 1) * ncu / P; ++c) mask[static_cast<size_t>(c / 32)] |= 1u << (c % 32);
+    W3D_HIP(hipExtStreamCreateWithCUMask(&s0_, static_cast<uint32_t>(mask.size()), mask.data()));
+  } else {
+    W3D_HIP(hipStreamCreateWithFlags(&s0_, hipStreamNonBlocking));
+  }
   {
     // the exchange stream gets the highest priority so RCCL's copy kernels are dispatched ahead of the waiting
     // interior workgroups: the halo overlaps the interior update instead of queueing behind it
@@ -279,7 +294,8 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
     W3D_HIP(hipMemset(stg_, 0, sb));
     W3D_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), 256, hipDeviceMallocUncached));
     W3D_HIP(hipMemset(flags_, 0, 256));
-    if (opt_.push_cp_wait) opt_.graph = false;  // (stream memops are not captured into graphs)
+    // (stream memops are not captured into graphs; running epochs are per-launch arguments)
+    if (opt_.push_cp_wait || opt_.push_no_collective) opt_.graph = false;
   }
   const std::vector<double> s = sin_table_ext(prob_);
   W3D_HIP(hipMalloc(&d_s_, s.size() * sizeof(double)));
@@ -402,7 +418,9 @@ bool GpuSolver::needs_exchange(int i) const {
   return post_exchange() ? i + 1 < static_cast<int>(units_.size()) : i > 0;
 }
 
-hipStream_t GpuSolver::xstream() const { return post_exchange() && opt_.overlap && !late_exchange() ? s1_ : s0_; }
+hipStream_t GpuSolver::xstream() const {
+  return post_exchange() && opt_.overlap && !late_exchange() && !push_ ? s1_ : s0_;
+}
 
 // Deep-halo fused passes need every unit to be a pair with no error check on its intermediate step, starting from the
 // analytic (u¹, u²): K even and no odd check step below K.
@@ -569,8 +587,12 @@ void GpuSolver::phase_init() {
   if (push_) {
     W3D_HIP(hipMemsetAsync(flags_ + 8, 0, sizeof(unsigned), s0_));  // workgroups done (the passes' signal counter)
     // (in-process group only: there every rank's init precedes every pass, so no neighbour has written yet)
-    if (opt_.poison_ghosts && loopback_)
+    if (opt_.poison_ghosts && loopback_) {
       W3D_HIP(hipMemsetAsync(stg_, 0xFF, static_cast<size_t>(8 * lay_.xg * lay_.plane) * sizeof(double), s0_));
+      // ... except each staging plane's zero slot (Layout::zero_off), which positions outside the global interior load
+      const size_t pb = static_cast<size_t>(lay_.plane) * sizeof(double);
+      W3D_HIP(hipMemset2DAsync(stg_ + lay_.zero_off(), pb, 0, sizeof(double), static_cast<size_t>(8 * lay_.xg), s0_));
+    }
   }
   // one rank on the LDS kernel: the first pass starts from the analytic u⁰, u¹ itself (no init kernel, no reads)
   analytic_ = (mode_ == Mode::kFusedSingle || mode_ == Mode::kDeepTb) && analytic_ok() && resume_n_ == 0;
@@ -742,10 +764,10 @@ void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase) {
     // with in-kernel waits has: the error all-gather); command-processor waits use a pass counter that runs on over
     // the solves, every pass signals and pass 1 waits for the neighbours' last pass of the previous solve (no reset,
     // no collective needed)
-    const bool mono = opt_.push_cp_wait;
+    const bool mono = opt_.push_cp_wait || opt_.push_no_collective;
     const unsigned G = static_cast<unsigned>(mono ? push_epoch_ + j : j);
     const unsigned wait = mono ? G - 1 : (j > 1 ? G - 1 : 0u);
-    q.wait_epoch = mono ? 0u : wait;
+    q.wait_epoch = opt_.push_cp_wait ? 0u : wait;
     q.signal_epoch = (mono || j < npass) ? G : 0u;
     q.done_target = q.signal_epoch ? static_cast<unsigned>(j * n_tb_) : 0u;
     static const unsigned long long ticks = [] {
@@ -765,7 +787,7 @@ void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase) {
       }
       q.rflag[side] = peer_flags_[side] + (1 - side);  // our slot in the neighbour's flags
       q.wait_side[side] = 1;
-      if (mono && wait > 0)
+      if (opt_.push_cp_wait && wait > 0)
         W3D_HIP(hipStreamWaitValue32(s0_, flags_ + side, wait, hipStreamWaitValueGte, 0xFFFFFFFFu));
     }
   }
@@ -1074,7 +1096,7 @@ void GpuSolver::connect_push_self() {
 // flags) the flags go back to 0, before this rank's end-of-solve collective: no neighbour can signal the next solve's
 // first pass before that collective has completed everywhere.
 void GpuSolver::push_finish(hipStream_t st) {
-  if (!opt_.push_cp_wait) W3D_HIP(hipMemsetAsync(flags_, 0, 2 * sizeof(unsigned), st));
+  if (!opt_.push_cp_wait && !opt_.push_no_collective) W3D_HIP(hipMemsetAsync(flags_, 0, 2 * sizeof(unsigned), st));
 }
 
 void GpuSolver::push_check() {

@@ -18,6 +18,35 @@ struct LBox {
 
 inline LBox compute_box(const Layout& l) { return LBox{l.cx0, l.cx1, l.cy0, l.cy1, l.cz0, l.cz1}; }
 
+// Shell / interior split of a rank's compute box for the overlapped single-step schedule: the interior is the box minus
+// one layer on every side that has a neighbour (nb[axis][side]); the shell is the rest, in ≤ 6 disjoint boxes (x faces
+// whole, y faces inside the x range, z faces inside x and y). The one definition: GpuSolver and the Python side
+// (mpi_cuda_amd.parallel.decomp.split_boxes, through the binding) both call it.
+inline void shell_split(const LBox& full, const bool nb[3][2], std::vector<LBox>& shell, LBox& interior) {
+  shell.clear();
+  interior = full;
+  if (nb[0][0]) interior.x0 += 1;
+  if (nb[0][1]) interior.x1 -= 1;
+  if (nb[1][0]) interior.y0 += 1;
+  if (nb[1][1]) interior.y1 -= 1;
+  if (nb[2][0]) interior.z0 += 1;
+  if (nb[2][1]) interior.z1 -= 1;
+  auto push = [&](LBox b) {
+    if (!b.empty()) shell.push_back(b);
+  };
+  if (!full.empty()) {
+    const i64 ix0 = imin(imax(interior.x0, full.x0), full.x1), ix1 = imax(interior.x1, ix0);
+    const i64 iy0 = imin(imax(interior.y0, full.y0), full.y1), iy1 = imax(interior.y1, iy0);
+    if (nb[0][0]) push(LBox{full.x0, full.x0 + 1, full.y0, full.y1, full.z0, full.z1});
+    if (nb[0][1]) push(LBox{imax(full.x1 - 1, full.x0 + (nb[0][0] ? 1 : 0)), full.x1, full.y0, full.y1, full.z0, full.z1});
+    if (nb[1][0]) push(LBox{ix0, ix1, full.y0, full.y0 + 1, full.z0, full.z1});
+    if (nb[1][1]) push(LBox{ix0, ix1, imax(full.y1 - 1, full.y0 + (nb[1][0] ? 1 : 0)), full.y1, full.z0, full.z1});
+    if (nb[2][0]) push(LBox{ix0, ix1, iy0, iy1, full.z0, full.z0 + 1});
+    if (nb[2][1]) push(LBox{ix0, ix1, iy0, iy1, imax(full.z1 - 1, full.z0 + (nb[2][0] ? 1 : 0)), full.z1});
+  }
+  if (interior.x1 < interior.x0 || interior.y1 < interior.y0 || interior.z1 < interior.z0) interior = LBox{};
+}
+
 // Resume / loaded-field start: the rank's padded local array (owned nodes and every ghost layer that lies inside the
 // domain; ghosts beyond the global boundary and the row padding 0) from a GLOBAL (N+1)³ C-order field. With ghosts
 // of any depth filled from the global field, the first pass after a resume needs no halo exchange.

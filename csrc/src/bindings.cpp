@@ -211,6 +211,20 @@ PYBIND11_MODULE(_C, m) {
       .def("count", &LBox::count)
       .def("as_tuple", [](const LBox& b) { return py::make_tuple(b.x0, b.x1, b.y0, b.y1, b.z0, b.z1); });
   m.def("compute_box", &compute_box);
+  m.def(
+      "shell_split",
+      [](const LBox& full, const std::vector<std::vector<bool>>& nbv) {
+        W3D_REQUIRE(nbv.size() == 3 && nbv[0].size() == 2 && nbv[1].size() == 2 && nbv[2].size() == 2,
+                    "shell_split: neighbours as [[x lo, x hi], [y lo, y hi], [z lo, z hi]]");
+        bool nb[3][2];
+        for (int a = 0; a < 3; ++a)
+          for (int s = 0; s < 2; ++s) nb[a][s] = nbv[static_cast<size_t>(a)][static_cast<size_t>(s)];
+        std::vector<LBox> shell;
+        LBox interior;
+        shell_split(full, nb, shell, interior);
+        return py::make_tuple(shell, interior);
+      },
+      "(shell boxes, interior box) of a compute box with neighbours nb[axis][side] (the runtime's own split)");
 
   // ---------------- CPU kernels ----------------
   m.def("cpu_set_threads", &cpu_set_threads);

@@ -191,31 +191,11 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   plan_ = make_halo_plan(lay_, dims_, rank);
   full_ = compute_box(lay_);
 
-  // interior = compute box minus one layer on every side that has a neighbour; shell = the rest, in ≤6 disjoint boxes
+  // interior = compute box minus one layer on every side that has a neighbour; shell = the rest (cpu.hpp shell_split)
   bool nb[3][2];
   for (int a = 0; a < 3; ++a)
     for (int s = 0; s < 2; ++s) nb[a][s] = neighbor_rank(dims_, rank, a, s) >= 0;
-  interior_ = full_;
-  if (nb[0][0]) interior_.x0 += 1;
-  if (nb[0][1]) interior_.x1 -= 1;
-  if (nb[1][0]) interior_.y0 += 1;
-  if (nb[1][1]) interior_.y1 -= 1;
-  if (nb[2][0]) interior_.z0 += 1;
-  if (nb[2][1]) interior_.z1 -= 1;
-  auto push = [&](LBox b) {
-    if (!b.empty()) shell_.push_back(b);
-  };
-  if (!full_.empty()) {
-    const i64 ix0 = imin(imax(interior_.x0, full_.x0), full_.x1), ix1 = imax(interior_.x1, ix0);
-    const i64 iy0 = imin(imax(interior_.y0, full_.y0), full_.y1), iy1 = imax(interior_.y1, iy0);
-    if (nb[0][0]) push(LBox{full_.x0, full_.x0 + 1, full_.y0, full_.y1, full_.z0, full_.z1});
-    if (nb[0][1]) push(LBox{imax(full_.x1 - 1, full_.x0 + (nb[0][0] ? 1 : 0)), full_.x1, full_.y0, full_.y1, full_.z0, full_.z1});
-    if (nb[1][0]) push(LBox{ix0, ix1, full_.y0, full_.y0 + 1, full_.z0, full_.z1});
-    if (nb[1][1]) push(LBox{ix0, ix1, imax(full_.y1 - 1, full_.y0 + (nb[1][0] ? 1 : 0)), full_.y1, full_.z0, full_.z1});
-    if (nb[2][0]) push(LBox{ix0, ix1, iy0, iy1, full_.z0, full_.z0 + 1});
-    if (nb[2][1]) push(LBox{ix0, ix1, iy0, iy1, imax(full_.z1 - 1, full_.z0 + (nb[2][0] ? 1 : 0)), full_.z1});
-  }
-  if (interior_.x1 < interior_.x0 || interior_.y1 < interior_.y0 || interior_.z1 < interior_.z0) interior_ = LBox{};
+  shell_split(full_, nb, shell_, interior_);
 
   // deep-halo slab: the 2 owned planes next to each neighbour are the shell (they are what the neighbours receive);
   // stage-1 values are real one ghost plane beyond each neighbour face

@@ -44,37 +44,10 @@ def all_boxes(N: int, world: int, decomp: str = "slab"):
 
 def split_boxes(layout, neighbors: dict):
     """(shell boxes, interior box) of a rank: the shell is every updated node within one layer of a face that has a
-    neighbour (computed first so its faces can be sent while the interior is updated)."""
+    neighbour (computed first so its faces can be sent while the interior is updated). The native runtime's own split
+    (``shell_split`` in csrc/include/wave3d/cpu.hpp, the one GpuSolver uses), not a re-implementation."""
     C = load()
     full = C.compute_box(layout)
-    if full.empty():
-        return [], full
-    nb = {(a, s): (a, s) in neighbors for a in range(3) for s in range(2)}
-    i = C.LBox(full.x0 + nb[(0, 0)], full.x1 - nb[(0, 1)], full.y0 + nb[(1, 0)], full.y1 - nb[(1, 1)],
-               full.z0 + nb[(2, 0)], full.z1 - nb[(2, 1)])
-    ix0, ix1 = min(max(i.x0, full.x0), full.x1), None
-    ix1 = max(i.x1, ix0)
-    iy0 = min(max(i.y0, full.y0), full.y1)
-    iy1 = max(i.y1, iy0)
-    shell = []
-
-    def push(*a):
-        b = C.LBox(*a)
-        if not b.empty():
-            shell.append(b)
-
-    if nb[(0, 0)]:
-        push(full.x0, full.x0 + 1, full.y0, full.y1, full.z0, full.z1)
-    if nb[(0, 1)]:
-        push(max(full.x1 - 1, full.x0 + nb[(0, 0)]), full.x1, full.y0, full.y1, full.z0, full.z1)
-    if nb[(1, 0)]:
-        push(ix0, ix1, full.y0, full.y0 + 1, full.z0, full.z1)
-    if nb[(1, 1)]:
-        push(ix0, ix1, max(full.y1 - 1, full.y0 + nb[(1, 0)]), full.y1, full.z0, full.z1)
-    if nb[(2, 0)]:
-        push(ix0, ix1, iy0, iy1, full.z0, full.z0 + 1)
-    if nb[(2, 1)]:
-        push(ix0, ix1, iy0, iy1, max(full.z1 - 1, full.z0 + nb[(2, 0)]), full.z1)
-    if i.x1 < i.x0 or i.y1 < i.y0 or i.z1 < i.z0:
-        i = C.LBox(0, 0, 0, 0, 0, 0)
-    return shell, i
+    nb = [[(a, s) in neighbors for s in range(2)] for a in range(3)]
+    shell, interior = C.shell_split(full, nb)
+    return list(shell), interior

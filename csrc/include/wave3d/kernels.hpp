@@ -107,6 +107,8 @@ struct TbPush {
   unsigned* rflag[2] = {nullptr, nullptr};     // this rank's slot in the lower / upper neighbour's flags
   int wait_side[2] = {0, 0};
   unsigned wait_epoch = 0, signal_epoch = 0;
+  unsigned cp_wait = 0;               // host side: epoch the command processor waits for before the launch (0: none)
+  unsigned tag = 0;                   // integrity check: the kernel compares it with its argument (else status = 2)
   unsigned* done = nullptr;           // workgroups done (local counter, zeroed per solve)
   unsigned done_target = 0;
   unsigned* status = nullptr;         // set to 1 when a wait timed out
@@ -116,6 +118,11 @@ struct TbPush {
 // Stage-real ranges of an LDS pass: per axis, where the intermediate levels hold real values (S−1 nodes into the
 // S-deep ghosts towards neighbouring ranks); lo > hi: the axis default (x: compute box, y/z: no restriction).
 inline LBox tb_default_real() { return LBox{1, 0, 1, 0, 1, 0}; }
+// Write back and invalidate every XCD's L2 (and the L1s): enough workgroups to reach every CU each run a system-scope
+// fence. Called once after allocating uncached buffers: lines of the same physical memory that a freed CACHED
+// allocation left dirty in some L2 would otherwise be evicted over the new buffer's contents later (measured: an
+// intermittent O(1) error in a fresh push staging after other solvers had been freed).
+void l2_flush_all(hipStream_t stream);
 // Raise the dynamic-LDS limit of every instantiation (call before capturing launches into a graph).
 void leapfrog_tb_prepare(bool push = false);  // push: also the push-transport instantiations
 size_t leapfrog_tb_lds_bytes(int stages);
@@ -124,7 +131,7 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
                         double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
                         Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream,
                         const LBox& real = tb_default_real(), bool analytic_start = false, int level_stride = 0,
-                        int grid_blocks = 0, const TbPush* push = nullptr);
+                        int grid_blocks = 0, const TbPush* push = nullptr, const TbPush* push_dev = nullptr);
 
 // Error of a stored field vs φ·ct over `box` (step 1 / standalone check). Writes leapfrog-compatible partials and
 // returns how many.

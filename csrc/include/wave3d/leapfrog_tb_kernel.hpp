@@ -16,6 +16,18 @@ namespace tbk {
 
 constexpr int kTile = 32;  // tile edge (y and z)
 
+// Global-address-space views of pointers the kernel reads from memory (the push transport's staging pointers): a
+// generic pointer would turn every load and store through it into a FLAT instruction (and, merged with the field
+// pointers in a select, the hot loads of the march too)
+typedef __attribute__((address_space(1))) double gdouble;
+
+// A pointer read from the push table where it is used (volatile: type-based alias analysis would otherwise let the
+// compiler hoist the load out of the march and keep the pointer in SGPRs for the whole pass — 4 more SGPR pairs, spilled)
+template <class P>
+__device__ __forceinline__ P tb_ptr_at(const P* slot) {
+  return *static_cast<const volatile P*>(slot);
+}
+
 __device__ __forceinline__ void wave_reduce(double& m, double& s) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
@@ -50,49 +62,63 @@ struct TbParams {
   int nty, ntz, nblocks, xcd_remap;
   int lstride;         // partials between consecutive levels (≥ nblocks; larger when several launches share a level)
   int bby, bbz;        // > 0: each XCD's tiles form a bby × bbz block of the tile grid (else two-row strips)
-  TbPush push;         // slab peer-push transport (push.on == 0: off)
+  // slab peer-push transport (PUSH instantiations only): the per-pass parameters stay in device memory and are read
+  // where they are used (pass start and end, ghost-plane loads, face-plane stores), so the march keeps only the two
+  // scalars its tests need in registers (kernel arguments would all be hoisted into SGPRs and spill)
+  const TbPush* push;
+  int pnx, pT;         // push: this rank's planes, ghost depth
+  unsigned ptag;       // push: the tag the table entry must carry
 };
 
-// one spin on a flag in fine-grained / uncached memory: system-scope acquire load
+// Push transport memory protocol. The staging and the flags are uncached device memory (hipDeviceMallocUncached); the
+// forwarded face values are stored with system-scope (write-through) stores and every flag / counter access is a
+// system-scope atomic, so the WRITER needs no cache writeback: a workgroup's forwarded stores are all acknowledged
+// (s_waitcnt before its barrier) before it counts itself done, and the workgroup that completes the count raises the
+// neighbours' flags. (A system-scope release per workgroup instead writes back the whole L2 of its XCD — the field
+// stores' dirty lines included: measured, a third of a pass when thousands of workgroups do it.) The READER still
+// invalidates its XCD's L2 once per workgroup after the wait (system-scope acquire): the staging lines it read two
+// passes earlier (same parity) may be held there, stale, while the neighbour's write-through went to HBM — measured on
+// one GPU, where the neighbour runs on other XCDs: without the invalidate one solve in ~30 read a stale ghost plane.
 __device__ __forceinline__ unsigned tb_flag_load(const unsigned* f) {
-  return __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Push transport, pass start: every workgroup waits until both neighbours have signalled the previous pass (their face
-// planes are in this rank's staging, and they are done reading the staging this pass overwrites on their side). The
-// wait is bounded: after spin_ticks of the wall clock (min(W3D_TIMEOUT_S, 60) s) the workgroup records a timeout and goes on, so
-// a lost peer never leaves waves that do not finish (the host turns the flag into an error).
+// Pass start: every workgroup waits until both neighbours have signalled the previous pass (their face planes are in
+// this rank's staging, and they are done reading the staging this pass overwrites on their side). The wait is bounded:
+// after spin_ticks of the wall clock (min(W3D_TIMEOUT_S, 60) s) the workgroup records a timeout and goes on, so a lost
+// peer never leaves waves that do not finish (the host turns the status into an error).
 __device__ __forceinline__ void tb_push_wait(const TbPush& q) {
-  if (q.wait_epoch == 0) return;
-  if (threadIdx.x == 0) {
-    const unsigned long long t0 = wall_clock64();
-    for (int s = 0; s < 2; ++s) {
-      if (!q.wait_side[s]) continue;
-      while (tb_flag_load(q.flags + s) < q.wait_epoch) {
-        if (wall_clock64() - t0 > q.spin_ticks) {
-          __hip_atomic_store(q.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
+  if (q.wait_epoch != 0) {
+    if (threadIdx.x == 0) {
+      const unsigned long long t0 = wall_clock64();
+      for (int s = 0; s < 2; ++s) {
+        if (!q.wait_side[s]) continue;
+        while (tb_flag_load(q.flags + s) < q.wait_epoch) {
+          if (wall_clock64() - t0 > q.spin_ticks) {
+            __hip_atomic_store(q.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
         }
-        __builtin_amdgcn_s_sleep(2);
       }
     }
+    __syncthreads();
   }
-  __syncthreads();
+  // a pass that reads ghosts from the staging (whichever way it waited: here or by the command processor)
+  if (q.gcur[0] != nullptr || q.gcur[1] != nullptr) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // (system scope)
 }
 
-// Push transport, pass end: every workgroup makes its stores (the forwarded face planes in the neighbours' staging
-// included) visible at system scope, then counts itself done; the last one raises the pass epoch in both neighbours'
-// flag slots for this rank.
+// Pass end: every workgroup's forwarded stores are acknowledged before it counts itself done; the last one raises the
+// pass epoch in both neighbours' flag slots for this rank.
 __device__ __forceinline__ void tb_push_signal(const TbPush& q) {
   if (q.signal_epoch == 0) return;
-  __threadfence_system();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // (waits for this wave's outstanding stores)
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(q.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned old = __hip_atomic_fetch_add(q.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (old + 1 == q.done_target) {
-      __threadfence_system();
       for (int s = 0; s < 2; ++s)
-        if (q.rflag[s]) __hip_atomic_store(q.rflag[s], q.signal_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (q.rflag[s]) __hip_atomic_store(q.rflag[s], q.signal_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -172,7 +198,14 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
 #pragma unroll
   for (int k = 0; k < S; ++k) emax[k] = esum[k] = 0.0;
 
-  if constexpr (PUSH) tb_push_wait(p.push);
+  if constexpr (PUSH) {
+    // the table entry was written by a host-to-device copy: drop any L1 / L2 line of its memory first (system-scope
+    // acquire: invalidates this CU's L1 and the non-local lines of its XCD's L2)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (threadIdx.x == 0 && tb_ptr_at(&p.push->tag) != p.ptag)  // the table entry this launch reads is not its own
+      __hip_atomic_store(p.push->status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    tb_push_wait(*p.push);
+  }
   if (active) {
     // ---- per-thread descriptors of the owned positions (stage-1 region coordinates a, b ∈ [0, H1))
     const int zero_off = p.zero_off;
@@ -277,10 +310,11 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     // exec-mask branching than the arithmetic. Zero-initialised so every value is defined.
     // push transport: the upper face segment [wx1 − T, wx1) first, then [wx0, wx1 − T) (its S − 1 planes next to the
     // seam are recomputed: bit-identical values, not stored); otherwise one segment
-    const int nseg = (PUSH && p.push.faces_first && wx1 == p.x1 && wx1 - wx0 > p.push.T) ? 2 : 1;
+    int nseg = 1;
+    if constexpr (PUSH) nseg = (p.push->faces_first && wx1 == p.x1 && wx1 - wx0 > p.pT) ? 2 : 1;
     for (int seg = 0; seg < nseg; ++seg) {
-    const int x0 = nseg == 1 || seg == 1 ? wx0 : wx1 - p.push.T;
-    const int x1 = nseg == 1 || seg == 0 ? wx1 : wx1 - p.push.T;
+    const int x0 = nseg == 1 || seg == 1 ? wx0 : wx1 - p.pT;
+    const int x1 = nseg == 1 || seg == 0 ? wx1 : wx1 - p.pT;
     if (seg > 0) __syncthreads();  // the first segment's last LDS reads are done before this prologue writes LDS
     double L[S][Q][4] = {};  // L[0] = u^n, L[k] = u^{n+k} (k < S)
     double Lm[Q][2] = {};    // u^{n−1}
@@ -292,12 +326,14 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     const int wbase_r = __builtin_amdgcn_readfirstlane(tid & ~63);
     // plane xs of a field: the ghost planes of a push-transport rank come from its staging (plane 0 = ghost plane −T
     // on the low side, nx on the high side)
-    auto plane_ptr = [&](const double* fld, const double* glo, const double* ghi, int xs) -> const double* {
+    auto plane_ptr = [&](const double* fld, const double* const* gh, int xs) -> const gdouble* {
       if constexpr (PUSH) {
-        if (xs < 0 && glo) return glo + static_cast<i64>(xs + p.push.T) * P;
-        if (xs >= p.push.nx && ghi) return ghi + static_cast<i64>(xs - p.push.nx) * P;
+        if (static_cast<unsigned>(xs) >= static_cast<unsigned>(p.pnx)) {  // a ghost plane (one scalar test)
+          const double* g = tb_ptr_at(gh + (xs < 0 ? 0 : 1));
+          if (g) return (const gdouble*)(g) + static_cast<i64>(xs < 0 ? xs + p.pT : xs - p.pnx) * P;
+        }
       }
-      return fld + static_cast<i64>(xs + 1) * P;
+      return (const gdouble*)(fld) + static_cast<i64>(xs + 1) * P;
     };
     auto load_cur = [&](auto slot_c, auto rs_c, int x) {
       constexpr int slot = decltype(slot_c)::value, rs = decltype(rs_c)::value;
@@ -310,7 +346,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
           if (wbase_r + r * NT < G::NR) Rg[r][rs] = u1_at(x, lrid[r], grof[r] & kLd);
       } else {
         const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;  // always an allocated plane
-        const double* base = plane_ptr(p.cur, p.push.gcur[0], p.push.gcur[1], xs);
+        const gdouble* base = plane_ptr(p.cur, PUSH ? p.push->gcur : nullptr, xs);
 #pragma unroll
         for (int q = 0; q < Q; ++q)
           if (wsm[q]) L[0][q][slot] = base[gof[q] & kOff];
@@ -326,7 +362,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
           if (wsm[q]) Lm[q][slot] = phi_at(x, lid[q]);
       } else {
         const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
-        const double* base = plane_ptr(p.prev, p.push.gprev[0], p.push.gprev[1], xs);
+        const gdouble* base = plane_ptr(p.prev, PUSH ? p.push->gprev : nullptr, xs);
 #pragma unroll
         for (int q = 0; q < Q; ++q)
           if (wsm[q]) Lm[q][slot] = base[gof[q] & kOff];
@@ -452,11 +488,16 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
             // push transport: the face planes a neighbour reads as ghosts (u^{n+S}: T deep, u^{n+S−1}: T − 1 deep)
             // also go straight into its staging
             if constexpr (PUSH) {
-              const int d = k == S ? p.push.T : p.push.T - 1;
-              double* const* f = k == S ? p.push.fwd2 : p.push.fwd1;
-              const i64 off = g & kOff;
-              if (f[0] && xp < d) f[0][static_cast<i64>(xp) * P + off] = v;
-              if (f[1] && xp >= p.push.nx - d) f[1][static_cast<i64>(xp - p.push.nx + p.push.T) * P + off] = v;
+              const int d = k == S ? p.pT : p.pT - 1;
+              if (xp < d) {
+                gdouble* f = (gdouble*)tb_ptr_at((k == S ? p.push->fwd2 : p.push->fwd1) + 0);
+                if (f) __hip_atomic_store(f + static_cast<i64>(xp) * P + (g & kOff), v, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_SYSTEM);
+              } else if (xp >= p.pnx - d) {
+                gdouble* f = (gdouble*)tb_ptr_at((k == S ? p.push->fwd2 : p.push->fwd1) + 1);
+                if (f) __hip_atomic_store(f + static_cast<i64>(xp - p.pnx + p.pT) * P + (g & kOff), v, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_SYSTEM);
+              }
             }
           }
         }
@@ -568,7 +609,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     }
     }  // segments
   }
-  if constexpr (PUSH) tb_push_signal(p.push);
+  if constexpr (PUSH) tb_push_signal(*p.push);
 
   if (p.partials == nullptr) return;
   __shared__ double red_m[NT / 64], red_s[NT / 64];

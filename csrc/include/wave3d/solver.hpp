@@ -293,6 +293,10 @@ class GpuSolver {
   unsigned* peer_flags_[2] = {nullptr, nullptr};
   bool peer_ipc_[2] = {false, false};          // opened with hipIpcOpenMemHandle (closed in the destructor)
   int push_epoch_ = 0;                         // passes of the earlier solves (push_cp_wait: epochs run on)
+  TbPush* push_host_ = nullptr;                // per pass of a solve (pinned), uploaded at its start ...
+  TbPush* push_dev_ = nullptr;                 // ... to this device table the passes read
+  TbPush make_push(int j, int npass) const;    // pass j (1-based) of npass
+  mutable unsigned push_uid_ = 0;              // solver instance number (table tags)
   i64 stg_off(int par, int field, int side) const { return ((par * 2 + field) * 2 + side) * lay_.xg * lay_.plane; }
   void connect_push_peer(int side, double* stg, unsigned* flags, bool ipc);
   void push_finish(hipStream_t st);  // end of a solve: zero this rank's flags (after its last wait)

@@ -36,6 +36,20 @@ namespace wave3d {
 
 using namespace tbk;
 
+namespace {
+__global__ __launch_bounds__(64) void k_l2_flush() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, ""); }
+}  // namespace
+
+void l2_flush_all(hipStream_t stream) {
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+      hipSuccess)
+    fail("l2 flush: no device");
+  hipLaunchKernelGGL(k_l2_flush, dim3(static_cast<unsigned>(8 * ncu)), dim3(64), 0, stream);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) fail(std::string("l2 flush launch: ") + hipGetErrorString(e));
+}
+
 void leapfrog_tb_prepare(bool push) {
   if (push) prepare_push();
   prepare_nt<2, 512, false>();
@@ -65,7 +79,8 @@ int leapfrog_tb_partials(const Layout& l, const LBox& box, const LeapfrogTbTilin
 void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
                         double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
                         Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, const LBox& real,
-                        bool analytic_start, int level_stride, int grid_blocks, const TbPush* push) {
+                        bool analytic_start, int level_stride, int grid_blocks, const TbPush* push,
+                        const TbPush* push_dev) {
   W3D_REQUIRE(out1 != out2 && (analytic_start || (prev != out1 && prev != out2 && cur != out1 && cur != out2)),
               "leapfrog_tb needs four distinct buffers");
   TbPlan pl = make_plan_tb(l, box, t, real);
@@ -76,7 +91,11 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
     W3D_REQUIRE(push->T == l.xg && push->nx == l.nx && t.stages <= push->T && l.yg == 1 && l.zg == 1,
                 "leapfrog_tb push: slab ranks with T-deep x ghosts only");
     W3D_REQUIRE(push->T >= 2 && l.nx >= push->T, "leapfrog_tb push: a rank needs at least T planes");
-    p.push = *push;
+    W3D_REQUIRE(push_dev != nullptr, "leapfrog_tb push: the pass parameters must be in device memory");
+    p.push = push_dev;
+    p.pnx = push->nx;
+    p.pT = push->T;
+    p.ptag = push->tag;
   }
   // a padded grid (several launches sharing one level's partial slots, each of grid_blocks entries): the extra
   // workgroups have no tile and write (0, 0) partials, so every slot entry a reduction reads is written
@@ -101,9 +120,10 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
   W3D_REQUIRE(level_stride == 0 || level_stride >= pl.nblocks, "leapfrog_tb: level stride below the block count");
   p.lstride = level_stride > 0 ? level_stride : pl.nblocks;
   for (int k = 0; k < 4; ++k) p.ct[k] = (ct != nullptr && k < t.stages) ? ct[k] : 0.0;
-  W3D_REQUIRE(!p.push.on || p.push.signal_epoch == 0 || p.push.done_target % static_cast<unsigned>(pl.nblocks) == 0,
-              "leapfrog_tb push: done_target must be a multiple of the grid (every pass of a solve: one full grid)");
-  if (p.push.on) {
+  if (push != nullptr && push->on && push->signal_epoch != 0)  // (every pass of a solve: one full grid)
+    W3D_REQUIRE(push->done_target % static_cast<unsigned>(pl.nblocks) == 0,
+                "leapfrog_tb push: done_target must be a multiple of the grid");
+  if (push != nullptr && push->on) {
     launch_push(p, pl.nblocks, t.stages, analytic_start, stream);
   } else {
     switch (t.stages) {

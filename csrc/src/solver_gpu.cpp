@@ -267,13 +267,24 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
     W3D_HIP(hipMemset(u_[b], 0, static_cast<size_t>(lay_.bytes())));
   }
   if (push_) {
-    // staging in fine-grained memory (remote stores from the neighbours' passes stay coherent with this GPU's reads),
-    // flags in uncached memory (polled by the kernels and the command processor)
+    // staging and flags in uncached memory: the neighbours' write-through stores and this GPU's reads meet in HBM, no
+    // L2 ever holds them (the protocol needs no cache maintenance, leapfrog_tb_kernel.hpp)
     const size_t sb = static_cast<size_t>(8 * lay_.xg * lay_.plane) * sizeof(double);
-    W3D_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&stg_), sb, hipDeviceMallocFinegrained));
+    const char* mt = std::getenv("W3D_PUSH_STAGING");  // (experiment: "uncached" instead of fine-grained)
+    const unsigned stg_flags = mt && !std::strcmp(mt, "uncached") ? hipDeviceMallocUncached : hipDeviceMallocFinegrained;
+    W3D_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&stg_), sb, stg_flags));
     W3D_HIP(hipMemset(stg_, 0, sb));
     W3D_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), 256, hipDeviceMallocUncached));
+    l2_flush_all(nullptr);  // (no stale dirty line of a freed cached buffer may land on them later: kernels.hpp)
+    W3D_HIP(hipDeviceSynchronize());
+    W3D_HIP(hipMemset(stg_, 0, sb));
     W3D_HIP(hipMemset(flags_, 0, 256));
+    const size_t tb = static_cast<size_t>(prob_.K) * sizeof(TbPush);  // (a solve has at most K passes)
+    W3D_HIP(hipHostMalloc(reinterpret_cast<void**>(&push_host_), tb, hipHostMallocDefault));
+    // (uncached too: the table is rewritten by host-to-device copies, which a kernel must never read through an L2
+    // line the same memory held for an earlier, freed buffer — measured: a fresh solver's passes read the previous
+    // solver's table there and pushed into its freed staging)
+    W3D_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&push_dev_), tb, hipDeviceMallocFinegrained));
     // (stream memops are not captured into graphs; running epochs are per-launch arguments)
     if (opt_.push_cp_wait || opt_.push_no_collective) opt_.graph = false;
   }
@@ -343,6 +354,8 @@ GpuSolver::~GpuSolver() {
       (void)hipIpcCloseMemHandle(peer_flags_[k]);
     }
   if (stg_) (void)hipFree(stg_);
+  if (push_host_) (void)hipHostFree(push_host_);
+  if (push_dev_) (void)hipFree(push_dev_);
   if (flags_) (void)hipFree(flags_);
   if (s0_ && own_s0_) (void)hipStreamDestroy(s0_);
   if (s1_) (void)hipStreamDestroy(s1_);
@@ -611,6 +624,13 @@ void GpuSolver::phase_init() {
   cur_ = 1;
   old_ = 0;
   build_units();
+  if (push_) {  // every pass's push parameters, in device memory before the first pass reads them
+    const int npass = static_cast<int>(units_.size());
+    W3D_REQUIRE(npass <= prob_.K, "push: more passes than steps");
+    for (int j = 1; j <= npass; ++j) push_host_[j - 1] = make_push(j, npass);
+    W3D_HIP(hipMemcpyAsync(push_dev_, push_host_, static_cast<size_t>(npass) * sizeof(TbPush), hipMemcpyHostToDevice,
+                           s0_));
+  }
 }
 
 void GpuSolver::unit_shell(int i) {
@@ -724,57 +744,23 @@ void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase) {
   W3D_REQUIRE(tb_slots_ < slots, "leapfrog_tb: too many launches in one unit");
   Partial* part = mask ? tb_partials_ + tb_region_ * (4 * slots * n_tb_) + tb_slots_ * n_tb_ : nullptr;
   const LBox real = mode_ == Mode::kDeepTb ? sreal_ : tb_default_real();
-  // push transport: pass j (1-based) forwards its faces into the neighbours' staging of parity j % 2, reads its ghosts
-  // from its own staging of parity (j − 1) % 2 (pass 1: from the field, filled by the init / the loaded state), waits
-  // for both neighbours' pass j − 1 and signals its own (all but the last pass: nobody waits for that one)
-  TbPush q;
+  // push transport: this pass's parameters (make_push) from the table phase_init uploaded; the command-processor
+  // waits (push_cp_wait) are stream operations issued here, before the launch
+  const TbPush* qh = nullptr;
+  const TbPush* qd = nullptr;
   if (push_) {
-    const int j = cur_unit_ + 1, npass = static_cast<int>(units_.size());
-    W3D_REQUIRE(peer_flags_[0] || !nb_lo_, "push transport: lower neighbour not connected");
-    W3D_REQUIRE(peer_flags_[1] || !nb_hi_, "push transport: upper neighbour not connected");
-    q.on = 1;
-    q.faces_first = opt_.overlap ? 1 : 0;
-    q.T = static_cast<int>(lay_.xg);
-    q.nx = static_cast<int>(lay_.nx);
-    q.flags = flags_;
-    q.status = flags_ + 4;
-    q.done = flags_ + 8;
-    // epochs: in-kernel waits (graph-replayable) use the pass index j of the solve, every pass but the last signals
-    // and the flags are reset at the end of the solve, before its closing collective (which every multi-process run
-    // with in-kernel waits has: the error all-gather); command-processor waits use a pass counter that runs on over
-    // the solves, every pass signals and pass 1 waits for the neighbours' last pass of the previous solve (no reset,
-    // no collective needed)
-    const bool mono = opt_.push_cp_wait || opt_.push_no_collective;
-    const unsigned G = static_cast<unsigned>(mono ? push_epoch_ + j : j);
-    const unsigned wait = mono ? G - 1 : (j > 1 ? G - 1 : 0u);
-    q.wait_epoch = opt_.push_cp_wait ? 0u : wait;
-    q.signal_epoch = (mono || j < npass) ? G : 0u;
-    q.done_target = q.signal_epoch ? static_cast<unsigned>(j * n_tb_) : 0u;
-    static const unsigned long long ticks = [] {
-      int khz = 100000;
-      (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
-      return static_cast<unsigned long long>(std::min(gpu_timeout_s(), 60.0) * 1e3 * khz);
-    }();
-    q.spin_ticks = ticks;
-    const int par = j % 2, rpar = (j - 1) % 2;
-    for (int side = 0; side < 2; ++side) {
-      if (!(side == 0 ? nb_lo_ : nb_hi_)) continue;
-      q.fwd1[side] = peer_stg_[side] + stg_off(par, 0, 1 - side);  // the neighbour's ghosts on the side facing us
-      q.fwd2[side] = peer_stg_[side] + stg_off(par, 1, 1 - side);
-      if (j > 1) {
-        q.gprev[side] = stg_ + stg_off(rpar, 0, side);
-        q.gcur[side] = stg_ + stg_off(rpar, 1, side);
-      }
-      q.rflag[side] = peer_flags_[side] + (1 - side);  // our slot in the neighbour's flags
-      q.wait_side[side] = 1;
-      if (opt_.push_cp_wait && wait > 0)
-        W3D_HIP(hipStreamWaitValue32(s0_, flags_ + side, wait, hipStreamWaitValueGte, 0xFFFFFFFFu));
-    }
+    const int j = cur_unit_ + 1;
+    qh = push_host_ + (j - 1);
+    qd = push_dev_ + (j - 1);
+    if (opt_.push_cp_wait)
+      for (int side = 0; side < 2; ++side)
+        if (qh->wait_side[side] && qh->cp_wait > 0)
+          W3D_HIP(hipStreamWaitValue32(s0_, flags_ + side, qh->cp_wait, hipStreamWaitValueGte, 0xFFFFFFFFu));
   }
   timed(phase, s0_, [&] {
     // (every launch fills its whole slot of n_tb_ partials: shell and interior boxes may have fewer x chunks)
     launch_leapfrog_tb(lay_, coef_, u_[old_], u_[cur_], u_[uf_[0]], u_[uf_[1]], box, d_s_ + 1, cts, mask, part, t,
-                       s0_, real, u.analytic, slots * n_tb_, n_tb_, push_ ? &q : nullptr);
+                       s0_, real, u.analytic, slots * n_tb_, n_tb_, qh, qd);
   });
   if (mask) ++tb_slots_;
 }
@@ -1033,6 +1019,57 @@ RunResult GpuSolver::run() {
 // ------------------------------------------------------------------------------------------------------------------
 // push transport (slab LDS passes): peers, IPC, end of solve
 // ------------------------------------------------------------------------------------------------------------------
+// Pass j (1-based) of npass forwards its faces into the neighbours' staging of parity j % 2, reads its ghosts from its
+// own staging of parity (j − 1) % 2 (pass 1: from the field, filled by the init / the loaded state), waits for both
+// neighbours' pass j − 1 and signals its own. Epochs: in-kernel waits (graph-replayable) use the pass index j, every
+// pass but the last signals (nobody waits for that one) and the flags are reset at the end of the solve, before its
+// closing collective (which every multi-process run with in-kernel waits has: the error all-gather). Without a closing
+// collective (push_no_collective) or with command-processor waits the epochs run on over the solves, every pass
+// signals and pass 1 waits for the neighbours' last pass of the previous solve (no reset needed).
+TbPush GpuSolver::make_push(int j, int npass) const {
+  W3D_REQUIRE(peer_flags_[0] || !nb_lo_, "push transport: lower neighbour not connected");
+  W3D_REQUIRE(peer_flags_[1] || !nb_hi_, "push transport: upper neighbour not connected");
+  TbPush q;
+  q.on = 1;
+  q.faces_first = opt_.overlap ? 1 : 0;
+  q.T = static_cast<int>(lay_.xg);
+  q.nx = static_cast<int>(lay_.nx);
+  q.flags = flags_;
+  q.status = flags_ + 4;
+  q.done = flags_ + 8;
+  const bool mono = opt_.push_cp_wait || opt_.push_no_collective;
+  const unsigned G = static_cast<unsigned>(mono ? push_epoch_ + j : j);
+  const unsigned wait = mono ? G - 1 : (j > 1 ? G - 1 : 0u);
+  q.wait_epoch = opt_.push_cp_wait ? 0u : wait;
+  q.cp_wait = opt_.push_cp_wait ? wait : 0u;
+  q.signal_epoch = (mono || j < npass) ? G : 0u;
+  q.done_target = q.signal_epoch ? static_cast<unsigned>(j * n_tb_) : 0u;
+  static const unsigned long long ticks = [] {
+    int khz = 100000;
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
+    return static_cast<unsigned long long>(std::min(gpu_timeout_s(), 60.0) * 1e3 * khz);
+  }();
+  q.spin_ticks = ticks;
+  // (tag: unique per solver instance, rank, solve and pass, so a table entry left by another solver never matches)
+  static unsigned instances = 0;
+  if (push_uid_ == 0) push_uid_ = ++instances;
+  q.tag = (push_uid_ * 2654435761u) ^ (static_cast<unsigned>(rank_) << 20) ^
+          (static_cast<unsigned>(push_epoch_ & 0xFFF) << 8) ^ static_cast<unsigned>(j);
+  const int par = j % 2, rpar = (j - 1) % 2;
+  for (int side = 0; side < 2; ++side) {
+    if (!(side == 0 ? nb_lo_ : nb_hi_)) continue;
+    q.fwd1[side] = peer_stg_[side] + stg_off(par, 0, 1 - side);  // the neighbour's ghosts on the side facing us
+    q.fwd2[side] = peer_stg_[side] + stg_off(par, 1, 1 - side);
+    if (j > 1) {
+      q.gprev[side] = stg_ + stg_off(rpar, 0, side);
+      q.gcur[side] = stg_ + stg_off(rpar, 1, side);
+    }
+    q.rflag[side] = peer_flags_[side] + (1 - side);  // our slot in the neighbour's flags
+    q.wait_side[side] = 1;
+  }
+  return q;
+}
+
 std::string GpuSolver::push_handles() const {
   W3D_REQUIRE(push_, "push_handles: this solver does not use the push transport");
   hipIpcMemHandle_t h[2];
@@ -1083,6 +1120,7 @@ void GpuSolver::push_check() {
   if (!push_) return;
   unsigned st = 0;
   W3D_HIP(hipMemcpy(&st, flags_ + 4, sizeof st, hipMemcpyDeviceToHost));
+  W3D_REQUIRE(st != 2, "push transport: a pass read a stale parameter table (rank " + std::to_string(rank_) + ")");
   W3D_REQUIRE(st == 0, "push transport: a pass timed out waiting for a neighbour's signal (rank " +
                            std::to_string(rank_) + ")");
 }

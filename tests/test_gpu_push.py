@@ -18,7 +18,6 @@ import json
 import math
 import os
 import subprocess
-import uuid
 
 import numpy as np
 import pytest

@@ -8,6 +8,8 @@
 #   scripts/gpu.sh profbench [bench args]    rocprofv3 kernel trace + stats of bench.py     -> gpurun_out/profbench/
 #   scripts/gpu.sh pmc "<counters>" [wave3d args]  one PMC pass (counters of one block budget) -> gpurun_out/pmc/
 #   scripts/gpu.sh cli [wave3d args]         the reference-config CLI run (512 0.001 20 1)   -> gpurun_out/cli.log
+#   scripts/gpu.sh fakerank                  per-rank solve times (--fake-rank) of the slab schedules: RCCL overlap /
+#                                            sequential, push overlap / sequential, 512^3 ranks 1/8 + 1/2, 2048^3 3/8
 #   scripts/gpu.sh all                       test && cli && bench && profbench
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -55,6 +57,18 @@ run_pmc() {
     ./bin/wave3d 512 0.001 20 1 --repeat 2 --warmup 1 "$@" > gpurun_out/pmc.log 2>&1
 }
 
+run_fakerank() {
+  local fr v
+  for fr in 512:0.001:1/8 512:0.001:1/2 2048:0.00025:3/8; do
+    IFS=: read -r N tau r <<< "$fr"
+    for v in "" "--no-overlap" "--transport push" "--transport push --no-overlap"; do
+      echo "== N=$N fake $r $v"
+      timeout -k 5 120 ./bin/wave3d "$N" "$tau" 20 1 --fake-rank "$r" --repeat 5 --warmup 2 --quiet $v \
+        | grep "Total time" || return 1
+    done
+  done
+}
+
 case "$what" in
   test) run_test "$@" ;;
   bench) run_bench "$@" ;;
@@ -62,6 +76,7 @@ case "$what" in
   prof) run_prof "$@" ;;
   profbench) run_profbench "$@" ;;
   pmc) run_pmc "$@" ;;
+  fakerank) run_fakerank > gpurun_out/fakerank.log 2>&1; rc=$?; cat gpurun_out/fakerank.log; exit $rc ;;
   all) run_test && run_cli && run_bench && run_profbench ;;
   *) echo "unknown step $what" >&2; exit 2 ;;
 esac

@@ -89,7 +89,8 @@ __device__ __forceinline__ unsigned tb_flag_load(const unsigned* f) {
 // peer never leaves waves that do not finish (the host turns the status into an error).
 __device__ __forceinline__ void tb_push_wait(const TbPush& q) {
   if (q.wait_epoch != 0) {
-    if (threadIdx.x == 0) {
+    // (after one timed-out wait the solve is lost: later passes do not wait again, so it fails in one bound, not K)
+    if (threadIdx.x == 0 && __hip_atomic_load(q.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
       const unsigned long long t0 = wall_clock64();
       for (int s = 0; s < 2; ++s) {
         if (!q.wait_side[s]) continue;

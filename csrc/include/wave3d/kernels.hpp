@@ -77,7 +77,7 @@ void launch_leapfrog2(const Layout& l, const Coeffs& c, const double* prev, cons
 // the kernel (init_first's formulas, bit-identical), prev/cur are not read: it writes u^S, u^{S+1} with no HBM reads.
 struct LeapfrogTbTiling {
   int stages = 4;         // 2, 3 or 4 steps per pass
-  int threads = 1024;     // workgroup size (512 or 1024; 1024 measured faster at every S)
+  int threads = 1024;     // workgroup size (768 or 1024)
   bool xcd_remap = true;  // (stores are always non-temporal: measured faster at every S)
   bool xcd_blocks = false; // with xcd_remap: each XCD owns a square-ish tile block, not two-row strips (measured: no gain)
   int target_blocks = 256; // fewer (y,z) tiles than this: split x into chunks (one workgroup per CU at 1 WG/CU)

@@ -52,9 +52,12 @@ void l2_flush_all(hipStream_t stream) {
 
 void leapfrog_tb_prepare(bool push) {
   if (push) prepare_push();
-  prepare_nt<2, 512, false>();
-  prepare_nt<3, 512, false>();
-  prepare_nt<4, 512, false>();
+  prepare_nt<2, 768, false>();
+  prepare_nt<3, 768, false>();
+  prepare_nt<4, 768, false>();
+  prepare_nt<2, 768, true>();
+  prepare_nt<3, 768, true>();
+  prepare_nt<4, 768, true>();
   prepare_nt<2, 1024, false>();
   prepare_nt<3, 1024, false>();
   prepare_nt<4, 1024, false>();

@@ -1075,7 +1075,10 @@ std::string GpuSolver::push_handles() const {
   hipIpcMemHandle_t h[2];
   W3D_HIP(hipIpcGetMemHandle(&h[0], stg_));
   W3D_HIP(hipIpcGetMemHandle(&h[1], flags_));
-  return std::string(reinterpret_cast<const char*>(h), sizeof h);
+  int dv[2] = {0, 0};  // this rank's device and the visible device count (peer-access check on the other side)
+  W3D_HIP(hipGetDevice(&dv[0]));
+  W3D_HIP(hipGetDeviceCount(&dv[1]));
+  return std::string(reinterpret_cast<const char*>(h), sizeof h) + std::string(reinterpret_cast<const char*>(dv), sizeof dv);
 }
 
 void GpuSolver::connect_push_peer(int side, double* stg, unsigned* flags, bool ipc) {
@@ -1092,8 +1095,20 @@ void GpuSolver::connect_push(const std::vector<std::string>& all) {
     if (peer < 0) continue;
     const std::string& b = all[static_cast<size_t>(peer)];
     hipIpcMemHandle_t h[2];
-    W3D_REQUIRE(b.size() == sizeof h, "connect_push: bad handle size from rank " + std::to_string(peer));
+    int dv[2] = {0, 0};
+    W3D_REQUIRE(b.size() == sizeof h + sizeof dv, "connect_push: bad handle size from rank " + std::to_string(peer));
     std::memcpy(h, b.data(), sizeof h);
+    std::memcpy(dv, b.data() + sizeof h, sizeof dv);
+    // a neighbour on another GPU must be reachable by this GPU's stores (xGMI peer access), else the passes would
+    // fault: refuse here, where the autotune can still drop the candidate
+    int me = 0, nd = 0;
+    W3D_HIP(hipGetDevice(&me));
+    W3D_HIP(hipGetDeviceCount(&nd));
+    if (dv[1] == nd && dv[0] != me) {
+      int can = 0;
+      W3D_HIP(hipDeviceCanAccessPeer(&can, me, dv[0]));
+      W3D_REQUIRE(can, "push transport: GPU " + std::to_string(me) + " cannot access peer GPU " + std::to_string(dv[0]));
+    }
     void* stg = nullptr;
     void* fl = nullptr;
     W3D_HIP(hipIpcOpenMemHandle(&stg, h[0], hipIpcMemLazyEnablePeerAccess));

@@ -162,7 +162,7 @@ def test_leapfrog2_equals_two_single_steps(gpu, rows, N, target_waves):
 
 @pytest.mark.parametrize("stages", [2, 3, 4])
 @pytest.mark.parametrize("N", [40, 77, 130])
-@pytest.mark.parametrize("threads", [512, 1024])
+@pytest.mark.parametrize("threads", [768, 1024])
 def test_leapfrog_tb_equals_single_steps(gpu, stages, N, threads):
     """Deep temporal blocking: one LDS pass of S steps == S CPU steps, bit for bit, with every level checked."""
     C = gpu

@@ -789,9 +789,16 @@ int run_gpu(const Args& a) {
       }
       if (ref_log.empty()) ref_log = r0.max_err;
       double t = 1e30;
+      bool stable = true;  // the timed solves must reproduce the reference log too (an intermittent transport fault)
       for (int k = 0; k < 3; ++k) {
         if (comm) comm_barrier(*comm);
-        t = std::min(t, cand->run().solve_s);
+        const RunResult rk = cand->run();
+        t = std::min(t, rk.solve_s);
+        stable = stable && rk.finite && rk.max_err == ref_log;
+      }
+      if (!agree(stable)) {
+        std::fprintf(stderr, "[wave3d rank %d] candidate %s rejected: a timed solve's error log differs\n", rank, c.name);
+        continue;
       }
       t = max_over_ranks(t);
       tuned.emplace_back(c.name, t);

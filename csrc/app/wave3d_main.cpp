@@ -777,7 +777,8 @@ int run_gpu(const Args& a) {
         connect(*cand);     // (collective when the candidate pushes: every rank built it)
         r0 = cand->run();   // eager: RCCL peer connections
         r0 = cand->run();   // graph capture
-        same = r0.finite && (ref_log.empty() || r0.max_err == ref_log);
+        // (a fake rank's log holds its own partials only: they differ between decompositions, nothing to compare)
+        same = r0.finite && (fake || ref_log.empty() || r0.max_err == ref_log);
         if (!same) err = "its error log differs from the reference schedule's";
       } catch (const std::exception& e) {
         err = e.what();
@@ -794,7 +795,7 @@ int run_gpu(const Args& a) {
         if (comm) comm_barrier(*comm);
         const RunResult rk = cand->run();
         t = std::min(t, rk.solve_s);
-        stable = stable && rk.finite && rk.max_err == ref_log;
+        stable = stable && rk.finite && (fake || rk.max_err == ref_log);
       }
       if (!agree(stable)) {
         std::fprintf(stderr, "[wave3d rank %d] candidate %s rejected: a timed solve's error log differs\n", rank, c.name);

@@ -109,6 +109,7 @@ struct TbPush {
   unsigned wait_epoch = 0, signal_epoch = 0;
   unsigned cp_wait = 0;               // host side: epoch the command processor waits for before the launch (0: none)
   unsigned tag = 0;                   // integrity check: the kernel compares it with its argument (else status = 2)
+  int acquire = 1;                    // system-scope acquire at the pass start (perf attribution only: 0)
   unsigned* done = nullptr;           // workgroups done (local counter, zeroed per solve)
   unsigned done_target = 0;
   unsigned* status = nullptr;         // set to 1 when a wait timed out

@@ -68,6 +68,7 @@ struct TbParams {
   const TbPush* push;
   int pnx, pT;         // push: this rank's planes, ghost depth
   unsigned ptag;       // push: the tag the table entry must carry
+  int pacq;            // push: acquire at the pass start (TbPush::acquire)
 };
 
 // Push transport memory protocol. The staging and the flags are uncached device memory (hipDeviceMallocUncached); the
@@ -106,7 +107,8 @@ __device__ __forceinline__ void tb_push_wait(const TbPush& q) {
     __syncthreads();
   }
   // a pass that reads ghosts from the staging (whichever way it waited: here or by the command processor)
-  if (q.gcur[0] != nullptr || q.gcur[1] != nullptr) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // (system scope)
+  if ((q.gcur[0] != nullptr || q.gcur[1] != nullptr) && q.acquire)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // (system scope)
 }
 
 // Pass end: every workgroup's forwarded stores are acknowledged before it counts itself done; the last one raises the
@@ -202,7 +204,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
   if constexpr (PUSH) {
     // the table entry was written by a host-to-device copy: drop any L1 / L2 line of its memory first (system-scope
     // acquire: invalidates this CU's L1 and the non-local lines of its XCD's L2)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (p.pacq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     if (threadIdx.x == 0 && tb_ptr_at(&p.push->tag) != p.ptag)  // the table entry this launch reads is not its own
       __hip_atomic_store(p.push->status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     tb_push_wait(*p.push);

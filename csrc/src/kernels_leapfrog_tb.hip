@@ -99,6 +99,7 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
     p.pnx = push->nx;
     p.pT = push->T;
     p.ptag = push->tag;
+    p.pacq = push->acquire;
   }
   // a padded grid (several launches sharing one level's partial slots, each of grid_blocks entries): the extra
   // workgroups have no tile and write (0, 0) partials, so every slot entry a reduction reads is written

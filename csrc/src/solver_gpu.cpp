@@ -1056,11 +1056,17 @@ TbPush GpuSolver::make_push(int j, int npass) const {
   q.tag = (push_uid_ * 2654435761u) ^ (static_cast<unsigned>(rank_) << 20) ^
           (static_cast<unsigned>(push_epoch_ & 0xFFF) << 8) ^ static_cast<unsigned>(j);
   const int par = j % 2, rpar = (j - 1) % 2;
+  // (perf attribution of the transport with --fake-rank only: W3D_PUSH_ATTRIB=nofwd / noghost drop the forwarded
+  // stores / the staging reads — the results are then wrong)
+  const char* attrib = opt_.fake_comm ? std::getenv("W3D_PUSH_ATTRIB") : nullptr;
+  const bool nofwd = attrib && std::strstr(attrib, "nofwd"), noghost = attrib && std::strstr(attrib, "noghost");
+  if (attrib && std::strstr(attrib, "noacq")) q.acquire = 0;
+  if (attrib && std::strstr(attrib, "nosync")) q.wait_epoch = q.signal_epoch = q.done_target = 0;
   for (int side = 0; side < 2; ++side) {
     if (!(side == 0 ? nb_lo_ : nb_hi_)) continue;
-    q.fwd1[side] = peer_stg_[side] + stg_off(par, 0, 1 - side);  // the neighbour's ghosts on the side facing us
-    q.fwd2[side] = peer_stg_[side] + stg_off(par, 1, 1 - side);
-    if (j > 1) {
+    q.fwd1[side] = nofwd ? nullptr : peer_stg_[side] + stg_off(par, 0, 1 - side);  // the neighbour's ghosts facing us
+    q.fwd2[side] = nofwd ? nullptr : peer_stg_[side] + stg_off(par, 1, 1 - side);
+    if (j > 1 && !noghost) {
       q.gprev[side] = stg_ + stg_off(rpar, 0, side);
       q.gcur[side] = stg_ + stg_off(rpar, 1, side);
     }

@@ -388,24 +388,29 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     // bit-identical to k_init_first's; 2 products + 4 LDS reads instead of 12 products + 9 table reads per node.
     // The halo ring (no φ neighbours beyond it in LDS) keeps u1_at.
     // (S = 4: the queues leave no room for them — the factors are re-read from the LDS tables per use instead)
-    constexpr bool kFacReg = S < 4;
+    // (768-thread workgroups have 168 VGPRs per wave: the factors — and the check's row-table index — fit at S = 4 too)
+    constexpr bool kFacReg = S < 4 || NT <= 768;
     double fy[Q], fz[Q], fyr[QR], fzr[QR];
+    int yix[Q];  // check: row-table index of each position (kFacReg)
     // (the check's z factor of a position is re-read from the LDS table per use: keeping it in a register per position
     // spills at S = 4 since the y/z stage-real ranges of the block ranks were added)
     auto fyq = [&](int q) { return kFacReg ? fy[q] : syw[ytab(lid[q])]; };
     auto fzq = [&](int q) { return kFacReg ? fz[q] : szw[ztab(lid[q])]; };
     auto fyrr = [&](int r) { return kFacReg ? fyr[r] : syw[ytab(lrid[r])]; };
     auto fzrr = [&](int r) { return kFacReg ? fzr[r] : szw[ztab(lrid[r])]; };
-    if constexpr (INIT && kFacReg) {
+    if constexpr ((INIT || CM != 0) && kFacReg) {
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
-        fy[q] = syw[ytab(lid[q])];
+        yix[q] = ytab(lid[q]);
+        fy[q] = syw[yix[q]];
         fz[q] = szw[ztab(lid[q])];
       }
+      if constexpr (INIT) {
 #pragma unroll
-      for (int r = 0; r < QR; ++r) {
-        fyr[r] = syw[ytab(lrid[r])];
-        fzr[r] = szw[ztab(lrid[r])];
+        for (int r = 0; r < QR; ++r) {
+          fyr[r] = syw[ytab(lrid[r])];
+          fzr[r] = szw[ztab(lrid[r])];
+        }
       }
     }
     auto lds_phi = [&](int par) { return lds + (S * 2 + par) * PLP; };
@@ -506,7 +511,8 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         }
         if constexpr (kChk) {
           if (chk && own && xreal) {
-            const double e = fabs(v - (rowk[ytab(li)] * szw[ztab(li)]) * p.ct[k - 1]);
+            const double e = fabs(v - (rowk[kFacReg ? yix[q] : ytab(li)] * (kFacReg ? fz[q] : szw[ztab(li)])) *
+                                          p.ct[k - 1]);
             emax[k - 1] = fmax(e, emax[k - 1]);  // = (e > m ? e : m) for every non-NaN e; a NaN shows in the sum
             esum[k - 1] += e * e;
           }

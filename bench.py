@@ -73,7 +73,12 @@ def _args(argv=None):
     ap.add_argument("--allow-fallback", action="store_true",
                     help="if the native runtime fails, re-run over the torch transport (marked degraded)")
     ap.add_argument("--share-gpus", action="store_true",
-                    help="rehearsal: allow more ranks than visible GPUs (ranks share GPUs; RCCL refuses this)")
+                    help="rehearsal: allow more ranks than visible GPUs (ranks share GPUs; RCCL refuses this, so use it "
+                         "with --no-rccl --native-transport push; each rank then gets its own share of the CUs)")
+    ap.add_argument("--native-transport", default="rccl", choices=["rccl", "push"],
+                    help="halo transport of the native runtime with --no-autotune (push: slab passes forward their faces)")
+    ap.add_argument("--no-rccl", action="store_true",
+                    help="native ranks without an RCCL communicator (push only; host collectives through files)")
     ap.add_argument("--timeout", type=float, default=900.0, help="seconds before a native rank is killed")
     ap.add_argument("--out", default="", help="also append the JSON line to this file")
     return ap.parse_args(argv)
@@ -145,7 +150,11 @@ def run_native(a, rank: int, world: int, local: int) -> int:
     if a.cpu:
         cmd.append("--cpu")
     else:
-        if (multi or a.autotune) and not a.no_autotune:
+        if a.native_transport == "push":
+            cmd += ["--transport", "push"]
+        if a.no_rccl:
+            cmd.append("--no-rccl")
+        if (multi or a.autotune) and not a.no_autotune and not a.no_rccl:
             cmd.append("--autotune")
         if not a.no_phases:
             cmd.append("--phases")
@@ -157,6 +166,8 @@ def run_native(a, rank: int, world: int, local: int) -> int:
                W3D_JOB_ID=f"bench{nonce}", W3D_TIMEOUT_S=os.environ.get("W3D_TIMEOUT_S", "180"))
     if a.share_gpus:
         env["W3D_SHARE_GPUS"] = "1"
+        if multi and _distinct_gpus(world) < world:
+            env["W3D_CU_SPLIT"] = "auto"  # concurrent ranks on one GPU: disjoint CU ranges (in-kernel push waits)
     fail_rank = os.environ.get("W3D_BENCH_FAIL_SETUP_RANK")  # fault injection (tests)
     if fail_rank is not None:
         env["W3D_FAULT_RANK"] = fail_rank
@@ -244,6 +255,8 @@ def run_native(a, rank: int, world: int, local: int) -> int:
             "phases_ms": res.get("phases_ms"),
             "distinct_gpus": None if a.cpu else _distinct_gpus(world),
         }
+        if not a.cpu and multi and extra["distinct_gpus"] < world:
+            extra["rehearsal"] = f"{world} ranks sharing {extra['distinct_gpus']} GPU(s): not a scaling point"
         _emit(a, _line(a, world, value, ms, cfg, extra))
         return 0 if correct else 1
     return 0

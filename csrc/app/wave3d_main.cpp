@@ -655,9 +655,9 @@ constexpr Candidate kCandidates[] = {
 
 // Every rank's bytes through files next to the rendezvous file (ranks without a communicator: --no-rccl). Each rank
 // publishes <rdzv>.push<rank> atomically and reads the others' (written after this process started).
-std::vector<std::string> file_allgather(int rank, int world, const std::string& mine) {
+std::vector<std::string> file_allgather(int rank, int world, const std::string& mine, const std::string& tag = "push") {
   static const double t_start = static_cast<double>(std::time(nullptr));
-  auto path = [](int r) { return rdzv_path() + ".push" + std::to_string(r); };
+  auto path = [&](int r) { return rdzv_path() + "." + tag + std::to_string(r); };
   {
     const std::string tmp = path(rank) + ".tmp";
     std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
@@ -679,7 +679,7 @@ std::vector<std::string> file_allgather(int rank, int world, const std::string& 
           break;
         }
       }
-      if (now_s() - t0 > 120.0) fail("timed out waiting for " + path(r));
+      if (now_s() - t0 > 120.0) fail("timed out waiting for " + path(r));  // (a peer that died)
       std::this_thread::sleep_for(std::chrono::milliseconds(20));
     }
   }
@@ -728,7 +728,32 @@ int run_gpu(const Args& a) {
   auto agree = [&](bool ok) {
     return comm ? comm_allreduce(*comm, ok ? 1.0 : 0.0, false) == static_cast<double>(world) : ok;
   };
-  auto max_over_ranks = [&](double v) { return comm ? comm_allreduce(*comm, v, true) : v; };
+  // ranks without a communicator (--no-rccl push rehearsal): host collectives through files, outside timed regions
+  const bool file_coll = !comm && world > 1 && !fake;
+  int fcoll = 0;
+  std::vector<std::string> fcoll_files;
+  auto fgather = [&](const std::string& mine) {
+    const std::string tag = "c" + std::to_string(fcoll++) + "r";
+    fcoll_files.push_back(rdzv_path() + "." + tag + std::to_string(rank));
+    return file_allgather(rank, world, mine, tag);
+  };
+  auto max_over_ranks = [&](double v) {
+    if (comm) return comm_allreduce(*comm, v, true);
+    if (!file_coll) return v;
+    double m = v;
+    for (const std::string& b : fgather(std::string(reinterpret_cast<const char*>(&v), sizeof v))) {
+      double x = 0.0;
+      std::memcpy(&x, b.data(), sizeof x);
+      m = std::max(m, x);
+    }
+    return m;
+  };
+  auto barrier = [&]() {
+    if (comm)
+      comm_barrier(*comm);
+    else if (file_coll)
+      (void)fgather("b");
+  };
 
   W3D_REQUIRE(!a.no_rccl || world == 1 || fake || (a.transport == "push" && !a.autotune),
               "--no-rccl: ranks without a communicator can only run the push transport (no autotune)");
@@ -823,7 +848,7 @@ int run_gpu(const Args& a) {
   RunResult r;
   double best = 1e30, sum = 0, first = 0;
   for (int i = 0; i < a.warmup + a.repeat; ++i) {
-    if (comm) comm_barrier(*comm);
+    barrier();
     r = s->run();
     const double t = max_over_ranks(r.solve_s);
     if (i == 0) first = t;
@@ -837,18 +862,18 @@ int run_gpu(const Args& a) {
   double bench_s = 0.0;
   if (a.bench_steps > 0) {
     W3D_HIP(hipDeviceSynchronize());
-    if (comm) comm_barrier(*comm);
+    barrier();
     const double t0 = now_s();
     for (int i = 0; i < a.bench_steps; ++i) r = s->run();
     W3D_HIP(hipDeviceSynchronize());
-    if (comm) comm_barrier(*comm);
+    barrier();
     bench_s = max_over_ranks(now_s() - t0);
   }
   // per-phase breakdown of the schedule that was timed: one more solve with the same kernels, traced with events
   PhaseTimes ph;
   if (a.phases && !a.timers) {
     s->set_timers(true);  // same solver, same schedule and kernels, launched eagerly with events around each phase
-    if (comm) comm_barrier(*comm);
+    barrier();
     ph = s->run().phases;
     s->set_timers(false);
     ph.init_ms = max_over_ranks(ph.init_ms);
@@ -857,6 +882,25 @@ int run_gpu(const Args& a) {
     ph.comm_ms = max_over_ranks(ph.comm_ms);
     ph.check_ms = max_over_ranks(ph.check_ms);
     ph.gather_ms = max_over_ranks(ph.gather_ms);
+  }
+  if (file_coll) {  // the last solve's error log over all ranks (L∞: max; RMS: from the per-rank Σe² shares)
+    std::string mine;
+    for (size_t i = 0; i < r.steps.size(); ++i) {
+      const double v[2] = {r.max_err[i], r.rms_err[i] * r.rms_err[i]};
+      mine.append(reinterpret_cast<const char*>(v), sizeof v);
+    }
+    const std::vector<std::string> all = fgather(mine);
+    for (size_t i = 0; i < r.steps.size(); ++i) {
+      double m = 0.0, q = 0.0;
+      for (const std::string& b : all) {
+        double v[2];
+        std::memcpy(v, b.data() + i * sizeof v, sizeof v);
+        m = v[0] > m || std::isnan(v[0]) ? v[0] : m;
+        q += v[1];
+      }
+      r.max_err[i] = m;
+      r.rms_err[i] = std::sqrt(q);
+    }
   }
   const double mean = sum / a.repeat;
   const double t_proc = now_s() - t_proc0;
@@ -928,6 +972,9 @@ int run_gpu(const Args& a) {
   if (!a.checkpoint.empty())
     write_checkpoint(a.checkpoint, a.prob, s->layout(), s->download(0), s->download(1), rank, world, d);
   if (s->push() && !comm && !fake) std::remove((rdzv_path() + ".push" + std::to_string(rank)).c_str());
+  // (a peer may still be reading this rank's file of the LAST collective: it stays; every earlier one has been read by
+  // everyone, since every peer has entered a later collective — removing a file a peer still needs hangs that peer)
+  for (size_t i = 0; i + 1 < fcoll_files.size(); ++i) std::remove(fcoll_files[i].c_str());
   return r.finite ? 0 : 3;
 }
 

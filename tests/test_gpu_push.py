@@ -18,6 +18,7 @@ import json
 import math
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -126,6 +127,23 @@ def test_push_two_processes_in_kernel_waits(gpu, tmp_path):
            "--dump", prefix, "--quiet"]
     subprocess.run(cmd, check=True, timeout=150, env=env, capture_output=True, text=True)
     assert np.array_equal(_read_dump(prefix, 2, N), f1)
+
+
+def test_bench_two_ranks_rehearsal(gpu, tmp_path):
+    """bench.py end to end with 2 ranks on one GPU: torch.distributed.run → bench.py ranks (gloo nonce) → native runtime
+    children (IPC push transport, in-kernel waits on disjoint CU halves, host collectives through files) → one JSON
+    line whose log is the reference's (combined over both ranks) and which says it is a rehearsal, not a scaling point."""
+    out = tmp_path / "b.jsonl"
+    env = dict(os.environ, W3D_TIMEOUT_S="60")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(29700 + os.getpid() % 200), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--share-gpus", "--no-rccl", "--native-transport", "push", "--steps", "5", "--warmup", "2",
+           "--out", str(out)]
+    subprocess.run(cmd, check=True, timeout=240, env=env, capture_output=True, text=True)
+    line = json.loads(out.read_text().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["distinct_gpus"] == 1 and "rehearsal" in line
+    assert line["config"]["transport"] == "push" and line["config"]["schedule"].endswith("-push")
+    assert line["correct"] is True and line["final_max_err"] == pytest.approx(3.960129e-09, rel=1e-6)
 
 
 def test_push_fake_rank_runs(gpu, tmp_path):

@@ -431,6 +431,9 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("debug_sync", &SolverOptions::debug_sync)
       .def_readwrite("poison_ghosts", &SolverOptions::poison_ghosts)
       .def_readwrite("fake_comm", &SolverOptions::fake_comm)
+      .def_readwrite("push", &SolverOptions::push)
+      .def_readwrite("push_cp_wait", &SolverOptions::push_cp_wait)
+      .def_readwrite("push_no_collective", &SolverOptions::push_no_collective)
       .def_readwrite("temporal", &SolverOptions::temporal)
       .def_readwrite("init2", &SolverOptions::init2)
       .def_readwrite("deep_min_planes", &SolverOptions::deep_min_planes)
@@ -460,6 +463,15 @@ PYBIND11_MODULE(_C, m) {
            }),
            py::arg("problem"), py::arg("options"), py::arg("rank") = 0, py::arg("world") = 1,
            py::arg("comm") = nullptr)
+      .def_property_readonly("push", &GpuSolver::push)
+      .def("push_handles", [](const GpuSolver& s) { return py::bytes(s.push_handles()); },
+           "this rank's IPC handles (staging, flags) + device, to be all-gathered")
+      .def("connect_push", [](GpuSolver& s, const std::vector<py::bytes>& all) {
+             std::vector<std::string> v;
+             for (const py::bytes& b : all) v.emplace_back(b);
+             s.connect_push(v);
+           },
+           "open the slab neighbours' staging and flags from every rank's push_handles() (index = rank)")
       .def("run",
            [](GpuSolver& s) {
              RunResult r;

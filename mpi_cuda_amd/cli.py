@@ -27,8 +27,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("K", type=int, help="number of steps")
     ap.add_argument("L", type=float, nargs="?", default=1.0, help="cube edge (default 1)")
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "cpu", "torch"])
-    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "torch", "loopback", "rccl-self", "native",
-                                                               "none"])
+    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "torch", "loopback", "rccl-self", "push",
+                                                               "push-ipc", "native", "none"])
     ap.add_argument("--world", type=int, default=0,
                     help="ranks of an in-process group on one GPU (transport loopback, or rccl-self: RCCL send/recv)")
     ap.add_argument("--decomp", default="slab", help="slab | block | PxQxR")
@@ -79,7 +79,7 @@ def main(argv=None) -> int:
         kw["device"] = local if a.world == 0 else 0
         kw["timers"] = a.timers
     if a.world:
-        kw.update(transport="rccl-self" if transport == "rccl-self" else "loopback", rank=0, world=a.world)
+        kw.update(transport=transport if transport in ("rccl-self", "push") else "loopback", rank=0, world=a.world)
     s = Solver(spec, **kw)
     if a.resume:
         prev, meta = dumpio.load(a.resume + ".prev")
@@ -117,7 +117,7 @@ def main(argv=None) -> int:
                            "steps": [[n, m, e] for n, m, e in zip(r.steps, r.max_err, r.rms_err)]}, f)
     if a.dump or a.checkpoint:
         def write(prefix, which):
-            if s.transport in ("loopback", "rccl-self"):
+            if s.transport in ("loopback", "rccl-self", "push"):
                 if rank == 0:
                     dumpio.save(prefix, s.global_field(which).numpy(), N=a.N, L=a.L, tau=a.tau,
                                 step=a.K - which)

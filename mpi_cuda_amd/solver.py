@@ -12,8 +12,10 @@ hip        loopback    native GpuGroup: all ranks of a decomposition in THIS pro
                        (exercises the production multi-rank C++ path on a single GPU; tests)
 hip        rccl-self   native GpuGroup as above, halos moved by the production RCCL ncclSend/ncclRecv calls, each rank
                        over its own one-rank communicator (RCCL refuses 2 ranks of one communicator on one GPU)
-hip        push        native GpuGroup as above on the slab LDS passes, halos pushed by the passes themselves into the
-                       neighbours' fine-grained staging + flag signalling (the multi-process push transport's data path)
+hip        push        world > 1 in ONE process: native GpuGroup as above on the slab LDS passes, halos pushed by the
+                       passes themselves into the neighbours' fine-grained staging + flag signalling
+hip        push-ipc    one process per rank (torchrun): native GpuSolver on the slab LDS passes with the push transport
+                       between processes (IPC handles all-gathered over torch.distributed; RCCL for the error log)
 cpu        native      C++ CpuSolver, OpenMP (the reference's sequential / OpenMP programs), world == 1
 cpu        torch       Python step loop, native OpenMP kernels, halos over torch.distributed gloo (MPI analogue)
 torch      -           plain PyTorch fp64 reference solver (oracle), world == 1
@@ -60,6 +62,7 @@ def _resolve(backend: str, transport: str, world: int) -> tuple[str, str]:
     if transport == "auto":
         transport = {"hip": "rccl", "cpu": "native" if world == 1 else "torch", "torch": "none"}[backend]
     ok = {("hip", "rccl"), ("hip", "torch"), ("hip", "loopback"), ("hip", "rccl-self"), ("hip", "push"),
+          ("hip", "push-ipc"),
           ("cpu", "native"),
           ("cpu", "torch"),
           ("torch", "none")}
@@ -82,7 +85,7 @@ class Solver:
                  tiling2: dict | None = None, init2: bool = True, timers: bool = False, tb: bool = True,
                  tiling_tb: dict | None = None,
                  debug_sync: bool = False, poison_ghosts: bool = False, deep_min_planes: int | None = None,
-                 tb_min_planes: int | None = None):
+                 tb_min_planes: int | None = None, rccl: bool = True):
         import torch.distributed as dist
 
         if not spec.cfl_ok and not force:
@@ -116,7 +119,7 @@ class Solver:
                 opts.tb_min_planes = tb_min_planes
             self._impl = C.GpuGroup(spec.native(), opts, world, self.transport)
             self.dims = self._impl.dims().as_tuple()
-        elif self.backend == "hip" and self.transport == "rccl":
+        elif self.backend == "hip" and self.transport in ("rccl", "push-ipc"):
             from .parallel.rccl import make_comm
 
             opts = self._options(C, decomp, spec, overlap, graph, tiling, temporal, tiling2, init2, tb, tiling_tb)
@@ -125,10 +128,20 @@ class Solver:
                 opts.deep_min_planes = deep_min_planes
             if tb_min_planes is not None:
                 opts.tb_min_planes = tb_min_planes
-            if comm is None and world > 1:
+            opts.push = self.transport == "push-ipc"
+            # (push-ipc without RCCL — ranks sharing one GPU, which RCCL refuses: no communicator, so no end-of-solve
+            # collective; each rank's error log is its own)
+            opts.push_no_collective = opts.push and not rccl
+            if comm is None and world > 1 and (rccl or not opts.push):
                 comm = make_comm(rank, world, group)
             self.comm = comm
             self._impl = C.GpuSolver(spec.native(), opts, rank, world, comm)
+            if self._impl.push and world > 1:  # every rank's IPC handles, over torch.distributed (gloo)
+                import torch.distributed as tdist
+
+                handles = [None] * world
+                tdist.all_gather_object(handles, self._impl.push_handles(), group=group)
+                self._impl.connect_push(handles)
             self.dims = self._impl.dims.as_tuple()
         elif self.transport in ("torch",):
             from .parallel.dist_solver import TorchDistSolver

@@ -154,3 +154,44 @@ def test_push_fake_rank_runs(gpu, tmp_path):
                     "--json", js, "--quiet"], check=True, timeout=120)
     meta = json.loads(open(js).read())
     assert meta["transport"] == "push" and meta["mode"] == "deep-tb" and meta["finite"]
+
+
+_PUSH_WORKER = r"""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["ROOT"])
+from mpi_cuda_amd import ProblemSpec
+from mpi_cuda_amd.solver import Solver
+dist.init_process_group("gloo")
+spec = ProblemSpec(N=66, tau=1e-3, K=20)
+s = Solver(spec, backend="hip", transport="push-ipc", decomp="slab", device=0, graph=False, rccl=False)
+rs = [s.run() for _ in range(3)]
+torch.save({"err": [r.max_err for r in rs], "f": s.owned_field(0), "rank": dist.get_rank()},
+           os.environ["OUT"] + f".{dist.get_rank()}.pt")
+dist.destroy_process_group()
+"""
+
+
+def test_push_ipc_python_two_processes(gpu, tmp_path):
+    """Python Solver(transport="push-ipc") under torch.distributed.run: one GpuSolver per process with the push
+    transport, IPC handles all-gathered over gloo. Two processes on one GPU cannot hold an RCCL communicator, so each
+    rank's error log here is its own (push_no_collective); the owned fields must equal the single-GPU field."""
+    import sys
+
+    root = ROOT
+    script = tmp_path / "w.py"
+    script.write_text(_PUSH_WORKER)
+    env = dict(os.environ, ROOT=root, OUT=str(tmp_path / "res"), W3D_TIMEOUT_S="30", W3D_CU_SPLIT="auto")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(29500 + os.getpid() % 200), str(script)]
+    subprocess.run(cmd, env=env, check=True, timeout=240, capture_output=True, text=True)
+    spec = ProblemSpec(N=66, tau=1e-3, K=20)
+    ref = Solver(spec, backend="hip", device=0)
+    ref.run()
+    full = ref.global_field(0)
+    from mpi_cuda_amd.parallel.decomp import plan
+
+    for rank in range(2):
+        d = torch.load(str(tmp_path / f"res.{rank}.pt"), weights_only=True)
+        x0, x1, y0, y1, z0, z1 = plan(66, 2, rank, "slab").box
+        assert torch.equal(d["f"], full[x0:x1, y0:y1, z0:z1])
+        assert d["err"][0] == d["err"][2]  # repeated solves agree

@@ -49,6 +49,7 @@ struct Args {
   int temporal = 4;
   bool tb = true;
   int tb_threads = 0;
+  int tb_init_threads = 0;
   bool init2 = true;
   int fake_rank = -1, fake_world = 0;
   int group = 0;                       // --group P: all P ranks in this process on one GPU
@@ -112,7 +113,8 @@ constexpr Personality kPersonalities[] = {
                "  --no-tb            two-step register-queue passes instead of the LDS S-step kernel\n"
                "  --tb-min-planes M  slab ranks: LDS S-step passes with S-deep halos from M owned planes (default 16)\n"
                "  --deep-min-planes M  slab ranks without the LDS kernel: two-step passes from M planes (default 96)\n"
-               "  --tb-threads T     LDS S-step kernel workgroup size (768 or 1024)\n"
+               "  --tb-threads T     LDS S-step kernel workgroup size (768 or 1024; default 1024)\n"
+               "  --tb-init-threads T  ... of the analytic-start pass (768 or 1024; default 768)\n"
                "  --no-init2         start from u0,u1 + a first step instead of analytic u1,u2\n"
                "  --debug-sync       synchronize after every step (race triage)\n"
                "  --poison-ghosts    NaN-fill ghost layers before every exchange (missed-halo detector)\n"
@@ -182,6 +184,7 @@ Args parse(int argc, char** argv) {
     else if (s == "--temporal") a.temporal = std::stoi(next());
     else if (s == "--no-tb") a.tb = false;
     else if (s == "--tb-threads") a.tb_threads = std::stoi(next());
+    else if (s == "--tb-init-threads") a.tb_init_threads = std::stoi(next());
     else if (s == "--no-init2") a.init2 = false;
     else if (s == "--t2-rows") a.t2_rows = std::stoi(next());
     else if (s == "--deep-min-planes") a.deep_min = std::stoi(next());
@@ -572,6 +575,7 @@ SolverOptions options_from(const Args& a, bool fake) {
   o.temporal = a.temporal;
   o.tb = a.tb;
   if (a.tb_threads > 0) o.tiling_tb.threads = a.tb_threads;
+  if (a.tb_init_threads > 0) o.tiling_tb.init_threads = a.tb_init_threads;
   o.init2 = a.init2;
   o.fake_comm = fake;
   o.push = a.transport == "push";

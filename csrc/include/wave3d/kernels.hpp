@@ -78,6 +78,8 @@ void launch_leapfrog2(const Layout& l, const Coeffs& c, const double* prev, cons
 struct LeapfrogTbTiling {
   int stages = 4;         // 2, 3 or 4 steps per pass
   int threads = 1024;     // workgroup size (768 or 1024)
+  int init_threads = 768; // ... of the analytic-start pass (measured at 512³, S = 3: 768 → 932 µs, 1024 → 1027 µs;
+                          // the S = 4 passes go the other way: 768 → 1123 µs, 1024 → 1076 µs)
   bool xcd_remap = true;  // (stores are always non-temporal: measured faster at every S)
   bool xcd_blocks = false; // with xcd_remap: each XCD owns a square-ish tile block, not two-row strips (measured: no gain)
   int target_blocks = 256; // fewer (y,z) tiles than this: split x into chunks (one workgroup per CU at 1 WG/CU)

@@ -653,7 +653,8 @@ struct TbPlan {
 // takes the default (x: the compute box; y, z: the whole allocation, i.e. no restriction besides the global interior).
 inline TbPlan make_plan_tb(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, LBox real) {
   W3D_REQUIRE(t.stages >= 2 && t.stages <= 4, "leapfrog_tb: stages must be 2, 3 or 4");
-  W3D_REQUIRE(t.threads == 768 || t.threads == 1024, "leapfrog_tb: threads must be 768 or 1024");
+  W3D_REQUIRE((t.threads == 768 || t.threads == 1024) && (t.init_threads == 768 || t.init_threads == 1024),
+              "leapfrog_tb: threads must be 768 or 1024");
   const LBox full = compute_box(l);
   if (real.x0 > real.x1) {
     real.x0 = full.x0;
@@ -818,7 +819,7 @@ template <int S, bool PUSH>
 void launch_s(const TbParams& p, int nblocks, const LeapfrogTbTiling& t, bool init, hipStream_t st) {
   // 768 threads: 12 waves (3 per SIMD, 168 VGPRs each) for the 38² = 1444 stage-1 positions of an S = 4 tile, two sets
   // per thread with 6 % idle slots; 1024: 16 waves (128 VGPRs), 30 % of the second set idle
-  if (t.threads == 768)
+  if ((init ? t.init_threads : t.threads) == 768)
     init ? launch_nt<S, 768, true, PUSH>(p, nblocks, st) : launch_nt<S, 768, false, PUSH>(p, nblocks, st);
   else
     init ? launch_nt<S, 1024, true, PUSH>(p, nblocks, st) : launch_nt<S, 1024, false, PUSH>(p, nblocks, st);

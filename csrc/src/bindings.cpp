@@ -381,6 +381,7 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init<>())
       .def_readwrite("stages", &LeapfrogTbTiling::stages)
       .def_readwrite("threads", &LeapfrogTbTiling::threads)
+      .def_readwrite("init_threads", &LeapfrogTbTiling::init_threads)
       .def_readwrite("xcd_remap", &LeapfrogTbTiling::xcd_remap)
       .def_readwrite("xcd_blocks", &LeapfrogTbTiling::xcd_blocks)
       .def_readwrite("target_blocks", &LeapfrogTbTiling::target_blocks)

@@ -146,6 +146,26 @@ def test_bench_two_ranks_rehearsal(gpu, tmp_path):
     assert line["correct"] is True and line["final_max_err"] == pytest.approx(3.960129e-09, rel=1e-6)
 
 
+def test_bench_setup_failure_stops_every_rank(gpu, tmp_path):
+    """Fault injection on the GPU path: rank 1's native runtime fails right after setup. Its bench.py
+    process raises the abort flag, rank 0's process kills its own child (which would otherwise wait for rank 1's flags
+    or files), both agree on the failure over gloo, and the job exits non-zero quickly with no JSON line."""
+    import time
+
+    out = tmp_path / "b.jsonl"
+    env = dict(os.environ, W3D_TIMEOUT_S="60", W3D_BENCH_FAIL_SETUP_RANK="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(29300 + os.getpid() % 200), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--share-gpus", "--no-rccl", "--native-transport", "push", "--steps", "3", "--warmup", "2",
+           "--out", str(out)]
+    t0 = time.perf_counter()
+    p = subprocess.run(cmd, timeout=240, env=env, capture_output=True, text=True)
+    assert p.returncode != 0
+    assert "injected fault" in p.stderr
+    assert not out.exists() or not out.read_text().strip()
+    assert time.perf_counter() - t0 < 120
+
+
 def test_push_fake_rank_runs(gpu, tmp_path):
     """Perf-study mode: one slab rank of 4 timed alone, forwarding into its own staging and waiting for its own
     signals (the cost of the push without peers)."""

@@ -800,10 +800,23 @@ int run_gpu(const Args& a) {
       // every schedule computes bit-identical fields: a candidate that fails (e.g. a push wait timed out) or whose
       // error log differs from the first accepted one's (a transport that delivered wrong ghosts) is rejected on
       // every rank, whatever its speed
+      // (collective when the candidate pushes: every rank built it). Agreed on its own: a rank whose IPC mapping
+      // failed must not reach the next agreement while its peers sit in the first solve's collectives
+      bool connected = false;
+      try {
+        connect(*cand);
+        connected = true;
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
+      if (!agree(connected)) {
+        std::fprintf(stderr, "[wave3d rank %d] candidate %s rejected: %s\n", rank, c.name,
+                     err.empty() ? "a peer could not connect" : err.c_str());
+        continue;
+      }
       bool same = false;
       RunResult r0;
       try {
-        connect(*cand);     // (collective when the candidate pushes: every rank built it)
         r0 = cand->run();   // eager: RCCL peer connections
         r0 = cand->run();   // graph capture
         // (a fake rank's log holds its own partials only: they differ between decompositions, nothing to compare)

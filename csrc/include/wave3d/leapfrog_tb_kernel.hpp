@@ -814,7 +814,7 @@ void launch_nt(const TbParams& p, int nblocks, hipStream_t st) {
     launch_cfg<S, NT, kFull<S>, INIT, PUSH>(p, nblocks, st);
 }
 
-// the analytic-start pass is built for 1024-thread workgroups only
+// workgroup size per pass kind: LeapfrogTbTiling::threads, or init_threads for the analytic-start pass
 template <int S, bool PUSH>
 void launch_s(const TbParams& p, int nblocks, const LeapfrogTbTiling& t, bool init, hipStream_t st) {
   // 768 threads: 12 waves (3 per SIMD, 168 VGPRs each) for the 38² = 1444 stage-1 positions of an S = 4 tile, two sets
@@ -839,8 +839,8 @@ void prepare_nt() {
 }
 
 
-// push transport instantiations (kernels_leapfrog_tb_push.hip): 1024-thread workgroups
-void launch_push(const TbParams& p, int nblocks, int stages, bool init, hipStream_t st);
+// push transport instantiations (kernels_leapfrog_tb_push.hip): 1024-thread workgroups (analytic start: init_threads)
+void launch_push(const TbParams& p, int nblocks, int stages, bool init, int init_threads, hipStream_t st);
 void prepare_push();
 
 }  // namespace tbk

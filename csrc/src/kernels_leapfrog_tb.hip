@@ -128,7 +128,7 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
     W3D_REQUIRE(push->done_target % static_cast<unsigned>(pl.nblocks) == 0,
                 "leapfrog_tb push: done_target must be a multiple of the grid");
   if (push != nullptr && push->on) {
-    launch_push(p, pl.nblocks, t.stages, analytic_start, stream);
+    launch_push(p, pl.nblocks, t.stages, analytic_start, t.init_threads, stream);
   } else {
     switch (t.stages) {
       case 2: launch_s<2, false>(p, pl.nblocks, t, analytic_start, stream); break;

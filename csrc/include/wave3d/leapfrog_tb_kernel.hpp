@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <string>
 #include <type_traits>
 
@@ -279,13 +280,23 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     double* szw = syw + NYW;
     double* rowt = szw + NYW;  // per checked level, two plane-parity slots of NYW row factors s_x·s_y
     double* sxw = rowt + 2 * S * NYW;
-    if (p.check_mask || INIT) {
+    // push transport: the pass's eight staging pointers (TbPush fwd1, fwd2, gprev, gcur), copied into LDS once and
+    // re-read from there where used — an LDS read does not wait behind the march's outstanding prefetch loads, as a
+    // load from the table in device memory would (and kept in SGPRs for the whole pass they spill)
+    unsigned long long* pbk =
+        reinterpret_cast<unsigned long long*>(sxw + ((p.check_mask || INIT) ? tb_nx_table<S>(p.xlen) : 0));
+    if constexpr (PUSH) {
+      static_assert(offsetof(TbPush, gcur) == offsetof(TbPush, fwd1) + 6 * sizeof(void*), "TbPush pointer block");
+      if (tid < 8) pbk[tid] = reinterpret_cast<const volatile unsigned long long*>(&p.push->fwd1[0])[tid];
+    }
+    if (p.check_mask || INIT || PUSH) {
       auto sc = [&](int g) { return p.s[g < -1 ? -1 : g > N + 1 ? N + 1 : g]; };
-      for (int t = tid; t < NYW; t += NT) {
+      for (int t = tid; t < NYW && (p.check_mask || INIT); t += NT) {
         syw[t] = sc(p.gy0 + ty0 - S - 1 + t);
         szw[t] = sc(p.gz0 + tz0 - S - 1 + t);
       }
-      for (int i = tid; i < tb_nx_table<S>(wx1 - wx0); i += NT) sxw[i] = sc(p.gx0 + wx0 - S - 1 + i);
+      if (p.check_mask || INIT)
+        for (int i = tid; i < tb_nx_table<S>(wx1 - wx0); i += NT) sxw[i] = sc(p.gx0 + wx0 - S - 1 + i);
       __syncthreads();
     }
     // table indices of an LDS position li (u^n-region coordinates): y ↔ li / W0 + 1, z ↔ li % W0 + 1 (the pad's dummy
@@ -293,6 +304,15 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     auto ytab = [&](int li) { return imin(li / W0 + 1, W0); };
     auto ztab = [&](int li) { return li - (li / W0) * W0 + 1; };
     const int xtab0 = S + 1 - wx0;  // x ↔ sxw[x + xtab0]
+    // staging pointer i of the pass (0, 1: fwd1 lo/hi; 2, 3: fwd2; 4, 5: gprev; 6, 7: gcur), wave-uniform
+    auto push_ptr = [&](int i) -> gdouble* {
+      typedef __attribute__((address_space(3))) const volatile unsigned long long lds_u64;  // (a ds_read, not FLAT)
+      const unsigned long long v = ((lds_u64*)pbk)[i];
+      const unsigned lo = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(v));
+      const unsigned hi = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(v >> 32));
+      return reinterpret_cast<gdouble*>((static_cast<unsigned long long>(hi) << 32) | lo);
+    };
+    (void)push_ptr;
     // analytic u⁰ = φ and u¹ at plane x, LDS position li (INIT)
     auto phi_at = [&](int x, int li) {
       return (sxw[x + xtab0] * syw[ytab(li)]) * szw[ztab(li)];
@@ -329,11 +349,11 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     const int wbase_r = __builtin_amdgcn_readfirstlane(tid & ~63);
     // plane xs of a field: the ghost planes of a push-transport rank come from its staging (plane 0 = ghost plane −T
     // on the low side, nx on the high side)
-    auto plane_ptr = [&](const double* fld, const double* const* gh, int xs) -> const gdouble* {
+    auto plane_ptr = [&](const double* fld, int gi, int xs) -> const gdouble* {
       if constexpr (PUSH) {
         if (static_cast<unsigned>(xs) >= static_cast<unsigned>(p.pnx)) {  // a ghost plane (one scalar test)
-          const double* g = tb_ptr_at(gh + (xs < 0 ? 0 : 1));
-          if (g) return (const gdouble*)(g) + static_cast<i64>(xs < 0 ? xs + p.pT : xs - p.pnx) * P;
+          const gdouble* g = push_ptr(gi + (xs < 0 ? 0 : 1));
+          if (g) return g + static_cast<i64>(xs < 0 ? xs + p.pT : xs - p.pnx) * P;
         }
       }
       return (const gdouble*)(fld) + static_cast<i64>(xs + 1) * P;
@@ -349,7 +369,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
           if (wbase_r + r * NT < G::NR) Rg[r][rs] = u1_at(x, lrid[r], grof[r] & kLd);
       } else {
         const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;  // always an allocated plane
-        const gdouble* base = plane_ptr(p.cur, PUSH ? p.push->gcur : nullptr, xs);
+        const gdouble* base = plane_ptr(p.cur, 6, xs);
 #pragma unroll
         for (int q = 0; q < Q; ++q)
           if (wsm[q]) L[0][q][slot] = base[gof[q] & kOff];
@@ -365,7 +385,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
           if (wsm[q]) Lm[q][slot] = phi_at(x, lid[q]);
       } else {
         const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
-        const gdouble* base = plane_ptr(p.prev, PUSH ? p.push->gprev : nullptr, xs);
+        const gdouble* base = plane_ptr(p.prev, 4, xs);
 #pragma unroll
         for (int q = 0; q < Q; ++q)
           if (wsm[q]) Lm[q][slot] = base[gof[q] & kOff];
@@ -472,6 +492,17 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       // the check's (s_x·s_y) row factor of plane xp, tabulated one iteration ahead (row_tables), slot F & 1
       const double* rowk = rowt + ((k - 1) * 2 + ((D + k - 1) & 1)) * NYW;
       (void)xown;
+      // push transport: the face planes a neighbour reads as ghosts (u^{n+S}: T deep, u^{n+S−1}: T − 1 deep) also go
+      // straight into its staging; the plane's destination is found once per stage (scalar), not per position
+      gdouble* fwd = nullptr;
+      if constexpr (PUSH && k >= S - 1) {
+        const int d = k == S ? p.pT : p.pT - 1;
+        if (xp < d || xp >= p.pnx - d) {
+          const int side = xp < d ? 0 : 1;
+          fwd = push_ptr((k == S ? 2 : 0) + side);
+          if (fwd) fwd += static_cast<i64>(side ? xp - p.pnx + p.pT : xp) * P;
+        }
+      }
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         if (!((wsm[q] >> (k - 1)) & 1)) continue;  // wave-uniform
@@ -493,20 +524,8 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         if constexpr (k >= S - 1) {
           if (own && xreal) {
             __builtin_nontemporal_store(v, outp + (g & kOff));
-            // push transport: the face planes a neighbour reads as ghosts (u^{n+S}: T deep, u^{n+S−1}: T − 1 deep)
-            // also go straight into its staging
-            if constexpr (PUSH) {
-              const int d = k == S ? p.pT : p.pT - 1;
-              if (xp < d) {
-                gdouble* f = (gdouble*)tb_ptr_at((k == S ? p.push->fwd2 : p.push->fwd1) + 0);
-                if (f) __hip_atomic_store(f + static_cast<i64>(xp) * P + (g & kOff), v, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_SYSTEM);
-              } else if (xp >= p.pnx - d) {
-                gdouble* f = (gdouble*)tb_ptr_at((k == S ? p.push->fwd2 : p.push->fwd1) + 1);
-                if (f) __hip_atomic_store(f + static_cast<i64>(xp - p.pnx + p.pT) * P + (g & kOff), v, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_SYSTEM);
-              }
-            }
+            if constexpr (PUSH)
+              if (fwd) __hip_atomic_store(fwd + (g & kOff), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           }
         }
         if constexpr (kChk) {
@@ -781,7 +800,8 @@ size_t prepare_cfg() {
 
 template <int S, int NT, int CM, bool INIT, bool PUSH>
 void launch_cfg(const TbParams& p, int nblocks, hipStream_t st) {
-  const size_t shmem = tb_lds_bytes<S, kTile, NT, INIT>((p.check_mask || INIT) ? tb_nx_table<S>(p.xlen) : 0);
+  const size_t shmem = tb_lds_bytes<S, kTile, NT, INIT>((p.check_mask || INIT) ? tb_nx_table<S>(p.xlen) : 0) +
+                       (PUSH ? 8 * sizeof(unsigned long long) : 0);  // (the push block: staging pointers)
   if (p.nxc > 1) {
     const size_t lim = prepare_cfg<S, NT, CM, INIT, true, PUSH>();
     W3D_REQUIRE(shmem <= lim, "leapfrog_tb: too many planes for the LDS sin table");

@@ -15,13 +15,27 @@ namespace wave3d {
 // f64 operations per node and step in the hot kernels. The differences keep the reference's form
 // (u_{i+1} − 2u_i + u_{i−1}): the 512³ log stays identical to the reference's printed digits, which a neighbour-sum
 // form (Σ − 6c) does not (it moves the 7th digit of the L∞ lines).
+//
+// On the device each difference's first half is one v_fma_f64: 2c is exact (a power-of-two scale), so
+// fma(−2, c, xp) rounds the same exact value xp − 2c once, as xp − (2c) does — bit-identical to the host form, one
+// f64 operation per node and step fewer (no separate 2c; the leapfrog's 2c − old is fma(2, c, −old) likewise).
 W3D_HD double d2sum(double c, double xm, double xp, double ym, double yp, double zm, double zp) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (__builtin_fma(-2.0, c, xp) + xm) + (__builtin_fma(-2.0, c, yp) + ym) + (__builtin_fma(-2.0, c, zp) + zm);
+#else
   const double c2 = 2.0 * c;
   return (xp - c2 + xm) + (yp - c2 + ym) + (zp - c2 + zm);
+#endif
 }
 
 // Leapfrog update u^{n+1} = 2u^n − u^{n−1} + τ² Δ_h u^n (report.pdf p.5 §2.2(3)), with s = d2sum and lam = τ²/h².
-W3D_HD double leapfrog(double c, double old, double s, double lam) { return (2.0 * c - old) + lam * s; }
+W3D_HD double leapfrog(double c, double old, double s, double lam) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_fma(2.0, c, -old) + lam * s;
+#else
+  return (2.0 * c - old) + lam * s;
+#endif
+}
 
 // Second-order first step u^1 = u^0 + τ²/2 Δ_h u^0, using ∂u/∂t = 0 (report.pdf p.5 §2.2(2)); half_lam = τ²/(2h²).
 W3D_HD double first_step(double c, double s, double half_lam) { return c + half_lam * s; }

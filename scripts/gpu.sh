@@ -10,6 +10,7 @@
 #   scripts/gpu.sh cli [wave3d args]         the reference-config CLI run (512 0.001 20 1)   -> gpurun_out/cli.log
 #   scripts/gpu.sh fakerank                  per-rank solve times (--fake-rank) of the slab schedules: RCCL overlap /
 #                                            sequential, push overlap / sequential, 512^3 ranks 1/8 + 1/2, 2048^3 3/8
+#   scripts/gpu.sh ab [wave3d args]          same-box A/B: build/ab/wave3d_base vs bin/wave3d -> gpurun_out/ab.log
 #   scripts/gpu.sh all                       test && cli && bench && profbench
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -69,7 +70,20 @@ run_fakerank() {
   done
 }
 
+# same-box A/B of the reference-config CLI: build/ab/wave3d_base (a copy of an earlier build) against bin/wave3d,
+# interleaved rounds of best-of-20 solves
+run_ab() {
+  local r b
+  for r in 1 2 3; do
+    for b in build/ab/wave3d_base bin/wave3d; do
+      echo "== round $r $b"
+      timeout -k 5 120 "$b" 512 0.001 20 1 --repeat 20 --warmup 2 --quiet "$@" | grep -i "time" || return 1
+    done
+  done
+}
+
 case "$what" in
+  ab) run_ab "$@" > gpurun_out/ab.log 2>&1; rc=$?; cat gpurun_out/ab.log; exit $rc ;;
   test) run_test "$@" ;;
   bench) run_bench "$@" ;;
   cli) run_cli "$@" ;;

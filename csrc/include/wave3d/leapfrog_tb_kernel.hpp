@@ -505,7 +505,11 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       }
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
-        if (!((wsm[q] >> (k - 1)) & 1)) continue;  // wave-uniform
+        // wave-uniform: the mask stays an integer in an SGPR (bit test + scalar branch); hoisted out of the march as a
+        // boolean it became a lane mask whose negation the compiler re-formed with two VALU ops per use
+        int wm = wsm[q];
+        asm volatile("" : "+s"(wm));
+        if (!((wm >> (k - 1)) & 1)) continue;
         const int li = lid[q];
         const double c = L[k - 1][q][s0];
         const double lap = d2sum(c, L[k - 1][q][sm], L[k - 1][q][sp], nb[li - W0], nb[li + W0], nb[li - 1], nb[li + 1]);
@@ -596,8 +600,9 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     // the vector unit. Blocks of 4 iterations keep the register-queue slots static.
     using Gen = std::false_type;
     using Bulk = std::true_type;
-    if constexpr (INIT) {
-      // the analytic-start pass runs general blocks only: its register footprint leaves no room for a second copy
+    if constexpr (INIT && NT > 768) {
+      // the 1024-thread analytic-start pass runs general blocks only: its register footprint (128 VGPRs) leaves no
+      // room for a second copy (768 threads: 168 VGPRs, bulk blocks as below)
       for (int ib = i0; ib <= i1; ib += 4) {
         iteration(std::integral_constant<int, 0>{}, Gen{}, ib);
         if (ib + 1 > i1) break;

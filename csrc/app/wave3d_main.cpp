@@ -130,7 +130,7 @@ constexpr Personality kPersonalities[] = {
                "  --t2-rows R / --t2-target W   fused two-step kernel: rows per wave, x-chunking target (waves)\n"
                "  --repeat R / --warmup W   timed / untimed solves (report min and mean)\n"
                "  --bench-steps K    then K back-to-back solves between two sync+barriers (max over ranks)\n"
-               "  --autotune         time the multi-rank schedule candidates (slab S4/S4-seq/S3/S2/S1, block S4/S3/S1)\n"
+               "  --autotune         time the multi-rank schedule candidates (slab S4/S4-seq/S4-push/S3/S2/S1, block S4/S4-seq/S3/S1)\n"
                "                     and\n"
                "                     keep the fastest (slowest rank decides)\n"
                "  --phases           per-phase device times (init/compute/exchange/check) of the timed schedule\n"
@@ -654,7 +654,8 @@ constexpr Candidate kCandidates[] = {
     {"slab-S4-push", "slab", 4, true, true}, {"slab-S4-push-seq", "slab", 4, false, true},
     {"slab-S3", "slab", 3, true},          {"slab-S2", "slab", 2, true},
     {"slab-S1", "slab", 1, true},          {"block-S4", "block", 4, true},
-    {"block-S3", "block", 3, true},        {"block-S1", "block", 1, true},
+    {"block-S4-seq", "block", 4, false},   {"block-S3", "block", 3, true},
+    {"block-S1", "block", 1, true},
 };
 
 // Every rank's bytes through files next to the rendezvous file (ranks without a communicator: --no-rccl). Each rank
@@ -946,7 +947,7 @@ int run_gpu(const Args& a) {
     if (a.timers || a.phases)
       std::printf(
           "Phases (%s, device ms, max over ranks): init %.3f | compute %.3f (shell %.3f) | exchange %.3f | check %.3f"
-          " | gather+sync (host) %.3f\n",
+          " | error-log gather (all-gather + D2H) %.3f\n",
           a.timers ? "this run" : "traced solve of the timed schedule", pp.init_ms, pp.interior_ms + pp.shell_ms,
           pp.shell_ms, pp.comm_ms, pp.check_ms, pp.gather_ms);
     if (!a.json.empty()) {
@@ -968,7 +969,7 @@ int run_gpu(const Args& a) {
       if (a.timers || a.phases)
         j << ", \"phases_ms\": {\"init\": " << jnum(pp.init_ms) << ", \"compute\": "
           << jnum(pp.interior_ms + pp.shell_ms) << ", \"shell\": " << jnum(pp.shell_ms) << ", \"exchange\": "
-          << jnum(pp.comm_ms) << ", \"check\": " << jnum(pp.check_ms) << ", \"gather_host\": " << jnum(pp.gather_ms)
+          << jnum(pp.comm_ms) << ", \"check\": " << jnum(pp.check_ms) << ", \"gather\": " << jnum(pp.gather_ms)
           << "}";
       j << ", \"steps\": [";
       for (size_t i = 0; i < r.steps.size(); ++i)

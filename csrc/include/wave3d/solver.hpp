@@ -272,7 +272,7 @@ class GpuSolver {
   int runs_ = 0;  // completed run() calls (RCCL ranks capture the graph only after one eager solve)
   int final_buf_ = 0;            // buffer index holding u^K after a solve
   // per-phase timers
-  enum { kPhaseInit = 0, kPhaseShell, kPhaseCompute, kPhaseComm, kPhaseCheck, kNumPhases };
+  enum { kPhaseInit = 0, kPhaseShell, kPhaseCompute, kPhaseComm, kPhaseCheck, kPhaseGather, kNumPhases };
   struct Mark {
     int phase, unit;  // unit −1: init
     hipEvent_t b, e;

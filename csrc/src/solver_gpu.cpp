@@ -548,7 +548,7 @@ void GpuSolver::timed(int phase, hipStream_t st, F&& f) {
     f();
     return;
   }
-  static const char* const kNames[kNumPhases] = {"init", "shell", "compute", "exchange", "check"};
+  static const char* const kNames[kNumPhases] = {"init", "shell", "compute", "exchange", "check", "gather"};
   char label[48];
   std::snprintf(label, sizeof label, "w3d:%s:u%d", kNames[phase], cur_unit_);
   roctxRangePushA(label);
@@ -883,7 +883,7 @@ void GpuSolver::poison(hipStream_t st) {
 
 void GpuSolver::collect_phases(RunResult& r) {
   if (!opt_.timers) return;
-  double acc[kNumPhases] = {0, 0, 0, 0, 0};
+  double acc[kNumPhases] = {};
   r.trace.assign(units_.size(), UnitTrace{});
   for (size_t i = 0; i < units_.size(); ++i) {
     r.trace[i].unit = static_cast<int>(i);
@@ -904,6 +904,7 @@ void GpuSolver::collect_phases(RunResult& r) {
   r.phases.interior_ms = acc[kPhaseCompute];
   r.phases.comm_ms = acc[kPhaseComm];
   r.phases.check_ms = acc[kPhaseCheck];
+  r.phases.gather_ms = acc[kPhaseGather];  // device: the error log's all-gather and D2H copy after the last pass
 }
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -949,13 +950,16 @@ void GpuSolver::gather_errors(RunResult& r) {
   const int K = prob_.K;
   const size_t per = static_cast<size_t>(K + 1);
   std::vector<Partial> host(per * static_cast<size_t>(world_));
-  if (world_ > 1 && comm_) {
-    W3D_NCCL(ncclAllGather(errlog_, errall_, 2 * per, ncclFloat64, static_cast<ncclComm_t>(comm_->raw()), s0_));
-    W3D_HIP(hipMemcpyAsync(host.data(), errall_, host.size() * sizeof(Partial), hipMemcpyDeviceToHost, s0_));
-  } else {
-    host.resize(per);
-    W3D_HIP(hipMemcpyAsync(host.data(), errlog_, per * sizeof(Partial), hipMemcpyDeviceToHost, s0_));
-  }
+  cur_unit_ = -1;
+  timed(kPhaseGather, s0_, [&] {
+    if (world_ > 1 && comm_) {
+      W3D_NCCL(ncclAllGather(errlog_, errall_, 2 * per, ncclFloat64, static_cast<ncclComm_t>(comm_->raw()), s0_));
+      W3D_HIP(hipMemcpyAsync(host.data(), errall_, host.size() * sizeof(Partial), hipMemcpyDeviceToHost, s0_));
+    } else {
+      host.resize(per);
+      W3D_HIP(hipMemcpyAsync(host.data(), errlog_, per * sizeof(Partial), hipMemcpyDeviceToHost, s0_));
+    }
+  });
   wait_stream(s0_, comm_.get(), gpu_timeout_s());
   push_check();
   const int nsrc = static_cast<int>(host.size() / per);
@@ -1007,11 +1011,9 @@ RunResult GpuSolver::run() {
     W3D_HIP(hipGraphLaunch(graph_exec_, s0_));
   else
     enqueue_solve();
-  const double tg = now_s();
   gather_errors(r);
   r.solve_s = now_s() - t0;
   collect_phases(r);
-  r.phases.gather_ms = (now_s() - tg) * 1e3;  // host: waits for the device, then all-gathers the error log
   ++runs_;
   return r;
 }

@@ -58,7 +58,7 @@ def test_scaling_report_reads_driver_scale_record(tmp_path):
         return {"metric": "gcell_updates_per_s_512cube_K20", "n_gpus": n, "ms_per_step": ms,
                 "value": 512 ** 3 * 20 / (ms / 1e3) / 1e9, "config": {"schedule": "slab-S4" if n > 1 else "fused"},
                 "phases_ms": {"compute": ms * 0.9, "shell": 0.1 if n > 1 else 0, "exchange": 0.05 * (n > 1),
-                              "check": 0.02, "gather_host": ms}}
+                              "check": 0.02, "gather": 0.01}}
     rec = {"runs": {str(n): {"parsed": line(n, ms), "run": {"stdout": "...", "parsed": line(n, ms)}}
                     for n, ms in ((1, 4.97), (2, 2.6), (4, 1.4), (8, 0.9))}}
     p = tmp_path / "SCALE_r02.json"

@@ -99,13 +99,13 @@ def print_tables(rows):
         if ph:  # the reference's per-GPU-count time breakdown (report.pdf p.16 §4.4: compute / copies / MPI)
             print("\nPhase breakdown (device ms per solve, max over ranks, traced solve of the timed schedule; exchange "
                   "overlaps compute when the schedule overlaps):\n")
-            print("| GPUs | schedule | compute | of which shells | exchange | error check | host gather+sync |")
+            print("| GPUs | schedule | compute | of which shells | exchange | error check | error-log gather |")
             print("|---|---|---|---|---|---|---|")
             for r in ph:
                 p = r["phases_ms"]
                 print(f"| {r['n_gpus']} | {r.get('config', {}).get('schedule', '')} | {p.get('compute', 0):.3f} | "
                       f"{p.get('shell', 0):.3f} | {p.get('exchange', 0):.3f} | {p.get('check', 0):.3f} | "
-                      f"{p.get('gather_host', 0):.3f} |")
+                      f"{p.get('gather', p.get('gather_host', 0)):.3f} |")
         return
     for (mode, N), rs in cpu_groups(rows).items():
         print(f"\n{mode}, {N}^3:\n\n| workers | time s | speedup | efficiency | GCell/s |")

@@ -9,7 +9,8 @@
 #   scripts/gpu.sh pmc "<counters>" [wave3d args]  one PMC pass (counters of one block budget) -> gpurun_out/pmc/
 #   scripts/gpu.sh cli [wave3d args]         the reference-config CLI run (512 0.001 20 1)   -> gpurun_out/cli.log
 #   scripts/gpu.sh fakerank                  per-rank solve times (--fake-rank) of the slab schedules: RCCL overlap /
-#                                            sequential, push overlap / sequential, 512^3 ranks 1/8 + 1/2, 2048^3 3/8
+#                                            sequential, push overlap / sequential, 512^3 ranks 1/8 + 1/2, 2048^3 3/8;
+#                                            2x2x2 blocks (overlap / sequential) at 512^3 and 2048^3, rank 3/8
 #   scripts/gpu.sh ab [wave3d args]          same-box A/B: build/ab/wave3d_base vs bin/wave3d -> gpurun_out/ab.log
 #   scripts/gpu.sh all                       test && cli && bench && profbench
 set -o pipefail
@@ -65,6 +66,14 @@ run_fakerank() {
     for v in "" "--no-overlap" "--transport push" "--transport push --no-overlap"; do
       echo "== N=$N fake $r $v"
       timeout -k 5 120 ./bin/wave3d "$N" "$tau" 20 1 --fake-rank "$r" --repeat 5 --warmup 2 --quiet $v \
+        | grep "Total time" || return 1
+    done
+  done
+  for fr in 512:0.001:3/8 2048:0.00025:3/8; do  # 3-D blocks 2x2x2: overlap / sequential
+    IFS=: read -r N tau r <<< "$fr"
+    for v in "" "--no-overlap"; do
+      echo "== N=$N fake $r --decomp 2x2x2 $v"
+      timeout -k 5 120 ./bin/wave3d "$N" "$tau" 20 1 --fake-rank "$r" --decomp 2x2x2 --repeat 5 --warmup 2 --quiet $v \
         | grep "Total time" || return 1
     done
   done

@@ -11,6 +11,7 @@
 #   scripts/gpu.sh fakerank                  per-rank solve times (--fake-rank) of the slab schedules: RCCL overlap /
 #                                            sequential, push overlap / sequential, 512^3 ranks 1/8 + 1/2, 2048^3 3/8;
 #                                            2x2x2 blocks (overlap / sequential) at 512^3 and 2048^3, rank 3/8
+#   scripts/gpu.sh fakesweep                 512^3 compute-only scaling projection (one rank of P, P = 1/2/4/8)
 #   scripts/gpu.sh ab [wave3d args]          same-box A/B: build/ab/wave3d_base vs bin/wave3d -> gpurun_out/ab.log
 #   scripts/gpu.sh all                       test && cli && bench && profbench
 set -o pipefail
@@ -91,7 +92,28 @@ run_ab() {
   done
 }
 
+# compute-only strong-scaling projection of the 512^3 solve: one rank of P timed alone (--fake-rank, no transport
+# traffic) for the sequential slab and block schedules; one JSON line per point -> gpurun_out/fakesweep.jsonl
+run_fakesweep() {
+  local P dec r j out=gpurun_out/fakesweep.jsonl
+  : > "$out"
+  timeout -k 5 120 ./bin/wave3d 512 0.001 20 1 --repeat 10 --warmup 2 --quiet --json /tmp/fs.json > /dev/null || return 1
+  python3 -c "import json;d=json.load(open('/tmp/fs.json'));print(json.dumps({'P':1,'decomp':'1x1x1','rank':0,'solve_s':d['solve_s']}))" >> "$out" || return 1
+  for P in 2 4 8; do
+    for dec in slab block; do
+      [ "$dec" = block ] && [ "$P" -lt 4 ] && continue
+      for r in 0 1; do
+        timeout -k 5 120 ./bin/wave3d 512 0.001 20 1 --fake-rank "$r/$P" --decomp "$dec" --no-overlap --repeat 10 \
+          --warmup 2 --quiet --json /tmp/fs.json > /dev/null || return 1
+        python3 -c "import json,sys;d=json.load(open('/tmp/fs.json'));print(json.dumps({'P':$P,'decomp':'x'.join(map(str,d['dims'])),'schedule':'$dec-seq','rank':$r,'solve_s':d['solve_s']}))" >> "$out" || return 1
+      done
+    done
+  done
+  cat "$out"
+}
+
 case "$what" in
+  fakesweep) run_fakesweep ;;
   ab) run_ab "$@" > gpurun_out/ab.log 2>&1; rc=$?; cat gpurun_out/ab.log; exit $rc ;;
   test) run_test "$@" ;;
   bench) run_bench "$@" ;;

@@ -76,3 +76,26 @@ def test_scaling_report_reads_driver_scale_record(tmp_path):
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scaling_report.py"), str(p), "--plot", str(png)],
                    check=True, capture_output=True)
     assert png.stat().st_size > 1000
+
+
+def test_projection_figure(tmp_path, capsys):
+    """tools/projection_figure.py: per-P max over sampled ranks, fastest schedule per P, speedup/efficiency vs 1 GPU."""
+    lines = [{"P": 1, "rank": 0, "solve_s": 0.005},
+             {"P": 2, "schedule": "slab-seq", "rank": 0, "solve_s": 0.0026},
+             {"P": 2, "schedule": "slab-seq", "rank": 1, "solve_s": 0.0025},
+             {"P": 8, "schedule": "slab-seq", "rank": 1, "solve_s": 0.0008},
+             {"P": 8, "schedule": "block-seq", "rank": 0, "solve_s": 0.0009}]
+    src = tmp_path / "fs.jsonl"
+    src.write_text("\n".join(json.dumps(x) for x in lines) + "\n")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import projection_figure
+
+    rows = projection_figure.table(projection_figure.load(str(src)))
+    assert [r["P"] for r in rows] == [1, 2, 8]
+    assert rows[1]["t"] == 0.0026  # max over ranks
+    assert rows[2]["schedule"] == "slab-seq" and abs(rows[2]["speedup"] - 6.25) < 1e-9
+    assert abs(rows[2]["eff"] - 6.25 / 8) < 1e-9
+    fig = tmp_path / "p.png"
+    assert projection_figure.main([str(src), "--plot", str(fig)]) == 0
+    assert fig.stat().st_size > 1000
+    assert "compute only" in capsys.readouterr().out

@@ -349,8 +349,9 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     const int wbase_r = __builtin_amdgcn_readfirstlane(tid & ~63);
     // plane xs of a field: the ghost planes of a push-transport rank come from its staging (plane 0 = ghost plane −T
     // on the low side, nx on the high side)
-    auto plane_ptr = [&](const double* fld, int gi, int xs) -> const gdouble* {
-      if constexpr (PUSH) {
+    // (BK: a bulk plane, never a ghost plane — the push bulk range below keeps loads inside [0, pnx))
+    auto plane_ptr = [&](auto bkc, const double* fld, int gi, int xs) -> const gdouble* {
+      if constexpr (PUSH && !decltype(bkc)::value) {
         if (static_cast<unsigned>(xs) >= static_cast<unsigned>(p.pnx)) {  // a ghost plane (one scalar test)
           const gdouble* g = push_ptr(gi + (xs < 0 ? 0 : 1));
           if (g) return g + static_cast<i64>(xs < 0 ? xs + p.pT : xs - p.pnx) * P;
@@ -358,7 +359,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       }
       return (const gdouble*)(fld) + static_cast<i64>(xs + 1) * P;
     };
-    auto load_cur = [&](auto slot_c, auto rs_c, int x) {
+    auto load_cur = [&](auto slot_c, auto rs_c, int x, auto bkc) {
       constexpr int slot = decltype(slot_c)::value, rs = decltype(rs_c)::value;
       if constexpr (INIT) {
 #pragma unroll
@@ -369,7 +370,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
           if (wbase_r + r * NT < G::NR) Rg[r][rs] = u1_at(x, lrid[r], grof[r] & kLd);
       } else {
         const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;  // always an allocated plane
-        const gdouble* base = plane_ptr(p.cur, 6, xs);
+        const gdouble* base = plane_ptr(bkc, p.cur, 6, xs);
 #pragma unroll
         for (int q = 0; q < Q; ++q)
           if (wsm[q]) L[0][q][slot] = base[gof[q] & kOff];
@@ -377,7 +378,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         for (int r = 0; r < QR; ++r) Rg[r][rs] = base[grof[r] & kOff];
       }
     };
-    auto load_prev = [&](auto slot_c, int x) {
+    auto load_prev = [&](auto slot_c, int x, auto bkc) {
       constexpr int slot = decltype(slot_c)::value;
       if constexpr (INIT) {
 #pragma unroll
@@ -385,7 +386,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
           if (wsm[q]) Lm[q][slot] = phi_at(x, lid[q]);
       } else {
         const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
-        const gdouble* base = plane_ptr(p.prev, 4, xs);
+        const gdouble* base = plane_ptr(bkc, p.prev, 4, xs);
 #pragma unroll
         for (int q = 0; q < Q; ++q)
           if (wsm[q]) Lm[q][slot] = base[gof[q] & kOff];
@@ -495,7 +496,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       // push transport: the face planes a neighbour reads as ghosts (u^{n+S}: T deep, u^{n+S−1}: T − 1 deep) also go
       // straight into its staging; the plane's destination is found once per stage (scalar), not per position
       gdouble* fwd = nullptr;
-      if constexpr (PUSH && k >= S - 1) {
+      if constexpr (PUSH && !BK && k >= S - 1) {  // (bulk planes are never face planes: see the push bulk range)
         const int d = k == S ? p.pT : p.pT - 1;
         if (xp < d || xp >= p.pnx - d) {
           const int side = xp < d ? 0 : 1;
@@ -528,7 +529,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         if constexpr (k >= S - 1) {
           if (own && xreal) {
             __builtin_nontemporal_store(v, outp + (g & kOff));
-            if constexpr (PUSH)
+            if constexpr (PUSH && !BK)
               if (fwd) __hip_atomic_store(fwd + (g & kOff), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           }
         }
@@ -568,8 +569,8 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       if constexpr (INIT) {
         init_iter(fc, i);
       } else {
-        load_cur(std::integral_constant<int, (F + 2) & 3>{}, std::integral_constant<int, (F + 2) & 1>{}, i + 2);
-        load_prev(std::integral_constant<int, (F + 1) & 1>{}, i + 1);
+        load_cur(std::integral_constant<int, (F + 2) & 3>{}, std::integral_constant<int, (F + 2) & 1>{}, i + 2, bkc);
+        load_prev(std::integral_constant<int, (F + 1) & 1>{}, i + 1, bkc);
       }
 #define W3D_TB_STAGE(K)                                                                                          \
   if constexpr (K <= S) {                                                                                        \
@@ -585,11 +586,11 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     };
 
     // prologue: u^n planes i0−1, i0 (registers; plane i0 also to LDS), plane i0+1 and u^{n−1} plane i0 in flight
-    load_cur(std::integral_constant<int, 3>{}, std::integral_constant<int, 1>{}, i0 - 1);
-    load_cur(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, i0);
+    load_cur(std::integral_constant<int, 3>{}, std::integral_constant<int, 1>{}, i0 - 1, std::false_type{});
+    load_cur(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, i0, std::false_type{});
     commit_cur(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0);
-    load_cur(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, i0 + 1);
-    load_prev(std::integral_constant<int, 0>{}, i0);
+    load_cur(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, i0 + 1, std::false_type{});
+    load_prev(std::integral_constant<int, 0>{}, i0, std::false_type{});
     row_tables(i0, 0);
     if constexpr (INIT) {  // φ planes i0+1 (slot 1: read back as the x neighbour at i0) and i0+2 (slot 0)
       phi_plane(i0 + 1, 1);
@@ -614,8 +615,14 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       }
     } else {
       // head blocks (general) until the first block inside the bulk range, bulk blocks, then the general tail
-      const int blo = imax(imax(x0, p.sx0), 1 - p.gx0) + (S - 1);
-      const int bhi = imin(imin(x1, p.sx1), N - p.gx0);
+      int blo = imax(imax(x0, p.sx0), 1 - p.gx0) + (S - 1);
+      int bhi = imin(imin(x1, p.sx1), N - p.gx0);
+      if constexpr (PUSH) {
+        // push: bulk blocks neither forward face planes (stage S−1 / S plane xp with xp < T or xp ≥ pnx − T) nor load
+        // ghost planes (u^n plane i+2 ≥ pnx), so their push tests compile away; those iterations run general blocks
+        blo = imax(blo, p.pT + S - 1);
+        bhi = imin(bhi, imin(p.pnx - p.pT + S - 2, p.pnx - 2));
+      }
       int ib = i0;
       const int nhead = blo > i0 ? (blo - i0 + 3) / 4 : 0;
       for (int b = 0; b < nhead && ib + 3 <= i1; ++b, ib += 4) {

@@ -82,12 +82,15 @@ run_fakerank() {
 
 # same-box A/B of the reference-config CLI: build/ab/wave3d_base (a copy of an earlier build) against bin/wave3d,
 # interleaved rounds of best-of-20 solves
+# (W3D_AB_NEW_ARGS: extra arguments for bin/wave3d only, e.g. a new option the base build does not know)
 run_ab() {
-  local r b
+  local r b extra
   for r in 1 2 3; do
     for b in build/ab/wave3d_base bin/wave3d; do
-      echo "== round $r $b"
-      timeout -k 5 120 "$b" 512 0.001 20 1 --repeat 20 --warmup 2 --quiet "$@" | grep -i "time" || return 1
+      extra=""
+      [ "$b" = bin/wave3d ] && extra="${W3D_AB_NEW_ARGS:-}"
+      echo "== round $r $b $extra"
+      timeout -k 5 120 "$b" 512 0.001 20 1 --repeat 20 --warmup 2 --quiet $extra "$@" | grep -i "time" || return 1
     done
   done
 }

@@ -75,10 +75,11 @@ def _args(argv=None):
     ap.add_argument("--share-gpus", action="store_true",
                     help="rehearsal: allow more ranks than visible GPUs (ranks share GPUs; RCCL refuses this, so use it "
                          "with --no-rccl --native-transport push; each rank then gets its own share of the CUs)")
-    ap.add_argument("--native-transport", default="rccl", choices=["rccl", "push"],
-                    help="halo transport of the native runtime with --no-autotune (push: slab passes forward their faces)")
+    ap.add_argument("--native-transport", default="rccl", choices=["rccl", "push", "sdma"],
+                    help="halo transport of the native runtime with --no-autotune (push: slab passes forward their "
+                         "faces; sdma: copy engines move the halos into the peers' memory)")
     ap.add_argument("--no-rccl", action="store_true",
-                    help="native ranks without an RCCL communicator (push only; host collectives through files)")
+                    help="native ranks without an RCCL communicator (push / sdma only; host collectives through files)")
     ap.add_argument("--timeout", type=float, default=900.0, help="seconds before a native rank is killed")
     ap.add_argument("--out", default="", help="also append the JSON line to this file")
     return ap.parse_args(argv)
@@ -117,9 +118,28 @@ def _emit(a, line) -> None:
             f.write(s + "\n")
 
 
-def _correct(a, finite, final_linf) -> bool:
+def _correct(a, finite, steps) -> tuple[bool, str]:
+    """Every config is checked against the closed-form oracle of the discrete scheme (SURVEY.md §1.6,
+    models/wave3d.py oracle_errors): each checked step's L∞ and RMS within 1e-5 relative plus a rounding allowance of
+    4e-16 per step (≈ 2 ulp of the O(1) field per step: at 2048³, τ = 2.5e-4 the error itself is 1.6e-13 at step 2 and
+    the measured log sits 3e-16 from the oracle there, 1e-15 at step 20). The reference config must also reproduce
+    the reference's printed step-20 L∞ (report.pdf p.16 §4.3.1)."""
+    from mpi_cuda_amd import ProblemSpec
+    from mpi_cuda_amd.models.wave3d import oracle_errors
+
+    if not finite or not steps:
+        return False, "non-finite or empty error log"
+    spec = ProblemSpec(N=a.N, tau=a.tau, K=a.K, L=a.L, check_every=2)
+    ref = oracle_errors(spec, steps=[int(n) for n, _, _ in steps])
+    for n, m, e in steps:
+        om, oe = ref[int(n)]
+        tol = 4e-16 * int(n)
+        if abs(m - om) > 1e-5 * om + tol or abs(e - oe) > 1e-5 * oe + tol:
+            return False, f"step {n}: L-inf {m:.6e} / RMS {e:.6e} vs oracle {om:.6e} / {oe:.6e}"
     ref_cfg = a.N == 512 and a.K == 20 and a.tau == 1e-3 and a.L == 1.0
-    return bool(finite and (not ref_cfg or abs(final_linf / REF_FINAL_LINF - 1) < 1e-5))
+    if ref_cfg and abs(steps[-1][1] / REF_FINAL_LINF - 1) >= 1e-5:
+        return False, f"final L-inf {steps[-1][1]:.6e} is not the reference's {REF_FINAL_LINF:.6e}"
+    return True, f"{len(steps)} checked steps match the closed-form oracle"
 
 
 # ------------------------------------------------------------------------------------------------------------------
@@ -150,8 +170,8 @@ def run_native(a, rank: int, world: int, local: int) -> int:
     if a.cpu:
         cmd.append("--cpu")
     else:
-        if a.native_transport == "push":
-            cmd += ["--transport", "push"]
+        if a.native_transport != "rccl":
+            cmd += ["--transport", a.native_transport]
         if a.no_rccl:
             cmd.append("--no-rccl")
         if (multi or a.autotune) and not a.no_autotune and not a.no_rccl:
@@ -166,7 +186,7 @@ def run_native(a, rank: int, world: int, local: int) -> int:
                W3D_JOB_ID=f"bench{nonce}", W3D_TIMEOUT_S=os.environ.get("W3D_TIMEOUT_S", "180"))
     if a.share_gpus:
         env["W3D_SHARE_GPUS"] = "1"
-        if multi and _distinct_gpus(world) < world:
+        if multi and _distinct_gpus(world) < world and a.native_transport == "push":
             env["W3D_CU_SPLIT"] = "auto"  # concurrent ranks on one GPU: disjoint CU ranges (in-kernel push waits)
     fail_rank = os.environ.get("W3D_BENCH_FAIL_SETUP_RANK")  # fault injection (tests)
     if fail_rank is not None:
@@ -225,7 +245,7 @@ def run_native(a, rank: int, world: int, local: int) -> int:
         steps = res.get("steps") or []
         final_linf = steps[-1][1] if steps else float("nan")
         final_rms = steps[-1][2] if steps else None
-        correct = _correct(a, res.get("finite", False), final_linf)
+        correct, why_correct = _correct(a, res.get("finite", False), steps)
         dims = res.get("dims", [1, 1, 1])
         sched = res.get("schedule", "")
         par = (f"{sched.split('-')[0]}{world}" if multi else "single") if not a.cpu else f"cpu-ranks{world}"
@@ -246,6 +266,7 @@ def run_native(a, rank: int, world: int, local: int) -> int:
             "final_max_err": final_linf,
             "final_rms_err": final_rms,
             "correct": correct,
+            "correct_check": why_correct,
             "degraded": False,
             "rccl_nranks": res.get("rccl_nranks") if not a.cpu else None,
             "rccl_version": res.get("rccl_version"),
@@ -344,7 +365,7 @@ def run_python(a, rank: int, world: int, local: int, degraded: str = "") -> int:
     ms = float(t[0]) / a.steps * 1e3
     value = spec.cell_updates / (ms / 1e3) / 1e9
     final_linf = r.max_err[-1] if r.max_err else float("nan")
-    correct = _correct(a, r.finite, final_linf)
+    correct, why_correct = _correct(a, r.finite, [[n, m, e] for n, m, e in zip(r.steps, r.max_err, r.rms_err)])
     if rank == 0:
         py_loop = transport == "torch"
         dims = "x".join(str(d) for d in solver.dims)
@@ -357,7 +378,7 @@ def run_python(a, rank: int, world: int, local: int, degraded: str = "") -> int:
                "autotune_ms": None}
         extra = {"wall_clock_s": round(ms / 1e3, 6), "baseline_wall_clock_s": {1: 0.752, 2: 0.505}.get(world),
                  "final_max_err": final_linf, "final_rms_err": r.rms_err[-1] if r.rms_err else None,
-                 "correct": correct, "degraded": bool(degraded)}
+                 "correct": correct, "correct_check": why_correct, "degraded": bool(degraded)}
         if degraded:
             extra["degraded_reason"] = degraded
         _emit(a, _line(a, world, value, ms, cfg, extra))

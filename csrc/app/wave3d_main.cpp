@@ -396,6 +396,13 @@ int load_dump_global(const std::string& prefix, const Problem& p, std::vector<do
                               nn = json_numbers(m, "N");
     W3D_REQUIRE(sh.size() == 3 && of.size() == 3 && st.size() == 1 && nn.size() == 1, "resume: bad sidecar " + b);
     W3D_REQUIRE(static_cast<i64>(nn[0]) == p.N, "resume: dump N differs from the run's N");
+    // (tau and L too: a checkpoint of another problem would continue from an inconsistent state; the sidecar holds
+    // them with 17 significant digits, so they round-trip exactly)
+    for (const auto& [key, want] : {std::pair<const char*, double>{"tau", p.tau}, {"L", p.L}}) {
+      const std::vector<double> v = json_numbers(m, key);
+      W3D_REQUIRE(v.size() == 1 && std::fabs(v[0] - want) <= 1e-15 * std::fabs(want),
+                  std::string("resume: dump ") + key + " differs from the run's " + key);
+    }
     W3D_REQUIRE(step < 0 || step == static_cast<int>(st[0]), "resume: rank dumps of different steps");
     step = static_cast<int>(st[0]);
     const i64 nx = static_cast<i64>(sh[0]), ny = static_cast<i64>(sh[1]), nz = static_cast<i64>(sh[2]);
@@ -578,7 +585,10 @@ SolverOptions options_from(const Args& a, bool fake) {
   if (a.tb_init_threads > 0) o.tiling_tb.init_threads = a.tb_init_threads;
   o.init2 = a.init2;
   o.fake_comm = fake;
+  W3D_REQUIRE(a.transport == "rccl" || a.transport == "push" || a.transport == "sdma",
+              "--transport must be rccl, push or sdma, not " + a.transport);
   o.push = a.transport == "push";
+  o.sdma = a.transport == "sdma";
   o.push_cp_wait = a.push_cp_wait;
   o.push_no_collective = a.no_rccl;  // (no end-of-solve collective: the flag epochs run on, eager launches)
   if (a.t2_rows > 0) o.tiling2.rows = a.t2_rows;
@@ -760,11 +770,19 @@ int run_gpu(const Args& a) {
       (void)fgather("b");
   };
 
-  W3D_REQUIRE(!a.no_rccl || world == 1 || fake || (a.transport == "push" && !a.autotune),
-              "--no-rccl: ranks without a communicator can only run the push transport (no autotune)");
+  W3D_REQUIRE(!a.no_rccl || world == 1 || fake || ((a.transport == "push" || a.transport == "sdma") && !a.autotune),
+              "--no-rccl: ranks without a communicator can only run the push or sdma transport (no autotune)");
   // push transport: connect the slab neighbours (IPC handles through RCCL, or files without a communicator; a fake
   // rank forwards into its own staging and waits for its own signals: the cost of the push without peers)
   auto connect = [&](GpuSolver& g) {
+    if (g.sdma()) {
+      if (fake)
+        g.connect_sdma_self();
+      else
+        g.connect_sdma(comm ? comm_allgather_bytes(*comm, g.sdma_handles())
+                            : file_allgather(rank, world, g.sdma_handles(), "sdma"));
+      return;
+    }
     if (!g.push()) return;
     if (fake)
       g.connect_push_self();
@@ -774,7 +792,7 @@ int run_gpu(const Args& a) {
   };
   std::unique_ptr<GpuSolver> s;
   std::string sched = a.decomp + "-S" + std::to_string(a.temporal) + (a.overlap ? "" : "-seq") +
-                      (a.transport == "push" ? "-push" : "");
+                      (a.transport == "rccl" ? "" : "-" + a.transport);
   std::vector<std::pair<std::string, double>> tuned;
   if (a.autotune && (world > 1 || a.fake_rank < 0)) {
     double best_t = 1e30;
@@ -939,7 +957,7 @@ int run_gpu(const Args& a) {
         "Throughput: %.2f GCell/s; process wall-clock %.3f s (RCCL init %.3f s, %d ranks); schedule %s (%s), graph %s,"
         " overlap %s\n",
         gcell, t_proc, t_comm, rccl_nranks, s->mode().c_str(), sched.c_str(), s->options().graph ? "on" : "off",
-        s->options().overlap ? "on" : "off");
+        s->overlapped() ? "on" : "off");
     if (a.bench_steps > 0)
       std::printf("Bench: %d solves in %.6f s (%.6f s per solve, max over ranks)\n", a.bench_steps, bench_s,
                   bench_s / a.bench_steps);
@@ -959,9 +977,10 @@ int run_gpu(const Args& a) {
         << jnum(t_comm) << ", \"rccl_nranks\": " << rccl_nranks << ", \"rccl_version\": " << rccl_version()
         << ", \"hip_runtime\": " << hipv << ", \"gcell_per_s\": " << jnum(gcell)
         << ", \"graph\": " << (s->options().graph ? "true" : "false") << ", \"overlap\": "
-        << (s->options().overlap ? "true" : "false") << ", \"temporal\": " << s->options().temporal
+        << (s->overlapped() ? "true" : "false") << ", \"overlap_requested\": " << (s->options().overlap ? "true" : "false")
+        << ", \"temporal\": " << s->options().temporal
         << ", \"schedule\": " << jstr(sched) << ", \"mode\": " << jstr(s->mode())
-        << ", \"transport\": " << jstr(s->push() ? "push" : world > 1 ? "rccl" : "none") << ", \"device\": "
+        << ", \"transport\": " << jstr(s->transport()) << ", \"device\": "
         << jstr(prop.gcnArchName) << ", \"bench_steps\": " << a.bench_steps << ", \"bench_s\": " << jnum(bench_s)
         << ", \"warmup\": " << a.warmup << ", \"finite\": " << (r.finite ? "true" : "false") << ", \"autotune_s\": {";
       for (size_t i = 0; i < tuned.size(); ++i) j << (i ? ", " : "") << jstr(tuned[i].first) << ": " << jnum(tuned[i].second);
@@ -989,7 +1008,8 @@ int run_gpu(const Args& a) {
   if (!a.dump.empty()) write_dump(a.dump, a.prob, s->layout(), s->download(0), rank, world, d);
   if (!a.checkpoint.empty())
     write_checkpoint(a.checkpoint, a.prob, s->layout(), s->download(0), s->download(1), rank, world, d);
-  if (s->push() && !comm && !fake) std::remove((rdzv_path() + ".push" + std::to_string(rank)).c_str());
+  if ((s->push() || s->sdma()) && !comm && !fake)
+    std::remove((rdzv_path() + (s->push() ? ".push" : ".sdma") + std::to_string(rank)).c_str());
   // (a peer may still be reading this rank's file of the LAST collective: it stays; every earlier one has been read by
   // everyone, since every peer has entered a later collective — removing a file a peer still needs hangs that peer)
   for (size_t i = 0; i + 1 < fcoll_files.size(); ++i) std::remove(fcoll_files[i].c_str());

@@ -172,6 +172,18 @@ void free_box_copy_table(BoxCopyTable& t);
 void launch_box_copy(const Layout& l, const BoxCopyTable& t, int mode, double* u_s, double* u_s1, double* buf,
                      hipStream_t stream);
 
+// Cross-rank flag words (copy-engine transport): one launch first waits until every word of `wait` equals wait.value
+// (bounded by wait.ticks; a timeout sets *wait.status = 1), then stores signal.value into every word of `signal`.
+struct FlagOp {
+  static constexpr int kMax = 32;
+  unsigned* addr[kMax] = {};
+  int n = 0;
+  unsigned value = 0;
+  unsigned* status = nullptr;
+  unsigned long long ticks = 0;
+};
+void launch_flag_sync(const FlagOp& wait, const FlagOp& signal, hipStream_t stream);
+
 // Pack all strided faces of `plan` from `u` into `buf`, or unpack `buf` into the ghost layers of `u`.
 void launch_pack(const Layout& l, const HaloPlan& plan, const double* u, double* buf, hipStream_t stream);
 void launch_unpack(const Layout& l, const HaloPlan& plan, const double* buf, double* u, hipStream_t stream);

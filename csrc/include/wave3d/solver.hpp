@@ -11,7 +11,9 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
+#include <cstdio>
 #include <memory>
 #include <string>
 #include <vector>
@@ -61,6 +63,13 @@ struct SolverOptions {
   // hipStreamWaitValue32 — eager launches only, for ranks that share one GPU). Peers are connected with
   // connect_push() (multi-process: IPC handles) or by a GpuGroup.
   bool push = false;
+  // Copy-engine ("sdma") transport (deep-tb slab and block ranks): the halo regions are copied into the neighbours'
+  // memory (IPC-mapped: their field buffers' ghost planes for slabs, their staging buffers for blocks) by
+  // hipMemcpyAsync(..., hipMemcpyDeviceToDeviceNoCU) on the side stream — the SDMA engines move them, no compute unit
+  // is taken from the LDS passes — and cross-rank order is kept by flag words in uncached device memory, written and
+  // waited for by the command processors (hipStreamWriteValue32 / hipStreamWaitValue32, graph-capturable on HIP 7.2).
+  // See transport_sdma.cpp for the protocol.
+  bool sdma = false;
   bool push_cp_wait = false;
   // push ranks without an end-of-solve collective (no RCCL communicator): the flag epochs run on over the solves
   // instead of being reset (eager launches: every launch carries its own epochs)
@@ -157,6 +166,21 @@ class GpuSolver {
   std::string push_handles() const;
   void connect_push(const std::vector<std::string>& all);
   void connect_push_self();  // perf study (fake rank): forward into the own staging, wait for the own signals
+  // copy-engine transport: this rank's IPC handles (field buffers, staging, flags) + layout facts, and connecting to
+  // every neighbour from all ranks' handles (index = rank); a fake rank connects to itself
+  bool sdma() const { return sdma_; }
+  std::string sdma_handles() const;
+  void connect_sdma(const std::vector<std::string>& all);
+  void connect_sdma_self();
+  // the halo overlap that actually runs: the exchange is issued on the side stream while the pass's interior runs
+  // (push: the passes produce their face planes first); false for schedules that exchange after the whole pass,
+  // whatever options().overlap says
+  bool overlapped() const {
+    if (!plan_.any() || world_ == 1) return false;
+    return push_ ? opt_.overlap : xstream() != s0_;
+  }
+  // halo transport actually in use: "none" (one rank), "rccl", "push", "sdma", "fake" (perf study, no transport)
+  std::string transport() const;
 
  private:
   friend class GpuGroup;
@@ -301,7 +325,66 @@ class GpuSolver {
   void connect_push_peer(int side, double* stg, unsigned* flags, bool ipc);
   void push_finish(hipStream_t st);  // end of a solve: zero this rank's flags (after its last wait)
   void push_check();                 // after a solve: fail if a wait timed out
+  // copy-engine transport (transport_sdma.cpp). Link k = one neighbour: slab ranks [lo, hi] (faces that exist),
+  // block ranks the peers of deep_[] in direction order. This rank's flag words: [2k] "arrived" (link k's copies into
+  // this rank are complete), [2k + 1] "done" (link k has consumed this rank's previous message and finished the pass
+  // that read the regions the next message overwrites).
+  struct XLink {
+    int peer = -1;
+    int side = 0;                  // slab: 0 = lower neighbour, 1 = upper
+    int slot = 0;                  // this rank's link index in the PEER's flags
+    unsigned* flags = nullptr;     // the peer's flag words (IPC-mapped, or this rank's own for a fake rank)
+    double* u[4] = {nullptr, nullptr, nullptr, nullptr};  // slab: the peer's field buffers
+    double* recv = nullptr;        // block: the peer's receive staging
+    i64 peer_nx = 0;               // slab: the peer's owned planes
+    i64 recv_off[5] = {0, 0, 0, 0, 0};  // block: offset of this rank's message in the peer's staging, per depth s
+    bool ipc = false;              // mapped with hipIpcOpenMemHandle (closed in the destructor)
+  };
+  bool sdma_ = false;
+  std::vector<XLink> xlinks_;
+  unsigned* xflags_ = nullptr;     // uncached: 2 words per link
+  int xpar_ = 0;                   // parity of the solve being enqueued (flag values alternate between two sets)
+  unsigned long long xsolves_ = 0; // solves enqueued so far (every rank runs the same number)
+  hipGraphExec_t xgraph_[2] = {nullptr, nullptr};  // captured solves of either parity
+  unsigned xval(int i) const { return (xpar_ ? 0x10000u : 0u) + static_cast<unsigned>(i + 1); }
+  unsigned xend(int par) const { return (par ? 0x10000u : 0u) + 0xFFFFu; }
+  void sdma_alloc();
+  std::vector<XLink> sdma_links() const;  // link geometry (peer, side, slot) without pointers
+  unsigned* xsig(const XLink& l, int word) const { return l.flags + 2 * l.slot + word; }
+  void unit_exchange_sdma(int i);  // side stream after unit i's shells (or s0 after the pass): copies + "arrived"
+  void sdma_receive(int i);        // s0 before unit i ≥ 1: wait "arrived" (i − 1), unpack, signal "done" (i − 1)
+  void sdma_finish();              // s0 after the last unit: "done" for the next solve's first exchange
+  void sdma_poison(int i, const int uf[2]);  // --poison-ghosts: NaN into the regions exchange i fills
 };
+
+// Per-phase device timers (SolverOptions::timers, eager launches only): every timed launch group is bracketed by two
+// events on its stream; after the solve the intervals are summed per phase (and per unit for --trace). Each group is
+// also a roctx range ("w3d:<phase>:u<unit>"), so rocprofv3 --marker-trace timelines show the schedule.
+template <class F>
+void GpuSolver::timed(int phase, hipStream_t st, F&& f) {
+  if (!opt_.timers) {
+    f();
+    return;
+  }
+  static const char* const kNames[kNumPhases] = {"init", "shell", "compute", "exchange", "check", "gather"};
+  char label[48];
+  std::snprintf(label, sizeof label, "w3d:%s:u%d", kNames[phase], cur_unit_);
+  roctxRangePushA(label);
+  auto take = [&]() {
+    if (ev_next_ == ev_pool_.size()) {
+      hipEvent_t e;
+      W3D_HIP(hipEventCreate(&e));
+      ev_pool_.push_back(e);
+    }
+    return ev_pool_[ev_next_++];
+  };
+  hipEvent_t a = take(), b = take();
+  W3D_HIP(hipEventRecord(a, st));
+  f();
+  W3D_HIP(hipEventRecord(b, st));
+  roctxRangePop();
+  marks_.push_back({phase, cur_unit_, a, b});
+}
 
 }  // namespace wave3d
 

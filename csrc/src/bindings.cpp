@@ -434,6 +434,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("fake_comm", &SolverOptions::fake_comm)
       .def_readwrite("push", &SolverOptions::push)
       .def_readwrite("push_cp_wait", &SolverOptions::push_cp_wait)
+      .def_readwrite("sdma", &SolverOptions::sdma)
       .def_readwrite("push_no_collective", &SolverOptions::push_no_collective)
       .def_readwrite("temporal", &SolverOptions::temporal)
       .def_readwrite("init2", &SolverOptions::init2)
@@ -473,6 +474,17 @@ PYBIND11_MODULE(_C, m) {
              s.connect_push(v);
            },
            "open the slab neighbours' staging and flags from every rank's push_handles() (index = rank)")
+      .def_property_readonly("sdma", &GpuSolver::sdma)
+      .def("sdma_handles", [](const GpuSolver& s) { return py::bytes(s.sdma_handles()); },
+           "this rank's IPC handles (field buffers, staging, flags) + layout facts, to be all-gathered")
+      .def("connect_sdma", [](GpuSolver& s, const std::vector<py::bytes>& all) {
+             std::vector<std::string> v;
+             for (const py::bytes& b : all) v.emplace_back(b);
+             s.connect_sdma(v);
+           },
+           "map every neighbour's buffers and flag words from all ranks' sdma_handles() (index = rank)")
+      .def_property_readonly("overlapped", &GpuSolver::overlapped)
+      .def_property_readonly("transport", &GpuSolver::transport)
       .def("run",
            [](GpuSolver& s) {
              RunResult r;

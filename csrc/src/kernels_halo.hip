@@ -196,4 +196,35 @@ void launch_unpack(const Layout& l, const HaloPlan& plan, const double* buf, dou
   launch<false>(l, plan, u, const_cast<double*>(buf), stream);
 }
 
+// ------------------------------------------------------------------------------------------------------------------
+// Flag words of the copy-engine transport (transport_sdma.cpp): one-workgroup kernels, because a stream wait on a memory
+// value (hipStreamWaitValue32) is not recorded into a hipGraph by this HIP runtime (it runs once, at capture time:
+// tools/probes/memop_capture_probe.hip) while kernel nodes replay. Flag words live in uncached device memory (local or a
+// peer's, IPC-mapped); every access is a system-scope vector atomic.
+// ------------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_flag_sync(const FlagOp w, const FlagOp s) {
+  const int t = static_cast<int>(threadIdx.x);
+  // wait until every watched word equals the value (bounded: after `ticks` of the 100 MHz wall clock the status word
+  // records a timeout and the kernel ends, so a lost peer turns into a host-side error instead of a hung queue)
+  if (t < w.n) {
+    const unsigned long long t0 = wall_clock64();
+    unsigned* a = w.addr[t];
+    while (__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != w.value) {
+      if (wall_clock64() - t0 > w.ticks) {
+        __hip_atomic_store(w.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  __syncthreads();
+  if (t < s.n) __hip_atomic_store(s.addr[t], s.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void launch_flag_sync(const FlagOp& wait, const FlagOp& signal, hipStream_t stream) {
+  W3D_REQUIRE(wait.n <= FlagOp::kMax && signal.n <= FlagOp::kMax && wait.n >= 0 && signal.n >= 0, "flag op: too many");
+  if (wait.n == 0 && signal.n == 0) return;
+  hipLaunchKernelGGL(k_flag_sync, dim3(1), dim3(64), 0, stream, wait, signal);
+}
+
 }  // namespace wave3d

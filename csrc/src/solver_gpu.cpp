@@ -129,8 +129,9 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
       loopback_(loopback) {
   prob_.validate();
   W3D_REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
-  W3D_REQUIRE(world == 1 || comm_ || loopback_ || opt_.fake_comm || (opt_.push && opt_.push_no_collective),
-              "world > 1 needs an RCCL communicator (or the loopback group, or the push transport without one)");
+  W3D_REQUIRE(world == 1 || comm_ || loopback_ || opt_.fake_comm || ((opt_.push || opt_.sdma) && opt_.push_no_collective),
+              "world > 1 needs an RCCL communicator (or the loopback group, or the push / sdma transport without one)");
+  W3D_REQUIRE(!(opt_.push && opt_.sdma), "push and sdma are two different transports");
   dims_ = parse_dims(opt_.decomp, world, prob_.N);
   const Box box = rank_box(prob_, dims_, rank);
   W3D_REQUIRE(box.nx() >= 1 && box.ny() >= 1 && box.nz() >= 1,
@@ -187,6 +188,10 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
     W3D_REQUIRE(need2 + 1.0e8 < static_cast<double>(free_b),
                 "not enough device memory for two field buffers of " + std::to_string(lay_.bytes()) + " bytes");
     break;
+  }
+  if (opt_.sdma && world > 1) {
+    W3D_REQUIRE(mode_ == Mode::kDeepTb, "sdma transport: LDS multi-step passes (deep-tb, slab or block) only, not " + mode());
+    sdma_ = true;
   }
   plan_ = make_halo_plan(lay_, dims_, rank);
   full_ = compute_box(lay_);
@@ -296,6 +301,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
     W3D_HIP(hipMalloc(&send_buf_, static_cast<size_t>(stage) * sizeof(double)));
     W3D_HIP(hipMalloc(&recv_buf_, static_cast<size_t>(stage) * sizeof(double)));
   }
+  if (sdma_) sdma_alloc();
   if (block_tb_)
     for (int st = 2; st <= opt_.temporal; ++st) {
       pack_tab_[st] = make_box_copy_table(deep_[st], false);
@@ -336,6 +342,15 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
 GpuSolver::~GpuSolver() {
   // a destructor must not throw: release errors are dropped on purpose (the device may already be in an error state)
   if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
+  for (hipGraphExec_t g : xgraph_)
+    if (g) (void)hipGraphExecDestroy(g);
+  for (XLink& l : xlinks_)
+    if (l.ipc) {
+      for (double* p : {l.u[0], l.u[1], l.u[2], l.u[3], l.recv})
+        if (p) (void)hipIpcCloseMemHandle(p);
+      if (l.flags) (void)hipIpcCloseMemHandle(l.flags);
+    }
+  if (xflags_) (void)hipFree(xflags_);
   for (BoxCopyTable& t : pack_tab_) free_box_copy_table(t);
   for (BoxCopyTable& t : unpack_tab_) free_box_copy_table(t);
   for (double* p : {u_[0], u_[1], u_[2], u_[3], d_s_, send_buf_, recv_buf_})
@@ -385,6 +400,15 @@ std::vector<int> GpuSolver::check_steps() const {
   for (int n = resume_n_ + 1; n <= prob_.K; ++n)
     if ((ce > 0 && n % ce == 0) || n == prob_.K) v.push_back(n);
   return v;
+}
+
+std::string GpuSolver::transport() const {
+  if (world_ == 1) return "none";
+  if (sdma_) return "sdma";
+  if (push_) return "push";
+  if (opt_.fake_comm) return "fake";
+  if (loopback_) return comm_ ? "rccl-self" : "loopback";
+  return "rccl";
 }
 
 std::string GpuSolver::mode() const {
@@ -534,38 +558,6 @@ void GpuSolver::build_msgs(int i) {
     double* rp = f.contiguous ? field + f.recv_off : recv_buf_ + f.pack_off;
     msgs_.push_back(Msg{f.peer, 0, sp, rp, f.count});
   }
-}
-
-// Per-phase device timers (SolverOptions::timers, eager launches only): every timed launch group is bracketed by two
-// events on its stream; after the solve the intervals are summed per phase (and per unit for --trace). The reference
-// reports its GPU time as compute / H2D-D2H copies / MPI exchange (report.pdf p.16 §4.4); here: init, compute (shell
-// + interior / fused), exchange (pack + RCCL + unpack, overlapped with compute on the side stream) and error check
-// (reductions). Each group is also a roctx range ("w3d:<phase>:u<unit>"), so rocprofv3 --marker-trace timelines
-// show the schedule.
-template <class F>
-void GpuSolver::timed(int phase, hipStream_t st, F&& f) {
-  if (!opt_.timers) {
-    f();
-    return;
-  }
-  static const char* const kNames[kNumPhases] = {"init", "shell", "compute", "exchange", "check", "gather"};
-  char label[48];
-  std::snprintf(label, sizeof label, "w3d:%s:u%d", kNames[phase], cur_unit_);
-  roctxRangePushA(label);
-  auto take = [&]() {
-    if (ev_next_ == ev_pool_.size()) {
-      hipEvent_t e;
-      W3D_HIP(hipEventCreate(&e));
-      ev_pool_.push_back(e);
-    }
-    return ev_pool_[ev_next_++];
-  };
-  hipEvent_t a = take(), b = take();
-  W3D_HIP(hipEventRecord(a, st));
-  f();
-  W3D_HIP(hipEventRecord(b, st));
-  roctxRangePop();
-  marks_.push_back({phase, cur_unit_, a, b});
 }
 
 void GpuSolver::phase_init() {
@@ -783,7 +775,7 @@ void GpuSolver::unit_interior(int i) {
   const double* s = d_s_ + 1;
   // (group ranks: lb_fence already put s0 behind every rank's pull, ev_halo_ included; a second, redundant wait on
   // the own side stream after that fence crashes HIP 7.2's hipStreamEndCapture — tools/capture_probe2.hip flag 36)
-  const bool wait = needs_exchange(i) && xstream() != s0_ && !loopback_;
+  const bool wait = needs_exchange(i) && xstream() != s0_ && (!loopback_ || sdma_);
   int np = 0;  // partials to reduce
   if (mode_ == Mode::kDeep) {
     int off = 0;
@@ -858,13 +850,15 @@ void GpuSolver::enqueue_solve() {
   pending_.clear();
   const bool late = late_exchange();
   for (int i = 0; i < static_cast<int>(units_.size()); ++i) {
+    if (sdma_) sdma_receive(i);
     unit_shell(i);
-    if (!late) unit_exchange_rccl(i);
+    if (!late) sdma_ ? unit_exchange_sdma(i) : unit_exchange_rccl(i);
     unit_interior(i);
-    if (late) unit_exchange_rccl(i);
+    if (late) sdma_ ? unit_exchange_sdma(i) : unit_exchange_rccl(i);
   }
   flush_reduces();
   if (push_) push_finish(s0_);
+  if (sdma_) sdma_finish();
   push_epoch_ += static_cast<int>(units_.size());
   final_buf_ = cur_;
   prev_buf_ = old_;
@@ -963,6 +957,11 @@ void GpuSolver::gather_errors(RunResult& r) {
   wait_stream(s0_, comm_.get(), gpu_timeout_s());
   push_check();
   const int nsrc = static_cast<int>(host.size() / per);
+  // copy-engine transport: a flag wait that timed out marked word 0 of that rank's log (step 0 is never checked)
+  for (int q = 0; q < nsrc && sdma_; ++q)
+    W3D_REQUIRE(host[static_cast<size_t>(q) * per].x == 0.0,
+                "sdma transport: a flag wait timed out on rank " + std::to_string(nsrc > 1 ? q : rank_) +
+                    " (a neighbour stopped or its copies never arrived)");
   const double n_int = static_cast<double>(prob_.N - 1);
   const double denom = n_int * n_int * n_int;
   for (int n : check_steps()) {
@@ -985,7 +984,10 @@ RunResult GpuSolver::run() {
   // first send/recv, which must not happen inside a stream capture; the capture follows on the second run
   if (world_ > 1 && !multistream_capture_safe()) opt_.graph = false;
   const bool capture_ok = !(world_ > 1 && comm_) || runs_ >= 1;
-  if (opt_.graph && !graph_exec_ && capture_ok && !opt_.timers && resume_n_ == 0) {
+  // (copy-engine ranks: the flag values of a solve depend on its parity, so there is one graph per parity)
+  xpar_ = static_cast<int>(xsolves_ & 1);
+  hipGraphExec_t& gx = sdma_ ? xgraph_[xpar_] : graph_exec_;
+  if (opt_.graph && !gx && capture_ok && !opt_.timers && resume_n_ == 0) {
     // capture once (outside the timed region of later runs); fall back to eager launches if capture is refused
     hipGraph_t g = nullptr;
     bool ok = hipStreamBeginCapture(s0_, hipStreamCaptureModeThreadLocal) == hipSuccess;
@@ -998,19 +1000,20 @@ RunResult GpuSolver::run() {
       const hipError_t e = hipStreamEndCapture(s0_, &g);
       ok = ok && e == hipSuccess && g != nullptr;
     }
-    if (ok) ok = hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0) == hipSuccess;
+    if (ok) ok = hipGraphInstantiate(&gx, g, nullptr, nullptr, 0) == hipSuccess;
     if (g) (void)hipGraphDestroy(g);
     (void)hipGetLastError();
     if (!ok) {
-      graph_exec_ = nullptr;
+      gx = nullptr;
       opt_.graph = false;
     }
   }
   const double t0 = now_s();
-  if (graph_exec_ && !opt_.timers && resume_n_ == 0)
-    W3D_HIP(hipGraphLaunch(graph_exec_, s0_));
+  if (gx && opt_.graph && !opt_.timers && resume_n_ == 0)
+    W3D_HIP(hipGraphLaunch(gx, s0_));
   else
     enqueue_solve();
+  ++xsolves_;
   gather_errors(r);
   r.solve_s = now_s() - t0;
   collect_phases(r);
@@ -1208,10 +1211,11 @@ namespace wave3d {
 GpuGroup::GpuGroup(const Problem& prob, const SolverOptions& opt, int world, const std::string& transport)
     : transport_(transport) {
   W3D_REQUIRE(world >= 1, "world must be >= 1");
-  W3D_REQUIRE(transport == "loopback" || transport == "rccl-self" || transport == "push",
-              "group transport must be loopback, rccl-self or push, not " + transport);
+  W3D_REQUIRE(transport == "loopback" || transport == "rccl-self" || transport == "push" || transport == "sdma",
+              "group transport must be loopback, rccl-self, push or sdma, not " + transport);
   SolverOptions o = opt;
   o.push = transport == "push";
+  o.sdma = transport == "sdma";
   for (int r = 0; r < world; ++r) {
     std::shared_ptr<Comm> c;
     if (transport == "rccl-self") c = std::make_shared<Comm>(0, 1, Comm::make_unique_id());
@@ -1239,7 +1243,22 @@ GpuGroup::GpuGroup(const Problem& prob, const SolverOptions& opt, int world, con
       }
     }
   }
-  graph_ = opt.graph && !opt.timers && !opt.debug_sync && (world == 1 || multistream_capture_safe());
+  if (o.sdma && world > 1) {
+    // copy-engine ranks in one process: every link points at the peer rank's own buffers and flag words (no IPC)
+    for (auto& sp : ranks_) {
+      GpuSolver* s = sp.get();
+      W3D_REQUIRE(s->sdma_, "sdma group: every rank must run the LDS multi-step passes (deep-tb)");
+      for (GpuSolver::XLink& l : s->xlinks_) {
+        GpuSolver* q = ranks_[static_cast<size_t>(l.peer)].get();
+        l.flags = q->xflags_;
+        for (int b = 0; b < q->nbuf_; ++b) l.u[b] = q->u_[b];
+        l.recv = q->recv_buf_;
+      }
+    }
+  }
+  // (sdma: the flag waits of one rank's stream are released by other ranks' streams, so the group enqueues eagerly in
+  // an order where every wait is issued after the write it waits for — see enqueue)
+  graph_ = opt.graph && !opt.timers && !opt.debug_sync && (world == 1 || multistream_capture_safe()) && !o.sdma;
   W3D_HIP(hipStreamCreateWithFlags(&gs_, hipStreamNonBlocking));
   W3D_HIP(hipEventCreateWithFlags(&fork_, hipEventDisableTiming));
   W3D_HIP(hipEventCreateWithFlags(&all_packed_, hipEventDisableTiming));
@@ -1277,6 +1296,7 @@ void GpuGroup::enqueue() {
     if (dbg) std::fprintf(stderr, "[group] unit %d %s\n", i, what);
   };
   for (auto* s : rs) {
+    s->xpar_ = static_cast<int>(s->xsolves_ & 1);
     s->phase_init();
     s->tb_region_ = 0;
     s->pending_.clear();
@@ -1284,6 +1304,28 @@ void GpuGroup::enqueue() {
   step("init", -1);
   const int nu = static_cast<int>(rs[0]->units_.size());
   const bool late = rs[0]->late_exchange();
+  if (rs[0]->sdma_) {
+    // copy-engine group: each rank runs its own production schedule; the phases are issued rank by rank so that every
+    // flag wait reaches its HIP queue after the write that releases it (streams of one process may share a hardware
+    // queue, where a wait issued first would block the write behind it): all receives (done(i − 1) writes) of unit i
+    // before any exchange i (which waits for them), every exchange i − 1 ("arrived" writes) before the receives of unit i
+    for (int i = 0; i < nu; ++i) {
+      for (auto* s : rs) s->sdma_receive(i);
+      for (auto* s : rs) {
+        s->unit_shell(i);
+        if (!late) s->unit_exchange_sdma(i);
+        s->unit_interior(i);
+        if (late) s->unit_exchange_sdma(i);
+      }
+      step("unit", i);
+    }
+    for (auto* s : rs) {
+      s->flush_reduces();
+      s->sdma_finish();
+      ++s->xsolves_;
+    }
+    return;
+  }
   for (int i = 0; i < nu; ++i) {
     for (auto* s : rs) s->unit_shell(i);
     step("shell", i);
@@ -1411,6 +1453,9 @@ RunResult GpuGroup::run() {
     s->push_check();
   }
   RunResult r;
+  for (size_t q = 0; q < rs.size(); ++q)
+    W3D_REQUIRE(!rs[q]->sdma_ || all[q * per].x == 0.0,
+                "sdma transport: a flag wait timed out on rank " + std::to_string(q));
   const double n_int = static_cast<double>(rs[0]->prob_.N - 1);
   for (int n : rs[0]->check_steps()) {
     double m = 0.0, sum = 0.0;

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -28,7 +29,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("L", type=float, nargs="?", default=1.0, help="cube edge (default 1)")
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "cpu", "torch"])
     ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "torch", "loopback", "rccl-self", "push",
-                                                               "push-ipc", "native", "none"])
+                                                               "push-ipc", "sdma", "sdma-ipc", "native", "none"])
     ap.add_argument("--world", type=int, default=0,
                     help="ranks of an in-process group on one GPU (transport loopback, or rccl-self: RCCL send/recv)")
     ap.add_argument("--decomp", default="slab", help="slab | block | PxQxR")
@@ -79,11 +80,18 @@ def main(argv=None) -> int:
         kw["device"] = local if a.world == 0 else 0
         kw["timers"] = a.timers
     if a.world:
-        kw.update(transport=transport if transport in ("rccl-self", "push") else "loopback", rank=0, world=a.world)
+        kw.update(transport=transport if transport in ("rccl-self", "push", "sdma") else "loopback", rank=0,
+                  world=a.world)
     s = Solver(spec, **kw)
     if a.resume:
         prev, meta = dumpio.load(a.resume + ".prev")
         cur, meta_c = dumpio.load(a.resume + ".cur")
+        for m in (meta, meta_c):  # the checkpoint must be of THIS problem (tau and L were not compared)
+            for key, want in (("N", a.N), ("tau", a.tau), ("L", a.L)):
+                got = m.get(key)
+                if got is None or not math.isclose(float(got), float(want), rel_tol=1e-15, abs_tol=0.0):
+                    print(f"wave3d: resume: checkpoint {key} = {got} differs from the run's {want}", file=sys.stderr)
+                    return 2
         s.set_state(prev, cur, int(meta_c["step"]))
     r = None
     times = []
@@ -117,7 +125,7 @@ def main(argv=None) -> int:
                            "steps": [[n, m, e] for n, m, e in zip(r.steps, r.max_err, r.rms_err)]}, f)
     if a.dump or a.checkpoint:
         def write(prefix, which):
-            if s.transport in ("loopback", "rccl-self", "push"):
+            if s.transport in ("loopback", "rccl-self", "push", "sdma"):
                 if rank == 0:
                     dumpio.save(prefix, s.global_field(which).numpy(), N=a.N, L=a.L, tau=a.tau,
                                 step=a.K - which)

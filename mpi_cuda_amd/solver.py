@@ -16,6 +16,10 @@ hip        push        world > 1 in ONE process: native GpuGroup as above on the
                        passes themselves into the neighbours' fine-grained staging + flag signalling
 hip        push-ipc    one process per rank (torchrun): native GpuSolver on the slab LDS passes with the push transport
                        between processes (IPC handles all-gathered over torch.distributed; RCCL for the error log)
+hip        sdma        world > 1 in ONE process: native GpuGroup on the LDS passes (slab or block), halos copied by the
+                       SDMA copy engines into the peers' buffers, ordered by command-processor flag waits
+hip        sdma-ipc    one process per rank (torchrun): native GpuSolver with the copy-engine transport between
+                       processes (IPC handles all-gathered over torch.distributed; RCCL for the error log)
 cpu        native      C++ CpuSolver, OpenMP (the reference's sequential / OpenMP programs), world == 1
 cpu        torch       Python step loop, native OpenMP kernels, halos over torch.distributed gloo (MPI analogue)
 torch      -           plain PyTorch fp64 reference solver (oracle), world == 1
@@ -62,7 +66,7 @@ def _resolve(backend: str, transport: str, world: int) -> tuple[str, str]:
     if transport == "auto":
         transport = {"hip": "rccl", "cpu": "native" if world == 1 else "torch", "torch": "none"}[backend]
     ok = {("hip", "rccl"), ("hip", "torch"), ("hip", "loopback"), ("hip", "rccl-self"), ("hip", "push"),
-          ("hip", "push-ipc"),
+          ("hip", "push-ipc"), ("hip", "sdma"), ("hip", "sdma-ipc"),
           ("cpu", "native"),
           ("cpu", "torch"),
           ("torch", "none")}
@@ -110,7 +114,7 @@ class Solver:
             self.device = torch.device("cuda", dev)
         else:
             self.device = torch.device("cpu")
-        if self.backend == "hip" and self.transport in ("loopback", "rccl-self", "push"):
+        if self.backend == "hip" and self.transport in ("loopback", "rccl-self", "push", "sdma"):
             opts = self._options(C, decomp, spec, overlap, graph, tiling, temporal, tiling2, init2, tb, tiling_tb)
             opts.timers, opts.debug_sync, opts.poison_ghosts = timers, debug_sync, poison_ghosts
             if deep_min_planes is not None:
@@ -119,7 +123,7 @@ class Solver:
                 opts.tb_min_planes = tb_min_planes
             self._impl = C.GpuGroup(spec.native(), opts, world, self.transport)
             self.dims = self._impl.dims().as_tuple()
-        elif self.backend == "hip" and self.transport in ("rccl", "push-ipc"):
+        elif self.backend == "hip" and self.transport in ("rccl", "push-ipc", "sdma-ipc"):
             from .parallel.rccl import make_comm
 
             opts = self._options(C, decomp, spec, overlap, graph, tiling, temporal, tiling2, init2, tb, tiling_tb)
@@ -129,10 +133,11 @@ class Solver:
             if tb_min_planes is not None:
                 opts.tb_min_planes = tb_min_planes
             opts.push = self.transport == "push-ipc"
-            # (push-ipc without RCCL — ranks sharing one GPU, which RCCL refuses: no communicator, so no end-of-solve
-            # collective; each rank's error log is its own)
-            opts.push_no_collective = opts.push and not rccl
-            if comm is None and world > 1 and (rccl or not opts.push):
+            opts.sdma = self.transport == "sdma-ipc"
+            # (push-ipc / sdma-ipc without RCCL — ranks sharing one GPU, which RCCL refuses: no communicator, so no
+            # end-of-solve collective; each rank's error log is its own)
+            opts.push_no_collective = (opts.push or opts.sdma) and not rccl
+            if comm is None and world > 1 and (rccl or not (opts.push or opts.sdma)):
                 comm = make_comm(rank, world, group)
             self.comm = comm
             self._impl = C.GpuSolver(spec.native(), opts, rank, world, comm)
@@ -142,6 +147,12 @@ class Solver:
                 handles = [None] * world
                 tdist.all_gather_object(handles, self._impl.push_handles(), group=group)
                 self._impl.connect_push(handles)
+            if self._impl.sdma and world > 1:
+                import torch.distributed as tdist
+
+                handles = [None] * world
+                tdist.all_gather_object(handles, self._impl.sdma_handles(), group=group)
+                self._impl.connect_sdma(handles)
             self.dims = self._impl.dims.as_tuple()
         elif self.transport in ("torch",):
             from .parallel.dist_solver import TorchDistSolver
@@ -218,7 +229,7 @@ class Solver:
         """The whole (N+1)³ field u^K (which=0) / u^{K-1} (which=1) on the CPU (single rank or loopback group)."""
         from .ops.stencil import grid_view
 
-        if self.transport not in ("loopback", "rccl-self", "push"):
+        if self.transport not in ("loopback", "rccl-self", "push", "sdma"):
             if self.world != 1:
                 raise RuntimeError("global_field needs world == 1 or the loopback transport")
             return self.owned_field(which)

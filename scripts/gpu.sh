@@ -13,6 +13,10 @@
 #                                            2x2x2 blocks (overlap / sequential) at 512^3 and 2048^3, rank 3/8
 #   scripts/gpu.sh fakesweep                 512^3 compute-only scaling projection (one rank of P, P = 1/2/4/8)
 #   scripts/gpu.sh ab [wave3d args]          same-box A/B: build/ab/wave3d_base vs bin/wave3d -> gpurun_out/ab.log
+#   scripts/gpu.sh transports                per-rank solve times (--fake-rank) of sequential / RCCL-overlap / copy-engine
+#                                            (sdma) schedules: 512^3 slab 1/8 + 1/2, 2x2x2 blocks at 512^3 and 2048^3
+#                                            -> gpurun_out/transports.log
+#   scripts/gpu.sh probe                     tools/probes/sdma_probe (copy engines, memops, capture) -> gpurun_out/probe.log
 #   scripts/gpu.sh all                       test && cli && bench && profbench
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -115,7 +119,28 @@ run_fakesweep() {
   cat "$out"
 }
 
+run_transports() {
+  local fr v
+  for fr in 512:0.001:1/8:slab 512:0.001:0/2:slab 512:0.001:3/8:2x2x2 2048:0.00025:3/8:2x2x2; do
+    IFS=: read -r N tau r dec <<< "$fr"
+    for v in "--no-overlap" "" "--transport sdma" "--transport sdma --no-overlap"; do
+      echo "== N=$N fake $r --decomp $dec $v"
+      timeout -k 5 120 ./bin/wave3d "$N" "$tau" 20 1 --fake-rank "$r" --decomp "$dec" --repeat 7 --warmup 2 --quiet $v \
+        | grep -E "Total time|Throughput" || return 1
+    done
+  done
+}
+run_probe() {
+  [ -x build/sdma_probe ] || { echo "build/sdma_probe missing" >&2; return 1; }
+  timeout -k 10 120 build/sdma_probe > gpurun_out/probe.log 2>&1
+  local rc=$?
+  cat gpurun_out/probe.log
+  return $rc
+}
+
 case "$what" in
+  transports) run_transports > gpurun_out/transports.log 2>&1; rc=$?; cat gpurun_out/transports.log; exit $rc ;;
+  probe) run_probe ;;
   fakesweep) run_fakesweep ;;
   ab) run_ab "$@" > gpurun_out/ab.log 2>&1; rc=$?; cat gpurun_out/ab.log; exit $rc ;;
   test) run_test "$@" ;;

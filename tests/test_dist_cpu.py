@@ -104,3 +104,43 @@ def test_bench_setup_failure_on_one_rank_exits_instead_of_hanging(tmp_path):
     assert p.returncode != 0
     assert "injected fault" in p.stderr
     assert not [l for l in p.stdout.splitlines() if l.startswith("{")]
+
+
+def _bench_args(**kw):
+    import argparse
+
+    d = dict(N=512, tau=1e-3, K=20, L=1.0)
+    d.update(kw)
+    return argparse.Namespace(**d)
+
+
+def test_bench_correct_gate_uses_the_oracle_for_every_config():
+    """bench.py's correctness gate: every config, the 2048³ scale point included, is checked step by
+    step against the closed-form oracle of the discrete scheme; a log off by 0.1 % (or non-finite) fails."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from mpi_cuda_amd import ProblemSpec
+    from mpi_cuda_amd.models.wave3d import oracle_errors
+
+    for N, tau, K, L in [(512, 1e-3, 20, 1.0), (2048, 2.5e-4, 20, 1.0), (128, 1e-3, 20, 3.141592653589793),
+                         (96, 1e-3, 11, 1.0)]:
+        a = _bench_args(N=N, tau=tau, K=K, L=L)
+        spec = ProblemSpec(N=N, tau=tau, K=K, L=L, check_every=2)
+        ref = oracle_errors(spec)
+        steps = [[n, float(f"{m:.10g}"), float(f"{e:.10g}")] for n, (m, e) in sorted(ref.items())]  # CLI JSON digits
+        ok, why = bench._correct(a, True, steps)
+        assert ok, why
+        bad = [[n, m * 1.001, e] for n, m, e in steps]  # (2048³: caught at the later steps, where 0.1 % > rounding)
+        assert not bench._correct(a, True, bad)[0]
+        assert not bench._correct(a, False, steps)[0]
+        assert not bench._correct(a, True, [])[0]
+    # the reference config also pins the reference's printed digits (report.pdf p.16): the oracle alone would accept
+    # a log within 1e-5 of it
+    a = _bench_args()
+    steps = [[n, m, e] for n, (m, e) in sorted(oracle_errors(ProblemSpec(N=512, tau=1e-3, K=20)).items())]
+    ok, _ = bench._correct(a, True, steps)
+    assert ok
+    # the measured 2048³ log of profiles/r2_final/cli_2048.log (one MI355X) passes
+    a = _bench_args(N=2048, tau=2.5e-4)
+    logged = [[2, 1.553202e-13, 5.485516e-14], [10, 3.875233e-12, 1.370967e-12], [20, 1.549894e-11, 5.483359e-12]]
+    assert bench._correct(a, True, logged)[0]

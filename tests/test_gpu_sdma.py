@@ -1,0 +1,155 @@
+"""The copy-engine ("sdma") halo transport of the LDS multi-step passes (SolverOptions::sdma, transport_sdma.cpp).
+
+Halo regions are copied into the neighbours' memory by hipMemcpyAsync(..., hipMemcpyDeviceToDeviceNoCU) — the SDMA
+engines, no compute unit taken from the passes — and cross-rank order is kept by flag words written / waited for by the
+command processors (hipStreamWriteValue32 / hipStreamWaitValue32). Slab ranks copy their face planes straight into the
+neighbours' ghost planes on the side stream while the interior pass runs; block ranks pack (k_box_copy), copy every
+peer's message into its staging and unpack before the next pass.
+
+On one GPU this runs as
+  * an in-process GpuGroup (each rank's own production schedule on its own streams, eager);
+  * a fake rank (perf study: every link is the rank itself) — graph-captured, flags waited for inside the graph;
+  * P processes sharing the GPU (``--np P --no-rccl``): IPC-mapped buffers and flags of the other processes, one
+    captured graph per solve parity.
+Every variant must be BIT-identical to the single-GPU solve (the reference's "1-GPU log == 2-GPU log" property,
+report.pdf p.15-16 §4.3), with NaN-poisoned ghosts where the schedule allows it.
+"""
+import json
+import math
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from mpi_cuda_amd import ProblemSpec
+from mpi_cuda_amd.solver import Solver
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "bin", "wave3d")
+ENV = dict(os.environ, W3D_TIMEOUT_S="30")
+
+
+def _same(r, r1):
+    assert r.finite and r.steps == r1.steps
+    assert r.max_err == r1.max_err
+    for a, b in zip(r.rms_err, r1.rms_err):
+        assert math.isclose(a, b, rel_tol=1e-12)
+
+
+def _ref(spec):
+    ref = Solver(spec, backend="hip", device=0, temporal=1)
+    r1 = ref.run()
+    return r1, ref.global_field(0), ref.global_field(1)
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("K,check_every,temporal", [(20, 2, 4), (9, 1, 4), (12, 3, 3), (11, 2, 2)])
+def test_sdma_group_slab_bitexact(gpu, world, overlap, K, check_every, temporal):
+    spec = ProblemSpec(N=66, tau=1e-3, K=K, check_every=check_every)
+    r1, f0, f1 = _ref(spec)
+    g = Solver(spec, backend="hip", transport="sdma", world=world, rank=0, decomp="slab", overlap=overlap,
+               device=0, poison_ghosts=True, tb_min_planes=2 * temporal, temporal=temporal)
+    assert g.native.mode() == "deep-tb" and g.native.transport == "sdma"
+    for _ in range(3):  # both flag-value parities and a second solve of the first
+        r = g.run()
+        _same(r, r1)
+        assert torch.equal(g.global_field(0), f0)
+        assert torch.equal(g.global_field(1), f1)
+
+
+@pytest.mark.parametrize("world,decomp", [(4, "2x2x1"), (8, "2x2x2"), (4, "1x2x2"), (6, "3x2x1")])
+@pytest.mark.parametrize("K,check_every,temporal", [(20, 2, 4), (9, 1, 4), (11, 2, 2)])
+def test_sdma_group_block_bitexact(gpu, world, decomp, K, check_every, temporal):
+    spec = ProblemSpec(N=66, tau=1e-3, K=K, check_every=check_every)
+    r1, f0, f1 = _ref(spec)
+    g = Solver(spec, backend="hip", transport="sdma", world=world, rank=0, decomp=decomp, device=0,
+               poison_ghosts=True, temporal=temporal)
+    assert g.native.mode() == "deep-tb-block"
+    for _ in range(3):
+        r = g.run()
+        _same(r, r1)
+        assert torch.equal(g.global_field(0), f0)
+        assert torch.equal(g.global_field(1), f1)
+
+
+def test_sdma_needs_lds_passes(gpu):
+    spec = ProblemSpec(N=40, tau=1e-3, K=10)
+    with pytest.raises(Exception, match="sdma transport"):
+        Solver(spec, backend="hip", transport="sdma", world=4, rank=0, decomp="slab", device=0, temporal=1)
+
+
+@pytest.mark.parametrize("decomp,rank", [("slab", "1/4"), ("2x2x2", "3/8"), ("slab", "0/2")])
+def test_sdma_fake_rank_graph(gpu, tmp_path, decomp, rank):
+    """Perf-study mode with the real traffic: one rank of P alone, its copies landing in its own ghosts / staging and
+    its flags raised for itself — the solve is captured (one graph per parity) and replayed."""
+    js = str(tmp_path / "f.json")
+    subprocess.run([CLI, "128", "0.001", "20", "1", "--fake-rank", rank, "--decomp", decomp, "--transport", "sdma",
+                    "--repeat", "4", "--json", js, "--quiet"], check=True, timeout=120, env=ENV)
+    meta = json.loads(open(js).read())
+    assert meta["transport"] == "sdma" and meta["mode"].startswith("deep-tb") and meta["finite"]
+    assert meta["graph"] is True
+    assert meta["overlap"] is (decomp == "slab")  # block ranks exchange after the whole pass
+
+
+def _assert_same_field(f, ref):
+    d = np.abs(f - ref)
+    bad = np.argwhere(~(d == 0))
+    assert len(bad) == 0, f"{len(bad)} nodes differ, max |diff| {np.nanmax(d):.3e}, x planes {sorted(set(bad[:, 0]))[:10]}"
+
+
+def _single(N, K, check_every=2):
+    s = Solver(ProblemSpec(N=N, tau=1e-3, K=K, check_every=check_every), backend="hip", device=0)
+    r = s.run()
+    return r, s.global_field(0).numpy()
+
+
+def _read_dump(prefix, world, N):
+    field = np.zeros((N + 1,) * 3)
+    for r in range(world):
+        m = json.loads(open(f"{prefix}.rank{r}.json").read())
+        nx, ny, nz = m["shape"]
+        x0, y0, z0 = m["offset"]
+        field[x0:x0 + nx, y0:y0 + ny, z0:z0 + nz] = np.fromfile(f"{prefix}.rank{r}.bin").reshape(nx, ny, nz)
+    return field
+
+
+@pytest.mark.parametrize("np_,decomp,extra", [(2, "slab", ()), (2, "slab", ("--no-overlap",)),
+                                              (2, "slab", ("--poison-ghosts",)), (2, "1x2x1", ()),
+                                              (4, "2x2x1", ()), (3, "slab", ("--temporal", "3"))])
+def test_sdma_processes_share_gpu(gpu, tmp_path, np_, decomp, extra):
+    """P processes (fork before any GPU call) on one GPU, no RCCL: each maps its neighbours' buffers and flag words
+    through hipIpcOpenMemHandle (handles exchanged through files); the solves are graph-captured per parity. The dumped
+    fields are bit-identical to one GPU and the combined error log is the reference's."""
+    N, K = 96, 20
+    r1, f1 = _single(N, K)
+    prefix, js = str(tmp_path / "p"), str(tmp_path / "p.json")
+    env = dict(ENV, W3D_SHARE_GPUS="1")
+    env.pop("W3D_RDZV_FILE", None)
+    cmd = [CLI, str(N), "0.001", str(K), "1", "--np", str(np_), "--decomp", decomp, "--transport", "sdma", "--no-rccl",
+           "--warmup", "1", "--repeat", "4", "--dump", prefix, "--json", js, "--quiet", *extra]
+    subprocess.run(cmd, check=True, timeout=150, env=env, capture_output=True, text=True)
+    meta = json.loads(open(js).read())
+    assert meta["transport"] == "sdma" and meta["graph"] is True
+    _assert_same_field(_read_dump(prefix, np_, N), f1)
+    for (n, m, e), m1, e1 in zip(meta["steps"], r1.max_err, r1.rms_err):
+        assert m == pytest.approx(m1, rel=1e-9) and e == pytest.approx(e1, rel=1e-9)
+
+
+def test_bench_two_ranks_sdma_rehearsal(gpu, tmp_path):
+    """bench.py end to end with 2 ranks on one GPU over the copy-engine transport (IPC, host collectives through
+    files): the reference log, marked as a rehearsal, not a scaling point."""
+    out = tmp_path / "b.jsonl"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(29800 + os.getpid() % 150), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--share-gpus", "--no-rccl", "--native-transport", "sdma", "--steps", "5", "--warmup", "2",
+           "--out", str(out)]
+    subprocess.run(cmd, check=True, timeout=240, env=ENV, capture_output=True, text=True)
+    line = json.loads(out.read_text().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["distinct_gpus"] == 1 and "rehearsal" in line
+    assert line["config"]["transport"] == "sdma" and line["config"]["schedule"].endswith("-sdma")
+    assert line["correct"] is True and line["final_max_err"] == pytest.approx(3.960129e-09, rel=1e-6)

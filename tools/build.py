@@ -47,6 +47,7 @@ LIB_SOURCES = [
     ("src/kernels_leapfrog_tb.hip", "hip"),
     ("src/kernels_leapfrog_tb_push.hip", "hip"),
     ("src/solver_gpu.cpp", "hip"),
+    ("src/transport_sdma.cpp", "hip"),
     ("src/cpu_kernels.cpp", "cpu"),
     ("src/cpu_solver.cpp", "cpu"),
     ("src/cpu_dist.cpp", "cpu"),

@@ -28,6 +28,7 @@
 
 #include "wave3d/cpu.hpp"
 #include "wave3d/cpu_dist.hpp"
+#include "wave3d/runtime.hpp"
 #include "wave3d/solver.hpp"
 
 using namespace wave3d;
@@ -55,6 +56,7 @@ struct Args {
   int group = 0;                       // --group P: all P ranks in this process on one GPU
   int bench_steps = 0;                 // --bench-steps K: timed block of K solves (bench.py contract)
   bool autotune = false;               // --autotune: time the multi-rank schedule candidates, keep the fastest
+  int autotune_rounds = 5;             // --autotune-rounds R: interleaved timing rounds
   bool phases = false;                 // --phases: per-phase breakdown from a traced solve of the timed schedule
   std::string group_transport = "rccl-self";
   std::string transport = "rccl";      // --transport rccl | push (slab LDS passes: halos pushed by the passes)
@@ -199,6 +201,7 @@ Args parse(int argc, char** argv) {
     else if (s == "--group") a.group = std::stoi(next());
     else if (s == "--bench-steps") a.bench_steps = std::stoi(next());
     else if (s == "--autotune") a.autotune = true;
+    else if (s == "--autotune-rounds") a.autotune_rounds = std::stoi(next());
     else if (s == "--phases") a.phases = true;
     else if (s == "--group-transport") a.group_transport = next();
     else if (s == "--transport") a.transport = next();
@@ -241,227 +244,22 @@ Args parse(int argc, char** argv) {
   return a;
 }
 
-const char* const kRankEnv[] = {"RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID", nullptr};
-const char* const kSizeEnv[] = {"WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "SLURM_NTASKS", nullptr};
-
-// Name of the shared segment of the CPU ranks of one launcher job: W3D_JOB_ID, else the launcher's job id
-// (torchrun TORCHELASTIC_RUN_ID, SLURM_JOB_ID, PMIx namespace), else MASTER_PORT, else the parent pid (the ranks of
-// one node are children of the same launcher process).
-std::string job_segment_name() {
-  static const char* const kJob[] = {"W3D_JOB_ID", "TORCHELASTIC_RUN_ID", "SLURM_JOB_ID", "PMIX_NAMESPACE",
-                                     "OMPI_MCA_orte_ess_jobid", "MASTER_PORT", nullptr};
-  std::string id;
-  for (const char* const* n = kJob; *n && id.empty(); ++n)
-    if (const char* v = std::getenv(*n); v && *v) id = v;
-  if (id.empty()) id = std::to_string(static_cast<long long>(getppid()));
-  std::string name = "/wave3d-cpu-";
-  for (char c : id) name += std::isalnum(static_cast<unsigned char>(c)) ? c : '_';
-  return name;
-}
-
-int env_int(const char* const* names, int dflt) {
-  for (const char* const* n = names; *n; ++n) {
-    const char* v = std::getenv(*n);
-    if (v && *v) return std::atoi(v);
-  }
-  return dflt;
-}
-
-double now_s() {
-  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
-// Rendezvous of the RCCL unique id through a file on the node. The name is per launch: W3D_RDZV_FILE (the --np
-// self-spawn and bench.py pass a fresh nonce), else MASTER_PORT + TORCHELASTIC_RUN_ID + the launcher's pid (the ranks of
-// one torchrun/mpiexec job share their parent). Rank 0 removes a stale file of that name before publishing, and the
-// other ranks only accept a file written after this process started (minus a grace period for a fast rank 0), so a
-// file left by a crashed earlier job is never consumed.
-std::string rdzv_path() {
-  if (const char* p = std::getenv("W3D_RDZV_FILE")) return p;
-  const char* port = std::getenv("MASTER_PORT");
-  const char* run = std::getenv("TORCHELASTIC_RUN_ID");
-  std::ostringstream os;
-  os << "/tmp/wave3d-rdzv-" << (port ? port : "0") << "-" << (run ? run : "x") << "-" << getppid() << ".uid";
-  return os.str();
-}
-
-std::string exchange_unique_id(int rank) {
-  const std::string path = rdzv_path();
-  static const double t_start = static_cast<double>(std::time(nullptr));
-  if (rank == 0) {
-    std::remove(path.c_str());
-    const std::string id = Comm::make_unique_id();
-    const std::string tmp = path + ".tmp";
-    {
-      std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
-      f.write(id.data(), static_cast<std::streamsize>(id.size()));
-      if (!f) fail("cannot write rendezvous file " + tmp);
-    }
-    if (std::rename(tmp.c_str(), path.c_str()) != 0) fail("cannot publish rendezvous file " + path);
-    return id;
-  }
-  const double t0 = now_s();
-  for (;;) {
-    struct stat st {};
-    if (stat(path.c_str(), &st) == 0 && static_cast<double>(st.st_mtime) >= t_start - 60.0) {
-      std::ifstream f(path, std::ios::binary);
-      std::string id((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-      if (id.size() == 128) return id;
-    }
-    if (now_s() - t0 > 120.0) fail("timed out waiting for rendezvous file " + path);
-    std::this_thread::sleep_for(std::chrono::milliseconds(20));
-  }
-}
-
 void print_errors(const std::vector<int>& steps, const std::vector<double>& mx, const std::vector<double>& rms,
                   double tau) {
   for (size_t i = 0; i < steps.size(); ++i)
     std::printf("Step %d, t = %f, Max Error = %e, L2 Error = %e\n", steps[i], steps[i] * tau, mx[i], rms[i]);
 }
 
-void write_dump(const std::string& prefix, const Problem& p, const Layout& l, const std::vector<double>& u, int rank,
-                int world, const Dims& d, int step = -1) {
-  if (step < 0) step = p.K;
-  const std::string base = world > 1 ? prefix + ".rank" + std::to_string(rank) : prefix;
-  std::ofstream f(base + ".bin", std::ios::binary | std::ios::trunc);
-  std::vector<double> row(static_cast<size_t>(l.nz));
-  for (i64 ix = 0; ix < l.nx; ++ix)
-    for (i64 iy = 0; iy < l.ny; ++iy) {
-      const double* src = u.data() + l.off(ix, iy, 0);
-      std::memcpy(row.data(), src, row.size() * sizeof(double));
-      f.write(reinterpret_cast<const char*>(row.data()), static_cast<std::streamsize>(row.size() * sizeof(double)));
-    }
-  std::ofstream j(base + ".json", std::ios::trunc);
-  j.precision(17);
-  j << "{\"format\": \"wave3d-dump-v1\", \"dtype\": \"float64\", \"order\": \"C\", \"N\": " << p.N
-    << ", \"L\": " << p.L << ", \"tau\": " << p.tau << ", \"step\": " << step << ", \"t\": " << step * p.tau
-    << ", \"shape\": [" << l.nx << ", " << l.ny << ", " << l.nz << "], \"offset\": [" << l.gx0 << ", " << l.gy0
-    << ", " << l.gz0 << "], \"global_shape\": [" << p.N + 1 << ", " << p.N + 1 << ", " << p.N + 1
-    << "], \"rank\": " << rank << ", \"world\": " << world << ", \"dims\": [" << d.px << ", " << d.py << ", " << d.pz
-    << "]}\n";
-}
-
-// --checkpoint PREFIX: u^K → PREFIX.cur, u^{K−1} → PREFIX.prev (wave3d-dump-v1, per rank when world > 1)
-void write_checkpoint(const std::string& prefix, const Problem& p, const Layout& l, const std::vector<double>& cur,
-                      const std::vector<double>& prev, int rank, int world, const Dims& d) {
-  write_dump(prefix + ".cur", p, l, cur, rank, world, d, p.K);
-  write_dump(prefix + ".prev", p, l, prev, rank, world, d, p.K - 1);
-}
-
-// Number after "key": in a one-line JSON object (the dump sidecars this program writes).
-std::vector<double> json_numbers(const std::string& text, const std::string& key) {
-  std::vector<double> out;
-  const size_t k = text.find("\"" + key + "\"");
-  if (k == std::string::npos) return out;
-  size_t i = text.find(':', k) + 1;
-  const bool list = text.find_first_not_of(" ", i) != std::string::npos && text[text.find_first_not_of(" ", i)] == '[';
-  if (list) i = text.find('[', i) + 1;
-  for (;;) {
-    char* end = nullptr;
-    const double v = std::strtod(text.c_str() + i, &end);
-    if (end == text.c_str() + i) break;
-    out.push_back(v);
-    i = static_cast<size_t>(end - text.c_str());
-    if (!list) break;
-    i = text.find_first_of(",]", i);
-    if (i == std::string::npos || text[i] == ']') break;
-    ++i;
-  }
-  return out;
-}
-
-// The GLOBAL (N+1)³ field of a dump PREFIX (one file, or PREFIX.rankR of any decomposition); returns its step.
-int load_dump_global(const std::string& prefix, const Problem& p, std::vector<double>& g) {
-  auto slurp = [](const std::string& path) {
-    std::ifstream f(path);
-    return std::string((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-  };
-  std::string meta = slurp(prefix + ".json");
-  std::vector<std::string> bases;
-  if (!meta.empty()) {
-    bases.push_back(prefix);
-  } else {
-    meta = slurp(prefix + ".rank0.json");
-    W3D_REQUIRE(!meta.empty(), "resume: no dump " + prefix + ".json or " + prefix + ".rank0.json");
-    const std::vector<double> w = json_numbers(meta, "world");
-    W3D_REQUIRE(!w.empty() && w[0] >= 1, "resume: dump without a world size");
-    for (int r = 0; r < static_cast<int>(w[0]); ++r) bases.push_back(prefix + ".rank" + std::to_string(r));
-  }
-  const i64 n1 = p.N + 1;
-  g.assign(static_cast<size_t>(n1 * n1 * n1), 0.0);
-  int step = -1;
-  for (const std::string& b : bases) {
-    const std::string m = slurp(b + ".json");
-    const std::vector<double> sh = json_numbers(m, "shape"), of = json_numbers(m, "offset"), st = json_numbers(m, "step"),
-                              nn = json_numbers(m, "N");
-    W3D_REQUIRE(sh.size() == 3 && of.size() == 3 && st.size() == 1 && nn.size() == 1, "resume: bad sidecar " + b);
-    W3D_REQUIRE(static_cast<i64>(nn[0]) == p.N, "resume: dump N differs from the run's N");
-    // (tau and L too: a checkpoint of another problem would continue from an inconsistent state; the sidecar holds
-    // them with 17 significant digits, so they round-trip exactly)
-    for (const auto& [key, want] : {std::pair<const char*, double>{"tau", p.tau}, {"L", p.L}}) {
-      const std::vector<double> v = json_numbers(m, key);
-      W3D_REQUIRE(v.size() == 1 && std::fabs(v[0] - want) <= 1e-15 * std::fabs(want),
-                  std::string("resume: dump ") + key + " differs from the run's " + key);
-    }
-    W3D_REQUIRE(step < 0 || step == static_cast<int>(st[0]), "resume: rank dumps of different steps");
-    step = static_cast<int>(st[0]);
-    const i64 nx = static_cast<i64>(sh[0]), ny = static_cast<i64>(sh[1]), nz = static_cast<i64>(sh[2]);
-    const i64 x0 = static_cast<i64>(of[0]), y0 = static_cast<i64>(of[1]), z0 = static_cast<i64>(of[2]);
-    W3D_REQUIRE(x0 >= 0 && y0 >= 0 && z0 >= 0 && x0 + nx <= n1 && y0 + ny <= n1 && z0 + nz <= n1,
-                "resume: dump box outside the grid");
-    std::ifstream f(b + ".bin", std::ios::binary);
-    W3D_REQUIRE(static_cast<bool>(f), "resume: cannot read " + b + ".bin");
-    for (i64 x = 0; x < nx; ++x)
-      for (i64 y = 0; y < ny; ++y)
-        f.read(reinterpret_cast<char*>(g.data() + ((x0 + x) * n1 + (y0 + y)) * n1 + z0),
-               static_cast<std::streamsize>(nz * static_cast<i64>(sizeof(double))));
-    W3D_REQUIRE(static_cast<bool>(f), "resume: short file " + b + ".bin");
-  }
-  return step;
-}
-
-// --resume PREFIX: u^{n0−1} from PREFIX.prev, u^{n0} from PREFIX.cur; returns n0
-int load_checkpoint(const std::string& prefix, const Problem& p, std::vector<double>& prev, std::vector<double>& cur) {
-  const int sc = load_dump_global(prefix + ".cur", p, cur);
-  const int sp = load_dump_global(prefix + ".prev", p, prev);
-  W3D_REQUIRE(sp == sc - 1, "resume: PREFIX.prev must hold the step before PREFIX.cur");
-  W3D_REQUIRE(sc >= 1 && sc < p.K, "resume: checkpoint step " + std::to_string(sc) + " is not before K");
-  return sc;
-}
-
-int spawn(int np, char** argv) {
-  // Fork the ranks before anything touches the GPU; each child continues in main() with its rank in the env.
-  std::ostringstream rf;
-  rf << "/tmp/wave3d-rdzv-spawn-" << getpid() << "-" << static_cast<long long>(now_s() * 1e6) << ".uid";
-  const std::string rdzv = rf.str();
-  std::vector<pid_t> kids;
-  for (int r = 0; r < np; ++r) {
-    const pid_t pid = fork();
-    if (pid < 0) fail("fork failed");
-    if (pid == 0) {
-      setenv("RANK", std::to_string(r).c_str(), 1);
-      setenv("LOCAL_RANK", std::to_string(r).c_str(), 1);
-      setenv("WORLD_SIZE", std::to_string(np).c_str(), 1);
-      setenv("W3D_RDZV_FILE", rdzv.c_str(), 1);
-      setenv("W3D_SPAWNED", "1", 1);
-      return -1;  // child: continue
-    }
-    kids.push_back(pid);
-  }
-  (void)argv;
-  int rc = 0;
-  for (pid_t k : kids) {
-    int st = 0;
-    waitpid(k, &st, 0);
-    const int c = WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNALED(st) ? WTERMSIG(st) : 0);
-    if (c != 0 && rc == 0) rc = c;
-  }
-  std::remove(rdzv.c_str());
-  return rc;
-}
-
 // json helpers for the summary line
 std::string jstr(const std::string& v) { return "\"" + v + "\""; }
+std::string json_escape(const std::string& v) {
+  std::string o;
+  for (char c : v) {
+    if (c == '"' || c == '\\') o += '\\';
+    if (static_cast<unsigned char>(c) >= 0x20) o += c;
+  }
+  return o;
+}
 std::string jnum(double v) {
   char b[64];
   std::snprintf(b, sizeof b, "%.10g", v);
@@ -492,9 +290,9 @@ int run_cpu(const Args& a) {
   }
   double bench_s = 0.0;
   if (a.bench_steps > 0) {
-    const double t0 = now_s();
+    const double t0 = wall_s();
     for (int i = 0; i < a.bench_steps; ++i) r = s.run();
-    bench_s = now_s() - t0;
+    bench_s = wall_s() - t0;
   }
   if (!a.quiet) print_errors(r.steps, r.max_err, r.rms_err, a.prob.tau);
   const double gcell = a.prob.cell_updates() / best / 1e9;
@@ -535,10 +333,10 @@ int run_cpu_rank(const Args& a, ShmGroup& g, int rank) {
     double bench_s = 0.0;  // the end barrier waits for the slowest rank: rank 0's interval is the max over ranks
     if (a.bench_steps > 0) {
       g.barrier();
-      const double t0 = now_s();
+      const double t0 = wall_s();
       for (int i = 0; i < a.bench_steps; ++i) r = s.run();
       g.barrier();
-      bench_s = now_s() - t0;
+      bench_s = wall_s() - t0;
     }
     const Dims d = g.dims();
     if (rank == 0) {
@@ -648,74 +446,18 @@ int run_group(const Args& a, const SolverOptions& o, const hipDeviceProp_t& prop
   return r.finite ? 0 : 3;
 }
 
-// One schedule candidate of the multi-rank autotune (bench.py's --autotune): the halo volume of
-// S-deep passes against the per-step exchanges of single steps, overlap against whole passes, slabs against blocks —
-// a trade of xGMI bandwidth/latency against HBM traffic that depends on the node, so each candidate is timed on the
-// real interconnect and every rank adopts the one whose slowest rank was fastest.
-struct Candidate {
-  const char* name;
-  const char* decomp;
-  int temporal;
-  bool overlap;
-  bool push = false;  // slab LDS passes with the push transport (faces forwarded by the passes, flags)
-};
-constexpr Candidate kCandidates[] = {
-    {"slab-S4", "slab", 4, true},          {"slab-S4-seq", "slab", 4, false},
-    {"slab-S4-push", "slab", 4, true, true}, {"slab-S4-push-seq", "slab", 4, false, true},
-    {"slab-S3", "slab", 3, true},          {"slab-S2", "slab", 2, true},
-    {"slab-S1", "slab", 1, true},          {"block-S4", "block", 4, true},
-    {"block-S4-seq", "block", 4, false},   {"block-S3", "block", 3, true},
-    {"block-S1", "block", 1, true},
-};
-
-// Every rank's bytes through files next to the rendezvous file (ranks without a communicator: --no-rccl). Each rank
-// publishes <rdzv>.push<rank> atomically and reads the others' (written after this process started).
-std::vector<std::string> file_allgather(int rank, int world, const std::string& mine, const std::string& tag = "push") {
-  static const double t_start = static_cast<double>(std::time(nullptr));
-  auto path = [&](int r) { return rdzv_path() + "." + tag + std::to_string(r); };
-  {
-    const std::string tmp = path(rank) + ".tmp";
-    std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
-    f.write(mine.data(), static_cast<std::streamsize>(mine.size()));
-    if (!f) fail("cannot write " + tmp);
-    f.close();
-    if (std::rename(tmp.c_str(), path(rank).c_str()) != 0) fail("cannot publish " + path(rank));
-  }
-  std::vector<std::string> all(static_cast<size_t>(world));
-  const double t0 = now_s();
-  for (int r = 0; r < world; ++r) {
-    for (;;) {
-      struct stat st {};
-      if (stat(path(r).c_str(), &st) == 0 && static_cast<double>(st.st_mtime) >= t_start - 60.0) {
-        std::ifstream f(path(r), std::ios::binary);
-        std::string b((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-        if (b.size() == mine.size()) {
-          all[static_cast<size_t>(r)] = b;
-          break;
-        }
-      }
-      if (now_s() - t0 > 120.0) fail("timed out waiting for " + path(r));  // (a peer that died)
-      std::this_thread::sleep_for(std::chrono::milliseconds(20));
-    }
-  }
-  return all;
-}
-
 int run_gpu(const Args& a) {
-  static const char* const kRank[] = {"RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID", nullptr};
-  static const char* const kSize[] = {"WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "SLURM_NTASKS", nullptr};
-  static const char* const kLocal[] = {"LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", nullptr};
-  int rank = env_int(kRank, 0), world = env_int(kSize, 1);
+  int rank = env_int(kRankEnv, 0), world = env_int(kSizeEnv, 1);
   const bool fake = a.fake_rank >= 0;
   if (fake) {
     rank = a.fake_rank;
     world = a.fake_world;
   }
-  const double t_proc0 = now_s();
+  const double t_proc0 = wall_s();
   int ndev = 0;
   W3D_HIP(hipGetDeviceCount(&ndev));
   W3D_REQUIRE(ndev > 0, "no GPU visible (use --cpu for the CPU path)");
-  const int local = env_int(kLocal, rank);
+  const int local = env_int(kLocalEnv, rank);
   const int dev = local % ndev;
   W3D_HIP(hipSetDevice(dev));
   hipDeviceProp_t prop;
@@ -724,7 +466,7 @@ int run_gpu(const Args& a) {
   if (a.group > 0) return run_group(a, base, prop);
 
   std::shared_ptr<Comm> comm;
-  const double t_comm0 = now_s();
+  const double t_comm0 = wall_s();
   if (world > 1 && !fake && !a.no_rccl) {
     W3D_REQUIRE(local < ndev || std::getenv("W3D_SHARE_GPUS"),
                 "rank " + std::to_string(rank) + " has local rank " + std::to_string(local) + " but only " +
@@ -733,147 +475,28 @@ int run_gpu(const Args& a) {
     comm = std::make_shared<Comm>(rank, world, id);
     if (rank == 0) std::remove(rdzv_path().c_str());
   }
-  const double t_comm = now_s() - t_comm0;
+  const double t_comm = wall_s() - t_comm0;
   const int rccl_nranks = comm ? comm->count() : 0;
   // fault injection: W3D_FAULT_RANK=r makes rank r fail right after the communicator is up; its peers
   // then fail in their next collective (GPU-wait timeout W3D_TIMEOUT_S) instead of hanging
   if (const char* fr = std::getenv("W3D_FAULT_RANK"); fr && std::atoi(fr) == rank) fail("injected fault");
-
-  // every rank takes the same branch: min over ranks of a 0/1 flag (RCCL all-reduce)
-  auto agree = [&](bool ok) {
-    return comm ? comm_allreduce(*comm, ok ? 1.0 : 0.0, false) == static_cast<double>(world) : ok;
-  };
-  // ranks without a communicator (--no-rccl push rehearsal): host collectives through files, outside timed regions
+  // host collectives: RCCL; files for ranks without a communicator (--no-rccl rehearsal, outside timed regions); none
+  // for one rank or a fake rank
   const bool file_coll = !comm && world > 1 && !fake;
-  int fcoll = 0;
-  std::vector<std::string> fcoll_files;
-  auto fgather = [&](const std::string& mine) {
-    const std::string tag = "c" + std::to_string(fcoll++) + "r";
-    fcoll_files.push_back(rdzv_path() + "." + tag + std::to_string(rank));
-    return file_allgather(rank, world, mine, tag);
-  };
-  auto max_over_ranks = [&](double v) {
-    if (comm) return comm_allreduce(*comm, v, true);
-    if (!file_coll) return v;
-    double m = v;
-    for (const std::string& b : fgather(std::string(reinterpret_cast<const char*>(&v), sizeof v))) {
-      double x = 0.0;
-      std::memcpy(&x, b.data(), sizeof x);
-      m = std::max(m, x);
-    }
-    return m;
-  };
-  auto barrier = [&]() {
-    if (comm)
-      comm_barrier(*comm);
-    else if (file_coll)
-      (void)fgather("b");
-  };
-
+  const HostColl hc = comm ? HostColl::rccl(comm) : file_coll ? HostColl::files(rank, world) : HostColl::single(rank);
   W3D_REQUIRE(!a.no_rccl || world == 1 || fake || ((a.transport == "push" || a.transport == "sdma") && !a.autotune),
               "--no-rccl: ranks without a communicator can only run the push or sdma transport (no autotune)");
-  // push transport: connect the slab neighbours (IPC handles through RCCL, or files without a communicator; a fake
-  // rank forwards into its own staging and waits for its own signals: the cost of the push without peers)
-  auto connect = [&](GpuSolver& g) {
-    if (g.sdma()) {
-      if (fake)
-        g.connect_sdma_self();
-      else
-        g.connect_sdma(comm ? comm_allgather_bytes(*comm, g.sdma_handles())
-                            : file_allgather(rank, world, g.sdma_handles(), "sdma"));
-      return;
-    }
-    if (!g.push()) return;
-    if (fake)
-      g.connect_push_self();
-    else
-      g.connect_push(comm ? comm_allgather_bytes(*comm, g.push_handles())
-                          : file_allgather(rank, world, g.push_handles()));
-  };
   std::unique_ptr<GpuSolver> s;
   std::string sched = a.decomp + "-S" + std::to_string(a.temporal) + (a.overlap ? "" : "-seq") +
                       (a.transport == "rccl" ? "" : "-" + a.transport);
-  std::vector<std::pair<std::string, double>> tuned;
+  AutotuneResult tuned;
   if (a.autotune && (world > 1 || a.fake_rank < 0)) {
-    double best_t = 1e30;
-    std::vector<double> ref_log;
-    for (const Candidate& c : kCandidates) {
-      if (std::string(c.decomp) == "block" && world < 4) continue;  // (2 ranks: "block" is the slab)
-      SolverOptions o = base;
-      o.decomp = c.decomp;
-      o.temporal = c.temporal;
-      o.overlap = c.overlap;
-      o.push = c.push;
-      if (c.push && world < 2) continue;
-      std::unique_ptr<GpuSolver> cand;
-      std::string err;
-      try {
-        cand = std::make_unique<GpuSolver>(a.prob, o, rank, world, comm);
-      } catch (const std::exception& e) {
-        err = e.what();
-      }
-      if (!agree(static_cast<bool>(cand))) {  // a schedule some rank cannot build: skipped everywhere
-        if (!err.empty()) std::fprintf(stderr, "[wave3d rank %d] candidate %s rejected: %s\n", rank, c.name, err.c_str());
-        continue;
-      }
-      // every schedule computes bit-identical fields: a candidate that fails (e.g. a push wait timed out) or whose
-      // error log differs from the first accepted one's (a transport that delivered wrong ghosts) is rejected on
-      // every rank, whatever its speed
-      // (collective when the candidate pushes: every rank built it). Agreed on its own: a rank whose IPC mapping
-      // failed must not reach the next agreement while its peers sit in the first solve's collectives
-      bool connected = false;
-      try {
-        connect(*cand);
-        connected = true;
-      } catch (const std::exception& e) {
-        err = e.what();
-      }
-      if (!agree(connected)) {
-        std::fprintf(stderr, "[wave3d rank %d] candidate %s rejected: %s\n", rank, c.name,
-                     err.empty() ? "a peer could not connect" : err.c_str());
-        continue;
-      }
-      bool same = false;
-      RunResult r0;
-      try {
-        r0 = cand->run();   // eager: RCCL peer connections
-        r0 = cand->run();   // graph capture
-        // (a fake rank's log holds its own partials only: they differ between decompositions, nothing to compare)
-        same = r0.finite && (fake || ref_log.empty() || r0.max_err == ref_log);
-        if (!same) err = "its error log differs from the reference schedule's";
-      } catch (const std::exception& e) {
-        err = e.what();
-      }
-      if (!agree(same)) {
-        std::fprintf(stderr, "[wave3d rank %d] candidate %s rejected: %s\n", rank, c.name,
-                     err.empty() ? "failed on another rank" : err.c_str());
-        continue;
-      }
-      if (ref_log.empty()) ref_log = r0.max_err;
-      double t = 1e30;
-      bool stable = true;  // the timed solves must reproduce the reference log too (an intermittent transport fault)
-      for (int k = 0; k < 3; ++k) {
-        if (comm) comm_barrier(*comm);
-        const RunResult rk = cand->run();
-        t = std::min(t, rk.solve_s);
-        stable = stable && rk.finite && (fake || rk.max_err == ref_log);
-      }
-      if (!agree(stable)) {
-        std::fprintf(stderr, "[wave3d rank %d] candidate %s rejected: a timed solve's error log differs\n", rank, c.name);
-        continue;
-      }
-      t = max_over_ranks(t);
-      tuned.emplace_back(c.name, t);
-      if (t < best_t) {
-        best_t = t;
-        s = std::move(cand);
-        sched = c.name;
-      }
-    }
-    W3D_REQUIRE(s != nullptr, "autotune: no candidate schedule could be built");
+    tuned = autotune(a.prob, base, rank, world, comm, hc, fake, a.transport == "push", a.autotune_rounds);
+    s = std::move(tuned.solver);
+    sched = tuned.name;
   } else {
     s = std::make_unique<GpuSolver>(a.prob, base, rank, world, comm);
-    connect(*s);
+    connect_transport(*s, hc, fake);
   }
 
   if (!a.resume.empty()) {
@@ -884,9 +507,9 @@ int run_gpu(const Args& a) {
   RunResult r;
   double best = 1e30, sum = 0, first = 0;
   for (int i = 0; i < a.warmup + a.repeat; ++i) {
-    barrier();
+    hc.barrier();
     r = s->run();
-    const double t = max_over_ranks(r.solve_s);
+    const double t = hc.max(r.solve_s);
     if (i == 0) first = t;
     if (i >= a.warmup) {
       best = std::min(best, t);
@@ -898,26 +521,26 @@ int run_gpu(const Args& a) {
   double bench_s = 0.0;
   if (a.bench_steps > 0) {
     W3D_HIP(hipDeviceSynchronize());
-    barrier();
-    const double t0 = now_s();
+    hc.barrier();
+    const double t0 = wall_s();
     for (int i = 0; i < a.bench_steps; ++i) r = s->run();
     W3D_HIP(hipDeviceSynchronize());
-    barrier();
-    bench_s = max_over_ranks(now_s() - t0);
+    hc.barrier();
+    bench_s = hc.max(wall_s() - t0);
   }
   // per-phase breakdown of the schedule that was timed: one more solve with the same kernels, traced with events
   PhaseTimes ph;
   if (a.phases && !a.timers) {
     s->set_timers(true);  // same solver, same schedule and kernels, launched eagerly with events around each phase
-    barrier();
+    hc.barrier();
     ph = s->run().phases;
     s->set_timers(false);
-    ph.init_ms = max_over_ranks(ph.init_ms);
-    ph.shell_ms = max_over_ranks(ph.shell_ms);
-    ph.interior_ms = max_over_ranks(ph.interior_ms);
-    ph.comm_ms = max_over_ranks(ph.comm_ms);
-    ph.check_ms = max_over_ranks(ph.check_ms);
-    ph.gather_ms = max_over_ranks(ph.gather_ms);
+    ph.init_ms = hc.max(ph.init_ms);
+    ph.shell_ms = hc.max(ph.shell_ms);
+    ph.interior_ms = hc.max(ph.interior_ms);
+    ph.comm_ms = hc.max(ph.comm_ms);
+    ph.check_ms = hc.max(ph.check_ms);
+    ph.gather_ms = hc.max(ph.gather_ms);
   }
   if (file_coll) {  // the last solve's error log over all ranks (L∞: max; RMS: from the per-rank Σe² shares)
     std::string mine;
@@ -925,7 +548,7 @@ int run_gpu(const Args& a) {
       const double v[2] = {r.max_err[i], r.rms_err[i] * r.rms_err[i]};
       mine.append(reinterpret_cast<const char*>(v), sizeof v);
     }
-    const std::vector<std::string> all = fgather(mine);
+    const std::vector<std::string> all = hc.allgather(mine);
     for (size_t i = 0; i < r.steps.size(); ++i) {
       double m = 0.0, q = 0.0;
       for (const std::string& b : all) {
@@ -939,7 +562,7 @@ int run_gpu(const Args& a) {
     }
   }
   const double mean = sum / a.repeat;
-  const double t_proc = now_s() - t_proc0;
+  const double t_proc = wall_s() - t_proc0;
   const Dims d = s->dims();
   int hipv = 0;
   (void)hipRuntimeGetVersion(&hipv);
@@ -983,7 +606,11 @@ int run_gpu(const Args& a) {
         << ", \"transport\": " << jstr(s->transport()) << ", \"device\": "
         << jstr(prop.gcnArchName) << ", \"bench_steps\": " << a.bench_steps << ", \"bench_s\": " << jnum(bench_s)
         << ", \"warmup\": " << a.warmup << ", \"finite\": " << (r.finite ? "true" : "false") << ", \"autotune_s\": {";
-      for (size_t i = 0; i < tuned.size(); ++i) j << (i ? ", " : "") << jstr(tuned[i].first) << ": " << jnum(tuned[i].second);
+      for (size_t i = 0; i < tuned.times.size(); ++i)
+        j << (i ? ", " : "") << jstr(tuned.times[i].first) << ": " << jnum(tuned.times[i].second);
+      j << "}, \"autotune_rounds\": " << tuned.rounds << ", \"autotune_rejected\": {";
+      for (size_t i = 0; i < tuned.rejected.size(); ++i)
+        j << (i ? ", " : "") << jstr(tuned.rejected[i].first) << ": " << jstr(json_escape(tuned.rejected[i].second));
       j << "}";
       if (a.timers || a.phases)
         j << ", \"phases_ms\": {\"init\": " << jnum(pp.init_ms) << ", \"compute\": "
@@ -1010,9 +637,7 @@ int run_gpu(const Args& a) {
     write_checkpoint(a.checkpoint, a.prob, s->layout(), s->download(0), s->download(1), rank, world, d);
   if ((s->push() || s->sdma()) && !comm && !fake)
     std::remove((rdzv_path() + (s->push() ? ".push" : ".sdma") + std::to_string(rank)).c_str());
-  // (a peer may still be reading this rank's file of the LAST collective: it stays; every earlier one has been read by
-  // everyone, since every peer has entered a later collective — removing a file a peer still needs hangs that peer)
-  for (size_t i = 0; i + 1 < fcoll_files.size(); ++i) std::remove(fcoll_files[i].c_str());
+  hc.cleanup();
   return r.finite ? 0 : 3;
 }
 
@@ -1037,7 +662,7 @@ int main(int argc, char** argv) {
     if (a.cpu && a.np > 1 && !std::getenv("W3D_SPAWNED"))
       group = std::make_unique<ShmGroup>(a.prob, parse_dims(a.decomp, a.np, a.prob.N), a.np);
     if (a.np > 1 && !std::getenv("W3D_SPAWNED")) {
-      const int rc = spawn(a.np, argv);
+      const int rc = spawn_ranks(a.np);  // (fork before anything touches the GPU)
       if (rc >= 0) return rc;  // parent
     }
     if (group) cpu_rank = env_int(kRankEnv, 0);

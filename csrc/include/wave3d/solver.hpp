@@ -225,8 +225,11 @@ class GpuSolver {
   void unit_shell(int i);
   void unit_exchange_rccl(int i);
   void unit_interior(int i);
-  void tb_pass(const Unit& u, const LBox& box, int phase);  // one k_leapfrog_tb launch of unit u over box
-  LBox tb_interior(int i) const;                            // deep-tb: the box left after unit i's shells
+  void tb_pass(const Unit& u, const LBox& box, int phase, hipStream_t st = nullptr);  // one k_leapfrog_tb launch
+  // deep-tb with overlap: unit i's shell boxes (what the neighbours receive, computed first) and the interior box
+  void tb_split(int i, std::vector<LBox>& shells, LBox& interior) const;
+  std::vector<LBox> tb_shells(int i) const;
+  LBox tb_interior(int i) const;
   // in-process group steps (GpuGroup): pack own faces → (group barrier) → pull peers' faces → (group barrier)
   void lb_pack(int i);
   void lb_pull(int i, const std::vector<GpuSolver*>& ranks, hipEvent_t all_packed);
@@ -281,6 +284,7 @@ class GpuSolver {
   // LDS passes: each unit's partials go to region tb_region_ of kTbRegions; their reductions are queued and issued as
   // one batched launch when the regions wrap and at the end of the solve (one launch instead of one per checked step)
   static constexpr int kTbRegions = 8;
+  static constexpr int kTbSlots = 8;  // launches with partials per level and unit (shell boxes + interior)
   Partial* tb_partials_ = nullptr;
   int tb_region_ = 0;
   std::vector<ReduceJob> pending_;
@@ -346,6 +350,11 @@ class GpuSolver {
   int xpar_ = 0;                   // parity of the solve being enqueued (flag values alternate between two sets)
   unsigned long long xsolves_ = 0; // solves enqueued so far (every rank runs the same number)
   hipGraphExec_t xgraph_[2] = {nullptr, nullptr};  // captured solves of either parity
+  // copy streams: link k's wait / copies / signal go to xcs_[k % size] (each stream gets its own SDMA engine, measured:
+  // 2 streams move 118 GB/s on one GPU where one moves 60), forked from the exchange stream and joined back
+  std::vector<hipStream_t> xcs_;
+  std::vector<hipEvent_t> xcev_;
+  hipEvent_t xfork_ = nullptr;
   unsigned xval(int i) const { return (xpar_ ? 0x10000u : 0u) + static_cast<unsigned>(i + 1); }
   unsigned xend(int par) const { return (par ? 0x10000u : 0u) + 0xFFFFu; }
   void sdma_alloc();

@@ -11,6 +11,7 @@
 #include "wave3d/decomp.hpp"
 #include "wave3d/kernels.hpp"
 #include "wave3d/problem.hpp"
+#include "wave3d/runtime.hpp"
 #include "wave3d/solver.hpp"
 
 namespace py = pybind11;
@@ -515,6 +516,29 @@ PYBIND11_MODULE(_C, m) {
       .def("device_bytes", &GpuSolver::device_bytes)
       .def_property_readonly("mode", &GpuSolver::mode)
       .def_property_readonly("graph_enabled", [](const GpuSolver& s) { return s.options().graph; });
+
+  // the CLI's multi-rank schedule autotune (runtime_autotune.cpp): same candidates, same rules; collectives over the
+  // RCCL communicator (world > 1) or none (one rank / a fake rank)
+  m.def(
+      "autotune",
+      [](const Problem& p, const SolverOptions& o, int rank, int world, std::shared_ptr<Comm> c, bool fake,
+         bool with_push, int rounds, double tie) {
+        W3D_REQUIRE(world == 1 || fake || c, "autotune: world > 1 needs an RCCL communicator");
+        const HostColl hc = c ? HostColl::rccl(c) : HostColl::single(rank);
+        AutotuneResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = autotune(p, o, rank, world, c, hc, fake, with_push, rounds, tie);
+        }
+        py::dict times, rejected;
+        for (const auto& [k, v] : r.times) times[py::str(k)] = v;
+        for (const auto& [k, v] : r.rejected) rejected[py::str(k)] = v;
+        return py::make_tuple(py::cast(std::move(r.solver)), r.name, times, rejected);
+      },
+      py::arg("problem"), py::arg("options"), py::arg("rank") = 0, py::arg("world") = 1, py::arg("comm") = nullptr,
+      py::arg("fake") = false, py::arg("with_push") = false, py::arg("rounds") = 5, py::arg("tie") = 0.02,
+      "time the schedule candidates (slab/block, pass depth, overlap, RCCL/copy engines) and return "
+      "(GpuSolver, name, {name: seconds}, {name: reason rejected})");
 
   py::class_<GpuGroup>(m, "GpuGroup")
       .def(py::init([](const Problem& p, const SolverOptions& o, int world, const std::string& transport) {

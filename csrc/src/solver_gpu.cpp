@@ -330,7 +330,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   // the LDS passes' partials live apart: their reductions are deferred, so the immediate users of partials_ (init,
   // single steps between passes) must not overwrite them
   if (n_tb_ > 0)
-    W3D_HIP(hipMalloc(&tb_partials_, static_cast<size_t>(kTbRegions) * 4 * 3 * n_tb_ * sizeof(Partial)));
+    W3D_HIP(hipMalloc(&tb_partials_, static_cast<size_t>(kTbRegions) * 4 * kTbSlots * n_tb_ * sizeof(Partial)));
   W3D_HIP(hipMalloc(&errlog_, static_cast<size_t>(prob_.K + 1) * sizeof(Partial)));
   W3D_HIP(hipMalloc(&errall_, static_cast<size_t>(world_) * (prob_.K + 1) * sizeof(Partial)));
   ct_.resize(static_cast<size_t>(prob_.K + 1));
@@ -351,6 +351,9 @@ GpuSolver::~GpuSolver() {
       if (l.flags) (void)hipIpcCloseMemHandle(l.flags);
     }
   if (xflags_) (void)hipFree(xflags_);
+  for (hipStream_t c : xcs_) (void)hipStreamDestroy(c);
+  for (hipEvent_t e : xcev_) (void)hipEventDestroy(e);
+  if (xfork_) (void)hipEventDestroy(xfork_);
   for (BoxCopyTable& t : pack_tab_) free_box_copy_table(t);
   for (BoxCopyTable& t : unpack_tab_) free_box_copy_table(t);
   for (double* p : {u_[0], u_[1], u_[2], u_[3], d_s_, send_buf_, recv_buf_})
@@ -380,7 +383,7 @@ size_t GpuSolver::device_bytes() const {
   return static_cast<size_t>(nbuf_) * static_cast<size_t>(lay_.bytes()) +
          2 * static_cast<size_t>(imax(plan_.packed_doubles, deep_max_)) * sizeof(double) +
          static_cast<size_t>(n_partials_) * sizeof(Partial) + static_cast<size_t>(prob_.N + 3) * sizeof(double) +
-         static_cast<size_t>(kTbRegions) * 4 * 3 * static_cast<size_t>(n_tb_) * sizeof(Partial);
+         static_cast<size_t>(kTbRegions) * 4 * kTbSlots * static_cast<size_t>(n_tb_) * sizeof(Partial);
 }
 
 void GpuSolver::set_state(const double* prev, const double* cur, int n0) {
@@ -428,7 +431,7 @@ bool GpuSolver::post_exchange() const { return mode_ == Mode::kDeep || mode_ == 
 
 // (3-D block passes always exchange after the whole pass: the y/z face shells of S-deep halos would be thin tile
 // strips recomputing most of their tiles)
-bool GpuSolver::late_exchange() const { return mode_ == Mode::kDeepTb && (!opt_.overlap || block_tb_); }
+bool GpuSolver::late_exchange() const { return mode_ == Mode::kDeepTb && !opt_.overlap; }
 
 bool GpuSolver::needs_exchange(int i) const {
   if (!plan_.any() || push_) return false;  // (push: the passes deliver the ghosts themselves)
@@ -645,14 +648,17 @@ void GpuSolver::unit_shell(int i) {
       off += n_dshell_[k];
     }
   } else if (mode_ == Mode::kDeepTb) {
-    // the planes the neighbours receive first: as many as the next pass is deep, next to each neighbour face
+    // the regions the neighbours receive (tb_shells) first, on the side stream, CONCURRENTLY with the interior pass
+    // that unit_interior launches on s0 (same inputs, disjoint outputs): the shells' partial last waves leave CUs the
+    // interior fills, and the exchange follows the shells on the same side stream (no wait between sibling streams)
     tb_slots_ = 0;
     if (needs_exchange(i) && !late_exchange()) {
-      const i64 w = units_[static_cast<size_t>(i) + 1].steps;
-      if (nb_lo_) tb_pass(u, LBox{full_.x0, imin(full_.x0 + w, full_.x1), full_.y0, full_.y1, full_.z0, full_.z1},
-                          kPhaseShell);
-      if (nb_hi_) tb_pass(u, LBox{imax(full_.x1 - w, full_.x0), full_.x1, full_.y0, full_.y1, full_.z0, full_.z1},
-                          kPhaseShell);
+      build_msgs(i);
+      hipStream_t xs = xstream();
+      W3D_HIP(hipEventRecord(ev_shell_, s0_));  // (the unit's inputs are ready: fork)
+      W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
+      for (const LBox& b : tb_shells(i)) tb_pass(u, b, kPhaseShell, xs);
+      return;
     }
   } else if (mode_ == Mode::kSingleStep && split()) {
     timed(kPhaseShell, s0_, [&] {
@@ -715,15 +721,18 @@ void GpuSolver::exchange(hipStream_t st, const std::vector<GpuSolver*>* pull) {
 void GpuSolver::unit_exchange_rccl(int i) {
   if (!needs_exchange(i)) return;
   hipStream_t xs = xstream();
-  if (xs != s0_) W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
+  // (deep-tb: the shells ran on xs itself, after its wait for the unit's inputs)
+  if (xs != s0_ && mode_ != Mode::kDeepTb) W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
   if (opt_.poison_ghosts) poison(xs);
   timed(kPhaseComm, xs, [&] { exchange(xs); });
   if (xs != s0_) W3D_HIP(hipEventRecord(ev_halo_, xs));
 }
 
-// One LDS S-step pass of unit u over `box`. Its checked levels' partials go to slot tb_slots_ of each level: one slot
-// per level on one rank, three on slab ranks (shell lo, shell hi, interior), reduced together after the interior.
-void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase) {
+// One LDS S-step pass of unit u over `box` on stream st (s0 unless given). Its checked levels' partials go to slot
+// tb_slots_ of each level: one slot per level on one rank, up to kTbSlots on multi-rank ranks (the shell boxes, then
+// the interior), reduced together after the interior.
+void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase, hipStream_t st) {
+  if (st == nullptr) st = s0_;
   LeapfrogTbTiling t = opt_.tiling_tb;
   t.stages = u.steps;
   double cts[4] = {0, 0, 0, 0};
@@ -732,7 +741,7 @@ void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase) {
     cts[k - 1] = ct_[static_cast<size_t>(u.n + k)];
     if (is_check_[static_cast<size_t>(u.n + k)]) mask |= 1 << (k - 1);
   }
-  const int slots = mode_ == Mode::kDeepTb ? 3 : 1;
+  const int slots = mode_ == Mode::kDeepTb ? kTbSlots : 1;
   W3D_REQUIRE(tb_slots_ < slots, "leapfrog_tb: too many launches in one unit");
   Partial* part = mask ? tb_partials_ + tb_region_ * (4 * slots * n_tb_) + tb_slots_ * n_tb_ : nullptr;
   const LBox real = mode_ == Mode::kDeepTb ? sreal_ : tb_default_real();
@@ -749,22 +758,77 @@ void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase) {
         if (qh->wait_side[side] && qh->cp_wait > 0)
           W3D_HIP(hipStreamWaitValue32(s0_, flags_ + side, qh->cp_wait, hipStreamWaitValueGte, 0xFFFFFFFFu));
   }
-  timed(phase, s0_, [&] {
+  timed(phase, st, [&] {
     // (every launch fills its whole slot of n_tb_ partials: shell and interior boxes may have fewer x chunks)
     launch_leapfrog_tb(lay_, coef_, u_[old_], u_[cur_], u_[uf_[0]], u_[uf_[1]], box, d_s_ + 1, cts, mask, part, t,
-                       s0_, real, u.analytic, slots * n_tb_, n_tb_, qh, qd);
+                       st, real, u.analytic, slots * n_tb_, n_tb_, qh, qd);
   });
   if (mask) ++tb_slots_;
 }
 
-LBox GpuSolver::tb_interior(int i) const {
-  LBox b = full_;
-  if (needs_exchange(i) && !late_exchange()) {
-    const i64 w = units_[static_cast<size_t>(i) + 1].steps;
-    if (nb_lo_) b.x0 = imin(b.x0 + w, b.x1);
-    if (nb_hi_) b.x1 = imax(b.x1 - w, b.x0);
+// The shell / interior split of a deep-tb unit whose exchange overlaps the next part of the pass. The neighbours need
+// the w = (next pass depth) nodes next to each face with a neighbour (edges and corners included). In y and z the
+// shell is made of whole rows / columns of the pass's 32 × 32 tile grid (w ≤ 32), so the shell boxes recompute nothing
+// the interior also computes (a remainder row narrower than w: the w rows themselves); in x it is w planes of the
+// remaining (y, z) core (recomputing S − 1 planes at the seam).
+// Boxes: the y border rows (whole x, whole z), the z border columns of the rows between (whole x), then the core's
+// x-face slabs; the interior is the core between the x slabs. Slab ranks: just the two x slabs.
+void GpuSolver::tb_split(int i, std::vector<LBox>& shells, LBox& interior) const {
+  shells.clear();
+  interior = full_;
+  if (!needs_exchange(i) || late_exchange()) return;
+  const i64 w = units_[static_cast<size_t>(i) + 1].steps, T = 32;
+  const LBox f = full_;
+  bool nb[3][2];
+  for (int a = 0; a < 3; ++a)
+    for (int sd = 0; sd < 2; ++sd) nb[a][sd] = neighbor_rank(dims_, rank_, a, sd) >= 0;
+  // core range along a tiled axis: the border is the first / last tile row of the box, or — when the last row is a
+  // remainder narrower than w — exactly the w rows next to the face (its own one-row box; the core then ends a row
+  // earlier, so the total tile rows stay the same)
+  auto grid = [&](i64 b0, i64 b1, bool lo, bool hi, i64& c0, i64& c1) {
+    const i64 nt = ceil_div(b1 - b0, T), rem = (b1 - b0) - (nt - 1) * T;
+    c0 = lo ? imin(b0 + T, b1) : b0;
+    c1 = hi ? imax(rem >= w ? b0 + (nt - 1) * T : b1 - w, c0) : b1;
+  };
+  i64 ya, yb, za, zb;
+  grid(f.y0, f.y1, nb[1][0], nb[1][1], ya, yb);
+  grid(f.z0, f.z1, nb[2][0], nb[2][1], za, zb);
+  auto add = [&](const LBox& b) {
+    if (!b.empty()) shells.push_back(b);
+  };
+  add(LBox{f.x0, f.x1, f.y0, ya, f.z0, f.z1});
+  add(LBox{f.x0, f.x1, yb, f.y1, f.z0, f.z1});
+  add(LBox{f.x0, f.x1, ya, yb, f.z0, za});
+  add(LBox{f.x0, f.x1, ya, yb, zb, f.z1});
+  interior = LBox{f.x0, f.x1, ya, yb, za, zb};
+  if (interior.empty()) {
+    interior = LBox{};
+    return;
   }
-  return b;
+  if (nb[0][0]) {
+    add(LBox{f.x0, imin(f.x0 + w, f.x1), ya, yb, za, zb});
+    interior.x0 = imin(f.x0 + w, f.x1);
+  }
+  if (nb[0][1]) {
+    const i64 x = imax(f.x1 - w, interior.x0);
+    add(LBox{x, f.x1, ya, yb, za, zb});
+    interior.x1 = x;
+  }
+  W3D_REQUIRE(static_cast<int>(shells.size()) < kTbSlots, "deep-tb: too many shell boxes");
+}
+
+std::vector<LBox> GpuSolver::tb_shells(int i) const {
+  std::vector<LBox> s;
+  LBox in;
+  tb_split(i, s, in);
+  return s;
+}
+
+LBox GpuSolver::tb_interior(int i) const {
+  std::vector<LBox> s;
+  LBox in;
+  tb_split(i, s, in);
+  return in;
 }
 
 void GpuSolver::unit_interior(int i) {
@@ -777,6 +841,7 @@ void GpuSolver::unit_interior(int i) {
   // the own side stream after that fence crashes HIP 7.2's hipStreamEndCapture — tools/capture_probe2.hip flag 36)
   const bool wait = needs_exchange(i) && xstream() != s0_ && (!loopback_ || sdma_);
   int np = 0;  // partials to reduce
+  bool joined = false;
   if (mode_ == Mode::kDeep) {
     int off = 0;
     for (int n : n_dshell_) off += n;
@@ -793,7 +858,12 @@ void GpuSolver::unit_interior(int i) {
     if (mode_ != Mode::kDeepTb) tb_slots_ = 0;
     const LBox b = mode_ == Mode::kDeepTb ? tb_interior(i) : full_;
     if (!b.empty()) tb_pass(u, b, kPhaseCompute);
-    const int slots = mode_ == Mode::kDeepTb ? 3 : 1;
+    // (the shells ran on the side stream: join it before the reductions read their partials)
+    if (wait) {
+      W3D_HIP(hipStreamWaitEvent(s0_, ev_halo_, 0));
+      joined = true;
+    }
+    const int slots = mode_ == Mode::kDeepTb ? kTbSlots : 1;
     if (tb_slots_ > 0) {
       Partial* region = tb_partials_ + tb_region_ * (4 * slots * n_tb_);
       for (int k = 1; k <= u.steps; ++k)
@@ -825,7 +895,7 @@ void GpuSolver::unit_interior(int i) {
     });
     np = n_full_;
   }
-  if (wait) W3D_HIP(hipStreamWaitEvent(s0_, ev_halo_, 0));
+  if (wait && !joined) W3D_HIP(hipStreamWaitEvent(s0_, ev_halo_, 0));
   if (chk && np > 0) timed(kPhaseCheck, s0_, [&] { launch_reduce(partials_, np, errlog_ + nc, s0_); });
   if (opt_.debug_sync) W3D_HIP(hipDeviceSynchronize());
   if (u.fused()) {
@@ -909,7 +979,7 @@ void GpuSolver::collect_phases(RunResult& r) {
 void GpuSolver::lb_pack(int i) {
   if (!needs_exchange(i)) return;
   hipStream_t xs = xstream();
-  if (xs != s0_) W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
+  if (xs != s0_ && mode_ != Mode::kDeepTb) W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
   pack_halo(xs);
   W3D_HIP(hipEventRecord(ev_packed_, xs));
 }

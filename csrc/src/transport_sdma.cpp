@@ -105,6 +105,19 @@ void GpuSolver::sdma_alloc() {
   std::vector<unsigned> init(2 * n, 0u);
   for (size_t k = 0; k < n; ++k) init[2 * k + 1] = xend(1);
   W3D_HIP(hipMemcpy(xflags_, init.data(), init.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+  // copy streams (W3D_SDMA_STREAMS, default 4; at most one per link)
+  int ns = 4;
+  if (const char* v = std::getenv("W3D_SDMA_STREAMS")) ns = std::max(1, std::atoi(v));
+  ns = std::min<int>(ns, static_cast<int>(std::max<size_t>(1, xlinks_.size())));
+  int lo = 0, hi = 0;
+  W3D_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  xcs_.resize(static_cast<size_t>(ns));
+  xcev_.resize(static_cast<size_t>(ns));
+  for (int c = 0; c < ns; ++c) {
+    W3D_HIP(hipStreamCreateWithPriority(&xcs_[static_cast<size_t>(c)], hipStreamNonBlocking, hi));
+    W3D_HIP(hipEventCreateWithFlags(&xcev_[static_cast<size_t>(c)], hipEventDisableTiming));
+  }
+  W3D_HIP(hipEventCreateWithFlags(&xfork_, hipEventDisableTiming));
 }
 
 std::string GpuSolver::sdma_handles() const {
@@ -201,43 +214,50 @@ unsigned long long flag_ticks() {
 // Exchange i: on the side stream once the shells are written (overlap), else on s0 after the pass.
 void GpuSolver::unit_exchange_sdma(int i) {
   if (!needs_exchange(i)) return;
-  hipStream_t xs = xstream();
-  if (xs != s0_) W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
+  hipStream_t xs = xstream();  // (overlap: the shells already ran on xs, after its wait for the unit's inputs)
   timed(kPhaseComm, xs, [&] {
     const int s = units_[static_cast<size_t>(i) + 1].steps;
     if (block_tb_) pack_halo(xs);  // (build_msgs set deep_s_ = s)
-    // the receivers have finished with the regions these copies overwrite
-    FlagOp w, none;
-    w.value = i == 0 ? xend(1 - xpar_) : xval(i - 1);
-    w.status = reinterpret_cast<unsigned*>(errlog_);
-    w.ticks = flag_ticks();
-    for (size_t k = 0; k < xlinks_.size(); ++k) w.addr[w.n++] = xflags_ + 2 * k + 1;
-    launch_flag_sync(w, none, xs);
-    const size_t P = static_cast<size_t>(lay_.plane);
-    for (size_t k = 0; k < xlinks_.size(); ++k) {
-      const XLink& l = xlinks_[k];
-      if (block_tb_) {
-        const DeepPeer& q = deep_[s].peers[k];
-        W3D_HIP(hipMemcpyAsync(l.recv + l.recv_off[s], send_buf_ + q.buf_off, static_cast<size_t>(q.count) * sizeof(double),
-                               hipMemcpyDeviceToDeviceNoCU, xs));
-      } else {
-        // u^{n+S} s planes deep and u^{n+S−1} s − 1 deep: this rank's planes next to the face → the peer's ghost planes
-        // beyond its facing side (the peer's plane p sits at (p + xg)·plane in its buffers, same geometry)
-        for (int f = 0; f < 2; ++f) {
-          const i64 d = f == 0 ? s : s - 1;
-          const int b = uf_[f == 0 ? 1 : 0];
-          const i64 src = l.side == 0 ? 0 : lay_.nx - d;
-          const i64 dst = l.side == 0 ? l.peer_nx : -d;
-          W3D_HIP(hipMemcpyAsync(l.u[b] + (dst + lay_.xg) * static_cast<i64>(P), u_[b] + lay_.plane_off(src),
-                                 static_cast<size_t>(d) * P * sizeof(double), hipMemcpyDeviceToDeviceNoCU, xs));
+    // per copy stream: wait until its links' receivers have finished with the regions the copies overwrite, copy,
+    // then raise the links' "arrived" words (stream order: after the copies have completed)
+    W3D_HIP(hipEventRecord(xfork_, xs));
+    const size_t P = static_cast<size_t>(lay_.plane), nc = xcs_.size();
+    for (size_t c = 0; c < nc; ++c) {
+      hipStream_t cs = xcs_[c];
+      W3D_HIP(hipStreamWaitEvent(cs, xfork_, 0));
+      FlagOp w, sig, none;
+      w.value = i == 0 ? xend(1 - xpar_) : xval(i - 1);
+      w.status = reinterpret_cast<unsigned*>(errlog_);
+      w.ticks = flag_ticks();
+      sig.value = xval(i);
+      for (size_t k = c; k < xlinks_.size(); k += nc) {
+        w.addr[w.n++] = xflags_ + 2 * k + 1;
+        sig.addr[sig.n++] = xsig(xlinks_[k], 0);
+      }
+      launch_flag_sync(w, none, cs);
+      for (size_t k = c; k < xlinks_.size(); k += nc) {
+        const XLink& l = xlinks_[k];
+        if (block_tb_) {
+          const DeepPeer& q = deep_[s].peers[k];
+          W3D_HIP(hipMemcpyAsync(l.recv + l.recv_off[s], send_buf_ + q.buf_off,
+                                 static_cast<size_t>(q.count) * sizeof(double), hipMemcpyDeviceToDeviceNoCU, cs));
+        } else {
+          // u^{n+S} s planes deep and u^{n+S−1} s − 1 deep: this rank's planes next to the face → the peer's ghost
+          // planes beyond its facing side (the peer's plane p sits at (p + xg)·plane in its buffers, same geometry)
+          for (int f = 0; f < 2; ++f) {
+            const i64 d = f == 0 ? s : s - 1;
+            const int b = uf_[f == 0 ? 1 : 0];
+            const i64 src = l.side == 0 ? 0 : lay_.nx - d;
+            const i64 dst = l.side == 0 ? l.peer_nx : -d;
+            W3D_HIP(hipMemcpyAsync(l.u[b] + (dst + lay_.xg) * static_cast<i64>(P), u_[b] + lay_.plane_off(src),
+                                   static_cast<size_t>(d) * P * sizeof(double), hipMemcpyDeviceToDeviceNoCU, cs));
+          }
         }
       }
+      launch_flag_sync(none, sig, cs);
+      W3D_HIP(hipEventRecord(xcev_[c], cs));
+      W3D_HIP(hipStreamWaitEvent(xs, xcev_[c], 0));
     }
-    // stream order puts this after the copies have completed: the peers may read what they delivered
-    FlagOp sig;
-    sig.value = xval(i);
-    for (const XLink& l : xlinks_) sig.addr[sig.n++] = xsig(l, 0);
-    launch_flag_sync(none, sig, xs);
   });
   if (xs != s0_) W3D_HIP(hipEventRecord(ev_halo_, xs));
 }

@@ -89,7 +89,8 @@ class Solver:
                  tiling2: dict | None = None, init2: bool = True, timers: bool = False, tb: bool = True,
                  tiling_tb: dict | None = None,
                  debug_sync: bool = False, poison_ghosts: bool = False, deep_min_planes: int | None = None,
-                 tb_min_planes: int | None = None, rccl: bool = True):
+                 tb_min_planes: int | None = None, rccl: bool = True, autotune: bool = False,
+                 autotune_rounds: int = 5):
         import torch.distributed as dist
 
         if not spec.cfl_ok and not force:
@@ -140,7 +141,16 @@ class Solver:
             if comm is None and world > 1 and (rccl or not (opts.push or opts.sdma)):
                 comm = make_comm(rank, world, group)
             self.comm = comm
-            self._impl = C.GpuSolver(spec.native(), opts, rank, world, comm)
+            self.schedule, self.autotune_times, self.autotune_rejected = None, {}, {}
+            if autotune:
+                # the CLI's autotune (csrc/src/runtime_autotune.cpp): every candidate built, checked against the first
+                # accepted one's error log, timed in interleaved rounds; the slowest rank decides
+                if self.transport != "rccl":
+                    raise ValueError("autotune picks the transport itself: use transport='rccl' (the default)")
+                self._impl, self.schedule, self.autotune_times, self.autotune_rejected = C.autotune(
+                    spec.native(), opts, rank, world, comm, rounds=autotune_rounds)
+            else:
+                self._impl = C.GpuSolver(spec.native(), opts, rank, world, comm)
             if self._impl.push and world > 1:  # every rank's IPC handles, over torch.distributed (gloo)
                 import torch.distributed as tdist
 

@@ -259,3 +259,23 @@ def test_block_deep_tb_bitexact(gpu, world, decomp, overlap, K, check_every, tem
         _same(r, r1)
         assert torch.equal(g.global_field(0), f0)
         assert torch.equal(g.global_field(1), f1)
+
+
+@pytest.mark.parametrize("transport", ["loopback", "rccl-self", "sdma"])
+@pytest.mark.parametrize("world,decomp,N", [(27, "3x3x3", 100), (9, "1x3x3", 100), (27, "3x3x3", 140),
+                                            (8, "2x2x2", 70), (12, "3x2x2", 100)])
+def test_block_overlap_geometries(gpu, world, decomp, N, transport):
+    """Block ranks with overlap compute the regions their neighbours receive first (border tile rows/columns, the
+    core's x-face slabs) on the side stream while the core runs on s0. Box sizes whose last tile row is a remainder
+    narrower than the halo (N=100 over 3: 33 nodes = 32 + 1) put the border on the w rows next to the face instead."""
+    spec = ProblemSpec(N=N, tau=1e-3, K=20)
+    ref = Solver(spec, backend="hip", device=0, temporal=1)
+    r1 = ref.run()
+    f0 = ref.global_field(0)
+    g = Solver(spec, backend="hip", transport=transport, world=world, rank=0, decomp=decomp, device=0,
+               overlap=True, poison_ghosts=transport != "rccl-self")
+    assert g.native.mode() == "deep-tb-block"
+    for _ in range(2):
+        r = g.run()
+        _same(r, r1)
+        assert torch.equal(g.global_field(0), f0)

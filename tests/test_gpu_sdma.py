@@ -62,13 +62,17 @@ def test_sdma_group_slab_bitexact(gpu, world, overlap, K, check_every, temporal)
         assert torch.equal(g.global_field(1), f1)
 
 
-@pytest.mark.parametrize("world,decomp", [(4, "2x2x1"), (8, "2x2x2"), (4, "1x2x2"), (6, "3x2x1")])
+@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("world,decomp", [(4, "2x2x1"), (8, "2x2x2"), (4, "1x2x2"), (6, "3x2x1"), (27, "3x3x3")])
 @pytest.mark.parametrize("K,check_every,temporal", [(20, 2, 4), (9, 1, 4), (11, 2, 2)])
-def test_sdma_group_block_bitexact(gpu, world, decomp, K, check_every, temporal):
-    spec = ProblemSpec(N=66, tau=1e-3, K=K, check_every=check_every)
+def test_sdma_group_block_bitexact(gpu, world, decomp, overlap, K, check_every, temporal):
+    """Block ranks: with overlap the border tile rows/columns and the core's x-face slabs are computed first on the
+    side stream, concurrently with the interior, then packed and copied from there (3x3x3: a rank with all 26
+    neighbours)."""
+    spec = ProblemSpec(N=66 if world < 27 else 100, tau=1e-3, K=K, check_every=check_every)
     r1, f0, f1 = _ref(spec)
     g = Solver(spec, backend="hip", transport="sdma", world=world, rank=0, decomp=decomp, device=0,
-               poison_ghosts=True, temporal=temporal)
+               poison_ghosts=True, temporal=temporal, overlap=overlap)
     assert g.native.mode() == "deep-tb-block"
     for _ in range(3):
         r = g.run()
@@ -93,7 +97,7 @@ def test_sdma_fake_rank_graph(gpu, tmp_path, decomp, rank):
     meta = json.loads(open(js).read())
     assert meta["transport"] == "sdma" and meta["mode"].startswith("deep-tb") and meta["finite"]
     assert meta["graph"] is True
-    assert meta["overlap"] is (decomp == "slab")  # block ranks exchange after the whole pass
+    assert meta["overlap"] is True  # (slab: x-face slabs first; blocks: border tiles + x-face slabs first)
 
 
 def _assert_same_field(f, ref):

@@ -48,6 +48,9 @@ LIB_SOURCES = [
     ("src/kernels_leapfrog_tb_push.hip", "hip"),
     ("src/solver_gpu.cpp", "hip"),
     ("src/transport_sdma.cpp", "hip"),
+    ("src/runtime_launch.cpp", "hip"),
+    ("src/runtime_io.cpp", "hip"),
+    ("src/runtime_autotune.cpp", "hip"),
     ("src/cpu_kernels.cpp", "cpu"),
     ("src/cpu_solver.cpp", "cpu"),
     ("src/cpu_dist.cpp", "cpu"),

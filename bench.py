@@ -16,7 +16,7 @@ candidate solves are untimed too), then EXACTLY K solves between a device sync +
 the interval as the max over ranks. This process only orchestrates (torch.distributed over gloo: nonce broadcast and
 the agreement on success); it never touches the GPU. The child runs on the system ROCm (HIP 7.2 + RCCL 2.27), whose
 stream capture of the multi-rank schedules is verified; the HIP 7.0 runtime bundled with PyTorch crashes in
-hipStreamEndCapture on those graphs (tools/capture_probe*.hip, csrc/src/solver_gpu.cpp multistream_capture_safe).
+hipStreamEndCapture on those graphs (tools/probes/capture_probe*.hip, csrc/src/solver_gpu.cpp multistream_capture_safe).
 
 Rank 0 prints ONE JSON line. ``value`` = whole-job GCell-updates/s = N³·K / t_solve (reference convention) with
 t_solve = (max over ranks of the K-solve interval) / K; ``ms_per_step`` = ``ms_per_solve`` = t_solve in ms (one bench

@@ -75,6 +75,7 @@ void launch_leapfrog2(const Layout& l, const Coeffs& c, const double* prev, cons
 // Error check of u^{n+k} when bit k−1 of `check_mask` is set (ct[k−1] = its time factor); stage k's partials go to
 // partials + (k−1)·level_stride (0: leapfrog_tb_partials(), the launch's block count). analytic_start: the pass starts at n = 1 from u⁰ = φ and u¹ computed in
 // the kernel (init_first's formulas, bit-identical), prev/cur are not read: it writes u^S, u^{S+1} with no HBM reads.
+constexpr int kTbTile = 32;  // (y, z) tile edge of the LDS S-step passes (leapfrog_tb_kernel.hpp tbk::kTile)
 struct LeapfrogTbTiling {
   int stages = 4;         // 2, 3 or 4 steps per pass
   int threads = 1024;     // workgroup size (768 or 1024)

@@ -15,7 +15,7 @@
 namespace wave3d {
 namespace tbk {
 
-constexpr int kTile = 32;  // tile edge (y and z)
+constexpr int kTile = kTbTile;  // tile edge (y and z)
 
 // Global-address-space views of pointers the kernel reads from memory (the push transport's staging pointers): a
 // generic pointer would turn every load and store through it into a FLAT instruction (and, merged with the field
@@ -61,6 +61,7 @@ struct TbParams {
   double ct[4];        // time factor of u^{n+k} (k = 1..S) for the check
   int check_mask;      // bit k−1: check u^{n+k}
   int nty, ntz, nblocks, xcd_remap;
+  int xper;            // xcd_remap: blocks per XCD, ceil(active blocks / 8) (a padded grid's extra blocks get none)
   int lstride;         // partials between consecutive levels (≥ nblocks; larger when several launches share a level)
   int bby, bbz;        // > 0: each XCD's tiles form a bby × bbz block of the tile grid (else two-row strips)
   // slab peer-push transport (PUSH instantiations only): the per-pass parameters stay in device memory and are read
@@ -72,7 +73,8 @@ struct TbParams {
   int pacq;            // push: acquire at the pass start (TbPush::acquire)
 };
 
-// Push transport memory protocol. The staging and the flags are uncached device memory (hipDeviceMallocUncached); the
+// Push transport memory protocol. The staging is fine-grained device memory (hipDeviceMallocFinegrained; W3D_PUSH_STAGING=
+// uncached: uncached), the flags uncached (hipDeviceMallocUncached); the
 // forwarded face values are stored with system-scope (write-through) stores and every flag / counter access is a
 // system-scope atomic, so the WRITER needs no cache writeback: a workgroup's forwarded stores are all acknowledged
 // (s_waitcnt before its barrier) before it counts itself done, and the workgroup that completes the count raises the
@@ -174,7 +176,10 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
   extern __shared__ double lds[];
   const int tid = static_cast<int>(threadIdx.x);
   int blk = static_cast<int>(blockIdx.x);
-  if (p.xcd_remap) blk = (blk & 7) * (p.nblocks >> 3) + (blk >> 3);
+  if (p.xcd_remap) {  // XCD k (= blockIdx % 8 in dispatch order) takes the k-th contiguous range of xper blocks
+    const int j = blk >> 3;
+    blk = j < p.xper ? (blk & 7) * p.xper + j : (1 << 30);
+  }
   const int ntiles = p.nty * p.ntz;
   const bool active = blk < ntiles * (CH ? p.nxc : 1);
   // chunk-major: consecutive blocks (one XCD after the remap) are neighbouring tiles of one x chunk
@@ -766,6 +771,7 @@ inline TbPlan make_plan_tb(const Layout& l, const LBox& b, const LeapfrogTbTilin
   pl.nblocks = t.xcd_remap ? static_cast<int>(round_up(blocks, 8)) : blocks;
   p.nblocks = pl.nblocks;
   p.xcd_remap = t.xcd_remap ? 1 : 0;
+  p.xper = pl.nblocks / 8;
   // blocked XCD ownership when the tile grid splits into 8 equal blocks (one per XCD), the squarest such block
   p.bby = p.bbz = 0;
   if (t.xcd_remap && t.xcd_blocks && p.nxc == 1 && tiles == pl.nblocks && tiles % 8 == 0) {

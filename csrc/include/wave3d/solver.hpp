@@ -70,6 +70,11 @@ struct SolverOptions {
   // waited for by the command processors (hipStreamWriteValue32 / hipStreamWaitValue32, graph-capturable on HIP 7.2).
   // See transport_sdma.cpp for the protocol.
   bool sdma = false;
+  // deep-tb with overlap: the shell boxes run on the side stream concurrently with the interior (1), or on s0 before it
+  // (0: they get the whole GPU and finish first, so the exchange starts earlier); -1: per decomposition — concurrent for
+  // 3-D blocks (their up to 6 small shell launches leave most CUs idle when alone: 512³ 2x2x2 rank 1.20 vs 1.38 ms),
+  // serial for slabs (2 shell launches; the copy-engine exchange starts earlier: 512³ rank 1/8 1.65 vs 2.10 ms)
+  int shells_concurrent = -1;
   bool push_cp_wait = false;
   // push ranks without an end-of-solve collective (no RCCL communicator): the flag epochs run on over the solves
   // instead of being reset (eager launches: every launch carries its own epochs)
@@ -105,6 +110,9 @@ class Comm {
   // 128-byte ncclUniqueId as raw bytes (call on rank 0, ship to the others).
   static std::string make_unique_id();
   Comm(int rank, int world, const std::string& unique_id);
+  // every visible device's rank of one communicator, created in this process (ncclCommInitAll over devices
+  // 0..world−1): the single-process multi-GPU mode
+  static std::vector<std::shared_ptr<Comm>> init_all(int world);
   ~Comm();
   Comm(const Comm&) = delete;
   Comm& operator=(const Comm&) = delete;
@@ -119,6 +127,7 @@ class Comm {
   void check_async() const;
 
  private:
+  Comm() = default;
   int rank_ = 0, world_ = 1;
   void* comm_ = nullptr;
 };
@@ -145,6 +154,7 @@ class GpuSolver {
 
   // Host copy of the local array holding u^K (which = 0) or u^{K−1} (which = 1), full padded layout.
   std::vector<double> download(int which) const;
+  int device() const { return dev_; }  // the HIP device this rank's buffers and streams live on
 
   const Layout& layout() const { return lay_; }
   const Dims& dims() const { return dims_; }
@@ -238,6 +248,7 @@ class GpuSolver {
   Problem prob_;
   SolverOptions opt_;
   Coeffs coef_;
+  int dev_ = 0;
   int rank_, world_;
   std::shared_ptr<Comm> comm_;
   bool loopback_ = false;
@@ -321,7 +332,8 @@ class GpuSolver {
   unsigned* peer_flags_[2] = {nullptr, nullptr};
   bool peer_ipc_[2] = {false, false};          // opened with hipIpcOpenMemHandle (closed in the destructor)
   int push_epoch_ = 0;                         // passes of the earlier solves (push_cp_wait: epochs run on)
-  TbPush* push_host_ = nullptr;                // per pass of a solve (pinned), uploaded at its start ...
+  TbPush* push_host_ = nullptr;                // per pass of a solve (pinned; [0, K) captured, [K, 2K) eager), ...
+  TbPush* push_tab_ = nullptr;                 // ... the half the solve being enqueued uses, uploaded at its start ...
   TbPush* push_dev_ = nullptr;                 // ... to this device table the passes read
   TbPush make_push(int j, int npass) const;    // pass j (1-based) of npass
   mutable unsigned push_uid_ = 0;              // solver instance number (table tags)
@@ -403,6 +415,9 @@ namespace wave3d {
 // Same GpuSolver code as production except the transport; used to validate the multi-rank path on one GPU.
 // Transports:
 //   "loopback"  : halos by hipMemcpyAsync between the ranks' buffers (no RCCL);
+//   "multi-device": rank r on device r (world ≤ visible GPUs), one RCCL communicator over all of them from
+//                 ncclCommInitAll, each rank's production solve driven by its own host thread (RCCL needs the ranks'
+//                 calls concurrently): real cross-device RCCL / copy-engine traffic without a launcher;
 //   "rccl-self" : every rank owns a ONE-rank RCCL communicator (RCCL refuses two ranks of one communicator on one
 //                 device, but a one-rank communicator may send to itself) and moves each of its messages with
 //                 ncclGroupStart; ncclSend(peer's face, 0); ncclRecv(own ghosts, 0); ncclGroupEnd on its side stream,
@@ -420,7 +435,7 @@ class GpuGroup {
   GpuSolver& rank(int r) { return *ranks_[static_cast<size_t>(r)]; }
   int world() const { return static_cast<int>(ranks_.size()); }
   const std::string& transport() const { return transport_; }
-  bool graph_enabled() const { return graph_; }
+  bool graph_enabled() const { return multi_ ? ranks_[0]->options().graph : graph_; }
   // RCCL communicators in use and the rank count each reports (rccl-self: world one-rank communicators)
   std::vector<int> comm_counts() const;
   void set_state(const double* prev_global, const double* cur_global, int n0);  // every rank (GpuSolver::set_state)
@@ -437,6 +452,7 @@ class GpuGroup {
   hipEvent_t all_packed_ = nullptr, all_pulled_ = nullptr;  // group barriers on gs_ (see enqueue)
   std::vector<hipEvent_t> join_;
   hipGraphExec_t exec_ = nullptr;
+  bool multi_ = false;  // "multi-device": every rank on its own GPU, solved by its own thread
 };
 
 // Host-scalar collectives over the RCCL communicator (timer max-reduction, barriers). Blocking.

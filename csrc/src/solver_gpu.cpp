@@ -50,6 +50,23 @@ Comm::Comm(int rank, int world, const std::string& unique_id) : rank_(rank), wor
   }
 }
 
+std::vector<std::shared_ptr<Comm>> Comm::init_all(int world) {
+  W3D_REQUIRE(world >= 1, "init_all: world must be >= 1");
+  std::vector<ncclComm_t> raw(static_cast<size_t>(world), nullptr);
+  std::vector<int> devs(static_cast<size_t>(world));
+  for (int r = 0; r < world; ++r) devs[static_cast<size_t>(r)] = r;
+  W3D_NCCL(ncclCommInitAll(raw.data(), world, devs.data()));
+  std::vector<std::shared_ptr<Comm>> out;
+  for (int r = 0; r < world; ++r) {
+    std::shared_ptr<Comm> c(new Comm());
+    c->rank_ = r;
+    c->world_ = world;
+    c->comm_ = raw[static_cast<size_t>(r)];
+    out.push_back(std::move(c));
+  }
+  return out;
+}
+
 int Comm::count() const {
   int n = 0;
   W3D_NCCL(ncclCommCount(static_cast<ncclComm_t>(comm_), &n));
@@ -109,7 +126,7 @@ void wait_stream(hipStream_t s, const Comm* comm, double timeout_s) {
 
 // Multi-stream captures with cross-stream event joins repeated per unit (the multi-rank schedules: side-stream
 // exchange joined back every pass) crash inside hipStreamEndCapture of the HIP 7.0 runtime that PyTorch-ROCm bundles
-// (tools/capture_probe.hip pattern 5, capture_probe2.hip); the system ROCm 7.2 runtime captures them correctly
+// (tools/probes/capture_probe.hip pattern 5, capture_probe2.hip); the system ROCm 7.2 runtime captures them correctly
 // (probed, and the rccl-self group graphs). Multi-rank solves are therefore captured only on HIP >= 7.2 (the native
 // CLI, which bench.py runs per rank, always is); inside a torch process they run eagerly. W3D_FORCE_CAPTURE=1
 // overrides the check.
@@ -128,6 +145,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
     : prob_(prob), opt_(opt), coef_(Coeffs::from(prob)), rank_(rank), world_(world), comm_(std::move(comm)),
       loopback_(loopback) {
   prob_.validate();
+  W3D_HIP(hipGetDevice(&dev_));
   W3D_REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
   W3D_REQUIRE(world == 1 || comm_ || loopback_ || opt_.fake_comm || ((opt_.push || opt_.sdma) && opt_.push_no_collective),
               "world > 1 needs an RCCL communicator (or the loopback group, or the push / sdma transport without one)");
@@ -272,8 +290,9 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
     W3D_HIP(hipMemset(u_[b], 0, static_cast<size_t>(lay_.bytes())));
   }
   if (push_) {
-    // staging and flags in uncached memory: the neighbours' write-through stores and this GPU's reads meet in HBM, no
-    // L2 ever holds them (the protocol needs no cache maintenance, leapfrog_tb_kernel.hpp)
+    // staging in fine-grained device memory (W3D_PUSH_STAGING=uncached: uncached), flags uncached: the neighbours'
+    // stores are write-through (system scope) and a reader invalidates its L2 once per pass after its wait
+    // (system-scope acquire, leapfrog_tb_kernel.hpp)
     const size_t sb = static_cast<size_t>(8 * lay_.xg * lay_.plane) * sizeof(double);
     const char* mt = std::getenv("W3D_PUSH_STAGING");  // (experiment: "uncached" instead of fine-grained)
     const unsigned stg_flags = mt && !std::strcmp(mt, "uncached") ? hipDeviceMallocUncached : hipDeviceMallocFinegrained;
@@ -285,10 +304,13 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
     W3D_HIP(hipMemset(stg_, 0, sb));
     W3D_HIP(hipMemset(flags_, 0, 256));
     const size_t tb = static_cast<size_t>(prob_.K) * sizeof(TbPush);  // (a solve has at most K passes)
-    W3D_HIP(hipHostMalloc(reinterpret_cast<void**>(&push_host_), tb, hipHostMallocDefault));
-    // (uncached too: the table is rewritten by host-to-device copies, which a kernel must never read through an L2
-    // line the same memory held for an earlier, freed buffer — measured: a fresh solver's passes read the previous
-    // solver's table there and pushed into its freed staging)
+    // two host tables: [0, K) for the captured solve (its H2D copy node reads the table at every replay), [K, 2K) for
+    // eager solves — an eager solve after the capture (e.g. the phase-timer solve) must not rewrite the tags the graph's
+    // kernel nodes were captured with
+    W3D_HIP(hipHostMalloc(reinterpret_cast<void**>(&push_host_), 2 * tb, hipHostMallocDefault));
+    // (fine-grained device memory for the pass table: the table is rewritten by host-to-device copies, and each pass
+    // starts with a system-scope acquire, so no pass reads it through an L2 line the same memory held for an earlier,
+    // freed buffer — measured: a fresh solver's passes once read the previous solver's table there)
     W3D_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&push_dev_), tb, hipDeviceMallocFinegrained));
     // (stream memops are not captured into graphs; running epochs are per-launch arguments)
     if (opt_.push_cp_wait || opt_.push_no_collective) opt_.graph = false;
@@ -315,6 +337,12 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
     LeapfrogTbTiling t = opt_.tiling_tb;
     t.stages = opt_.temporal;  // partials per level do not depend on the stage count
     n_tb_ = leapfrog_tb_partials(lay_, full_, t);
+    // multi-rank units also launch sub-boxes of the compute box (shells, interior), whose fewer tiles may be split into
+    // more x chunks: at most tiles · ceil(target / tiles) < tiles + target blocks (their slots are n_tb_ wide)
+    if (mode_ == Mode::kDeepTb)
+      n_tb_ = static_cast<int>(imax(n_tb_, round_up(ceil_div(full_.y1 - full_.y0, kTbTile) *
+                                                            ceil_div(full_.z1 - full_.z0, kTbTile) +
+                                                        t.target_blocks, 8)));
     leapfrog_tb_prepare(push_);
   }
   int n_deep = 0;
@@ -622,8 +650,11 @@ void GpuSolver::phase_init() {
   if (push_) {  // every pass's push parameters, in device memory before the first pass reads them
     const int npass = static_cast<int>(units_.size());
     W3D_REQUIRE(npass <= prob_.K, "push: more passes than steps");
-    for (int j = 1; j <= npass; ++j) push_host_[j - 1] = make_push(j, npass);
-    W3D_HIP(hipMemcpyAsync(push_dev_, push_host_, static_cast<size_t>(npass) * sizeof(TbPush), hipMemcpyHostToDevice,
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    W3D_HIP(hipStreamIsCapturing(s0_, &cs));
+    push_tab_ = push_host_ + (cs == hipStreamCaptureStatusActive ? 0 : prob_.K);
+    for (int j = 1; j <= npass; ++j) push_tab_[j - 1] = make_push(j, npass);
+    W3D_HIP(hipMemcpyAsync(push_dev_, push_tab_, static_cast<size_t>(npass) * sizeof(TbPush), hipMemcpyHostToDevice,
                            s0_));
   }
 }
@@ -655,9 +686,16 @@ void GpuSolver::unit_shell(int i) {
     if (needs_exchange(i) && !late_exchange()) {
       build_msgs(i);
       hipStream_t xs = xstream();
-      W3D_HIP(hipEventRecord(ev_shell_, s0_));  // (the unit's inputs are ready: fork)
-      W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
-      for (const LBox& b : tb_shells(i)) tb_pass(u, b, kPhaseShell, xs);
+      if (opt_.shells_concurrent > 0 || (opt_.shells_concurrent < 0 && block_tb_)) {
+        W3D_HIP(hipEventRecord(ev_shell_, s0_));  // (the unit's inputs are ready: fork)
+        W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
+        for (const LBox& b : tb_shells(i)) tb_pass(u, b, kPhaseShell, xs);
+      } else {
+        // (serial: the shells own the GPU and finish first, so the exchange starts as early as possible)
+        for (const LBox& b : tb_shells(i)) tb_pass(u, b, kPhaseShell, s0_);
+        W3D_HIP(hipEventRecord(ev_shell_, s0_));
+        W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
+      }
       return;
     }
   } else if (mode_ == Mode::kSingleStep && split()) {
@@ -751,7 +789,7 @@ void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase, hipStream_t s
   const TbPush* qd = nullptr;
   if (push_) {
     const int j = cur_unit_ + 1;
-    qh = push_host_ + (j - 1);
+    qh = push_tab_ + (j - 1);
     qd = push_dev_ + (j - 1);
     if (opt_.push_cp_wait)
       for (int side = 0; side < 2; ++side)
@@ -777,7 +815,7 @@ void GpuSolver::tb_split(int i, std::vector<LBox>& shells, LBox& interior) const
   shells.clear();
   interior = full_;
   if (!needs_exchange(i) || late_exchange()) return;
-  const i64 w = units_[static_cast<size_t>(i) + 1].steps, T = 32;
+  const i64 w = units_[static_cast<size_t>(i) + 1].steps, T = kTbTile;
   const LBox f = full_;
   bool nb[3][2];
   for (int a = 0; a < 3; ++a)
@@ -838,7 +876,7 @@ void GpuSolver::unit_interior(int i) {
   const double ct = ct_[static_cast<size_t>(nc)];
   const double* s = d_s_ + 1;
   // (group ranks: lb_fence already put s0 behind every rank's pull, ev_halo_ included; a second, redundant wait on
-  // the own side stream after that fence crashes HIP 7.2's hipStreamEndCapture — tools/capture_probe2.hip flag 36)
+  // the own side stream after that fence crashes HIP 7.2's hipStreamEndCapture — tools/probes/capture_probe2.hip flag 36)
   const bool wait = needs_exchange(i) && xstream() != s0_ && (!loopback_ || sdma_);
   int np = 0;  // partials to reduce
   bool joined = false;
@@ -1061,14 +1099,22 @@ RunResult GpuSolver::run() {
     // capture once (outside the timed region of later runs); fall back to eager launches if capture is refused
     hipGraph_t g = nullptr;
     bool ok = hipStreamBeginCapture(s0_, hipStreamCaptureModeThreadLocal) == hipSuccess;
+    std::string thrown;
     if (ok) {
       try {
         enqueue_solve();
-      } catch (...) {
+      } catch (const std::exception& ex) {
         ok = false;
+        thrown = ex.what();
       }
       const hipError_t e = hipStreamEndCapture(s0_, &g);
       ok = ok && e == hipSuccess && g != nullptr;
+    }
+    // (an error of the schedule itself is not a capture problem: report it instead of retrying eagerly on streams the
+    // aborted capture may have left unusable)
+    if (!thrown.empty()) {
+      if (g) (void)hipGraphDestroy(g);
+      fail("solve schedule failed while being captured: " + thrown);
     }
     if (ok) ok = hipGraphInstantiate(&gx, g, nullptr, nullptr, 0) == hipSuccess;
     if (g) (void)hipGraphDestroy(g);
@@ -1128,8 +1174,10 @@ TbPush GpuSolver::make_push(int j, int npass) const {
   // (tag: unique per solver instance, rank, solve and pass, so a table entry left by another solver never matches)
   static unsigned instances = 0;
   if (push_uid_ == 0) push_uid_ = ++instances;
-  q.tag = (push_uid_ * 2654435761u) ^ (static_cast<unsigned>(rank_) << 20) ^
-          (static_cast<unsigned>(push_epoch_ & 0xFFF) << 8) ^ static_cast<unsigned>(j);
+  // (disjoint fields: the pass index in the low 16 bits, the solve epoch in the high 16, XORed with a hash of the
+  // instance and rank — distinct (epoch, pass) pairs never share a tag within 65536 epochs)
+  q.tag = ((push_uid_ * 2654435761u) ^ (static_cast<unsigned>(rank_) * 40503u)) ^
+          ((static_cast<unsigned>(push_epoch_) & 0xFFFFu) << 16) ^ (static_cast<unsigned>(j) & 0xFFFFu);
   const int par = j % 2, rpar = (j - 1) % 2;
   // (perf attribution of the transport with --fake-rank only: W3D_PUSH_ATTRIB=nofwd / noghost drop the forwarded
   // stores / the staging reads — the results are then wrong)
@@ -1224,8 +1272,12 @@ void GpuSolver::push_check() {
 std::vector<double> GpuSolver::download(int which) const {
   std::vector<double> h(static_cast<size_t>(lay_.total));
   const double* src = u_[which == 0 ? final_buf_ : prev_buf_];
+  int cur = 0;
+  W3D_HIP(hipGetDevice(&cur));
+  W3D_HIP(hipSetDevice(dev_));
   W3D_HIP(hipDeviceSynchronize());
   W3D_HIP(hipMemcpy(h.data(), src, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+  W3D_HIP(hipSetDevice(cur));
   return h;
 }
 
@@ -1281,9 +1333,45 @@ namespace wave3d {
 GpuGroup::GpuGroup(const Problem& prob, const SolverOptions& opt, int world, const std::string& transport)
     : transport_(transport) {
   W3D_REQUIRE(world >= 1, "world must be >= 1");
-  W3D_REQUIRE(transport == "loopback" || transport == "rccl-self" || transport == "push" || transport == "sdma",
-              "group transport must be loopback, rccl-self, push or sdma, not " + transport);
+  W3D_REQUIRE(transport == "loopback" || transport == "rccl-self" || transport == "push" || transport == "sdma" ||
+                  transport == "multi-device",
+              "group transport must be loopback, rccl-self, push, sdma or multi-device, not " + transport);
   SolverOptions o = opt;
+  if (transport == "multi-device") {
+    // one rank per visible device, each with its rank of one communicator; the production GpuSolver (not a group
+    // member): its own graph, RCCL exchanges and error-log all-gather; opt.sdma selects the copy engines between the
+    // devices (peer pointers, peer access enabled), else RCCL
+    multi_ = true;
+    int ndev = 0, dev0 = 0;
+    W3D_HIP(hipGetDeviceCount(&ndev));
+    W3D_HIP(hipGetDevice(&dev0));
+    W3D_REQUIRE(world <= ndev, "multi-device group: " + std::to_string(world) + " ranks but " + std::to_string(ndev) +
+                                   " visible GPU(s)");
+    const auto comms = Comm::init_all(world);
+    for (int r = 0; r < world; ++r) {
+      W3D_HIP(hipSetDevice(r));
+      for (int q = 0; q < world && o.sdma; ++q)
+        if (q != r) {
+          int can = 0;
+          W3D_HIP(hipDeviceCanAccessPeer(&can, r, q));
+          W3D_REQUIRE(can, "multi-device sdma: GPU " + std::to_string(r) + " cannot access GPU " + std::to_string(q));
+          const hipError_t e = hipDeviceEnablePeerAccess(q, 0);
+          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) W3D_HIP(e);
+          (void)hipGetLastError();
+        }
+      ranks_.push_back(std::make_unique<GpuSolver>(prob, o, r, world, comms[static_cast<size_t>(r)], false));
+    }
+    if (o.sdma && world > 1)
+      for (auto& sp : ranks_)
+        for (GpuSolver::XLink& l : sp->xlinks_) {
+          GpuSolver* q = ranks_[static_cast<size_t>(l.peer)].get();
+          l.flags = q->xflags_;
+          for (int b = 0; b < q->nbuf_; ++b) l.u[b] = q->u_[b];
+          l.recv = q->recv_buf_;
+        }
+    W3D_HIP(hipSetDevice(dev0));
+    return;
+  }
   o.push = transport == "push";
   o.sdma = transport == "sdma";
   for (int r = 0; r < world; ++r) {
@@ -1338,6 +1426,13 @@ GpuGroup::GpuGroup(const Problem& prob, const SolverOptions& opt, int world, con
 }
 
 GpuGroup::~GpuGroup() {
+  if (multi_) {  // (each rank's resources on its own device)
+    for (auto& r : ranks_) {
+      (void)hipSetDevice(r->device());
+      r.reset();
+    }
+    return;
+  }
   if (exec_) (void)hipGraphExecDestroy(exec_);
   for (hipEvent_t e : join_) (void)hipEventDestroy(e);
   for (hipEvent_t e : {fork_, all_packed_, all_pulled_})
@@ -1404,7 +1499,7 @@ void GpuGroup::enqueue() {
     // Cross-rank ordering goes through the group stream: it joins every rank's "packed" event, and every puller
     // waits on the join (likewise "pulled" before anyone overwrites its send regions). Direct waits of one rank's
     // stream on a PEER's side-stream event are avoided on purpose: HIP 7.2 crashes in hipStreamEndCapture on such
-    // sibling-to-sibling waits (tools/capture_probe2.hip, flag 1); fork/join through the origin captures fine.
+    // sibling-to-sibling waits (tools/probes/capture_probe2.hip, flag 1); fork/join through the origin captures fine.
     for (auto* s : rs) s->lb_pack(i);
     step("pack", i);
     bool any = false;
@@ -1448,6 +1543,32 @@ void GpuGroup::join() {
 }
 
 RunResult GpuGroup::run() {
+  if (multi_) {
+    // every rank's production solve on its own thread and device, concurrently (RCCL's collectives and send/recv
+    // pairs need every rank's call in flight); each rank's log is the global one (all-gathered), rank 0's is returned
+    std::vector<RunResult> out(ranks_.size());
+    std::vector<std::string> err(ranks_.size());
+    std::vector<std::thread> th;
+    const double t0 = now_s();
+    for (size_t r = 0; r < ranks_.size(); ++r)
+      th.emplace_back([&, r] {
+        try {
+          W3D_HIP(hipSetDevice(ranks_[r]->device()));
+          out[r] = ranks_[r]->run();
+        } catch (const std::exception& e) {
+          err[r] = e.what();
+        }
+      });
+    for (auto& t : th) t.join();
+    for (size_t r = 0; r < ranks_.size(); ++r)
+      W3D_REQUIRE(err[r].empty(), "multi-device rank " + std::to_string(r) + ": " + err[r]);
+    for (size_t r = 1; r < ranks_.size(); ++r)
+      W3D_REQUIRE(out[r].max_err == out[0].max_err, "multi-device: ranks gathered different error logs");
+    RunResult r = out[0];
+    r.solve_s = now_s() - t0;
+    ++runs_;
+    return r;
+  }
   std::vector<GpuSolver*> rs;
   for (auto& p : ranks_) rs.push_back(p.get());
   const int K = rs[0]->prob_.K;

@@ -18,6 +18,9 @@ hip        push-ipc    one process per rank (torchrun): native GpuSolver on the 
                        between processes (IPC handles all-gathered over torch.distributed; RCCL for the error log)
 hip        sdma        world > 1 in ONE process: native GpuGroup on the LDS passes (slab or block), halos copied by the
                        SDMA copy engines into the peers' buffers, ordered by command-processor flag waits
+hip        multi-dev.  world ≤ visible GPUs in ONE process: rank r on device r, one RCCL communicator from
+                       ncclCommInitAll, one host thread per rank running the production GpuSolver (transport
+                       "multi-device"; sdma=True: copy engines between the devices instead of RCCL)
 hip        sdma-ipc    one process per rank (torchrun): native GpuSolver with the copy-engine transport between
                        processes (IPC handles all-gathered over torch.distributed; RCCL for the error log)
 cpu        native      C++ CpuSolver, OpenMP (the reference's sequential / OpenMP programs), world == 1
@@ -66,7 +69,7 @@ def _resolve(backend: str, transport: str, world: int) -> tuple[str, str]:
     if transport == "auto":
         transport = {"hip": "rccl", "cpu": "native" if world == 1 else "torch", "torch": "none"}[backend]
     ok = {("hip", "rccl"), ("hip", "torch"), ("hip", "loopback"), ("hip", "rccl-self"), ("hip", "push"),
-          ("hip", "push-ipc"), ("hip", "sdma"), ("hip", "sdma-ipc"),
+          ("hip", "push-ipc"), ("hip", "sdma"), ("hip", "sdma-ipc"), ("hip", "multi-device"),
           ("cpu", "native"),
           ("cpu", "torch"),
           ("torch", "none")}
@@ -90,7 +93,7 @@ class Solver:
                  tiling_tb: dict | None = None,
                  debug_sync: bool = False, poison_ghosts: bool = False, deep_min_planes: int | None = None,
                  tb_min_planes: int | None = None, rccl: bool = True, autotune: bool = False,
-                 autotune_rounds: int = 5):
+                 autotune_rounds: int = 5, copy_engines: bool = False):
         import torch.distributed as dist
 
         if not spec.cfl_ok and not force:
@@ -115,13 +118,14 @@ class Solver:
             self.device = torch.device("cuda", dev)
         else:
             self.device = torch.device("cpu")
-        if self.backend == "hip" and self.transport in ("loopback", "rccl-self", "push", "sdma"):
+        if self.backend == "hip" and self.transport in ("loopback", "rccl-self", "push", "sdma", "multi-device"):
             opts = self._options(C, decomp, spec, overlap, graph, tiling, temporal, tiling2, init2, tb, tiling_tb)
             opts.timers, opts.debug_sync, opts.poison_ghosts = timers, debug_sync, poison_ghosts
             if deep_min_planes is not None:
                 opts.deep_min_planes = deep_min_planes
             if tb_min_planes is not None:
                 opts.tb_min_planes = tb_min_planes
+            opts.sdma = copy_engines and self.transport == "multi-device"
             self._impl = C.GpuGroup(spec.native(), opts, world, self.transport)
             self.dims = self._impl.dims().as_tuple()
         elif self.backend == "hip" and self.transport in ("rccl", "push-ipc", "sdma-ipc"):
@@ -239,7 +243,7 @@ class Solver:
         """The whole (N+1)³ field u^K (which=0) / u^{K-1} (which=1) on the CPU (single rank or loopback group)."""
         from .ops.stencil import grid_view
 
-        if self.transport not in ("loopback", "rccl-self", "push", "sdma"):
+        if self.transport not in ("loopback", "rccl-self", "push", "sdma", "multi-device"):
             if self.world != 1:
                 raise RuntimeError("global_field needs world == 1 or the loopback transport")
             return self.owned_field(which)

@@ -56,7 +56,7 @@ LIB_SOURCES = [
     ("src/cpu_dist.cpp", "cpu"),
 ]
 EXT_SOURCES = [("src/bindings.cpp", "hip")]
-CLI_SOURCES = [("app/wave3d_main.cpp", "hip")]
+CLI_SOURCES = [("app/wave3d_main.cpp", "hip"), ("app/cli_args.cpp", "hip"), ("app/cli_cpu.cpp", "hip")]
 PERSONALITIES = ["wave", "openmpwave", "wave3dOMP", "onlyMPI", "mpi", "mpiomp", "mpigpu-1"]
 
 
@@ -70,7 +70,7 @@ def _hash_inputs(src: Path, flags: list[str]) -> str:
     h = hashlib.sha256()
     h.update(" ".join(flags).encode())
     h.update(src.read_bytes())
-    for hdr in sorted((CSRC / "include").rglob("*.hpp")):
+    for hdr in sorted([*(CSRC / "include").rglob("*.hpp"), *(CSRC / "app").glob("*.hpp")]):
         h.update(hdr.read_bytes())
     return h.hexdigest()[:16]
 

@@ -3,6 +3,8 @@
 value per dispatch, plus derived ratios. Usage: python tools/pmc_summary.py gpurun_out/pmc/*/run_counter_collection.csv"""
 import collections
 import csv
+import glob
+import os
 import re
 import sys
 
@@ -13,7 +15,21 @@ def short(name: str) -> str:
     return m.group(1) if m else n[:60]
 
 
+def expand(paths):
+    """Files as given; a directory stands for every *counter_collection.csv below it (rocprofv3 -d DIR)."""
+    out = []
+    for p in paths:
+        if os.path.isdir(p):
+            out += sorted(glob.glob(os.path.join(p, "**", "*counter_collection.csv"), recursive=True))
+        else:
+            out.append(p)
+    if not out:
+        raise SystemExit(f"pmc_summary: no counter_collection.csv under {paths}")
+    return out
+
+
 def main(paths):
+    paths = expand(paths)
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     dur = collections.defaultdict(list)
     for p in paths:

@@ -228,7 +228,7 @@ SolverOptions options_from(const Args& a, bool fake) {
               "--transport must be rccl, push or sdma, not " + a.transport);
   o.push = a.transport == "push";
   o.sdma = a.transport == "sdma";
-  if (const char* sh = std::getenv("W3D_SHELLS")) o.shells_concurrent = std::string(sh) == "concurrent" ? 1 : 0;
+  if (const char* sh = std::getenv("W3D_SHELLS")) o.shells_concurrent = std::string(sh) == "concurrent";
   o.push_cp_wait = a.push_cp_wait;
   o.push_no_collective = a.no_rccl;  // (no end-of-solve collective: the flag epochs run on, eager launches)
   if (a.t2_rows > 0) o.tiling2.rows = a.t2_rows;

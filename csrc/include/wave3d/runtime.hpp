@@ -71,6 +71,8 @@ struct Candidate {
   std::string name, decomp, transport;  // transport: rccl | sdma | push
   int temporal = 4;
   bool overlap = true;
+  int sdma_streams = 0;            // copy streams (0: the solver's default)
+  bool shells_concurrent = false;  // overlap: shells beside the interior instead of before it
 };
 // the candidates for `world` ranks (fake: one rank of a `world`-rank job alone); push candidates only on request
 std::vector<Candidate> autotune_candidates(int world, bool with_push);

@@ -70,11 +70,13 @@ struct SolverOptions {
   // waited for by the command processors (hipStreamWriteValue32 / hipStreamWaitValue32, graph-capturable on HIP 7.2).
   // See transport_sdma.cpp for the protocol.
   bool sdma = false;
-  // deep-tb with overlap: the shell boxes run on the side stream concurrently with the interior (1), or on s0 before it
-  // (0: they get the whole GPU and finish first, so the exchange starts earlier); -1: per decomposition — concurrent for
-  // 3-D blocks (their up to 6 small shell launches leave most CUs idle when alone: 512³ 2x2x2 rank 1.20 vs 1.38 ms),
-  // serial for slabs (2 shell launches; the copy-engine exchange starts earlier: 512³ rank 1/8 1.65 vs 2.10 ms)
-  int shells_concurrent = -1;
+  // deep-tb with overlap: the shell boxes run on the side stream concurrently with the interior (true), or on s0 before
+  // it (false: they get the whole GPU and finish first, so the exchange starts earlier — measured faster with the copy
+  // engines at 512³ and 2048³; concurrent helps the small block shells when no transfer follows; env W3D_SHELLS)
+  bool shells_concurrent = false;
+  // copy-engine transport: copy streams (each gets its own SDMA engine; 0 = auto: one per slab face, one for a block
+  // rank's messages — in a replayed graph a second copy stream made the 2048³ 2x2x2 rank slower, 48.8 vs 43.6 ms)
+  int sdma_streams = 0;
   bool push_cp_wait = false;
   // push ranks without an end-of-solve collective (no RCCL communicator): the flag epochs run on over the solves
   // instead of being reset (eager launches: every launch carries its own epochs)
@@ -179,6 +181,7 @@ class GpuSolver {
   // copy-engine transport: this rank's IPC handles (field buffers, staging, flags) + layout facts, and connecting to
   // every neighbour from all ranks' handles (index = rank); a fake rank connects to itself
   bool sdma() const { return sdma_; }
+  int copy_streams() const { return static_cast<int>(xcs_.size()); }
   std::string sdma_handles() const;
   void connect_sdma(const std::vector<std::string>& all);
   void connect_sdma_self();
@@ -367,6 +370,10 @@ class GpuSolver {
   std::vector<hipStream_t> xcs_;
   std::vector<hipEvent_t> xcev_;
   hipEvent_t xfork_ = nullptr;
+  // flag values as device words ([parity][i] = xval(i)): the "arrived" signal is a 4-byte copy-engine write queued
+  // after the data copies on the same stream, so no compute queue waits for the copies (a signal kernel would, and a
+  // hardware queue shared with s0 would hold the interior pass behind it: measured, profiles/r3)
+  unsigned* xvals_ = nullptr;
   unsigned xval(int i) const { return (xpar_ ? 0x10000u : 0u) + static_cast<unsigned>(i + 1); }
   unsigned xend(int par) const { return (par ? 0x10000u : 0u) + 0xFFFFu; }
   void sdma_alloc();

@@ -14,8 +14,9 @@ namespace wave3d {
 
 std::vector<Candidate> autotune_candidates(int world, bool with_push) {
   std::vector<Candidate> v;
-  auto add = [&](const char* name, const char* decomp, const char* transport, int temporal, bool overlap) {
-    v.push_back(Candidate{name, decomp, transport, temporal, overlap});
+  auto add = [&](const char* name, const char* decomp, const char* transport, int temporal, bool overlap,
+                 int streams = 0, bool conc = false) {
+    v.push_back(Candidate{name, decomp, transport, temporal, overlap, streams, conc});
   };
   if (world <= 1) {  // one rank: only the pass depth matters
     add("slab-S4", "slab", "rccl", 4, true);
@@ -39,8 +40,10 @@ std::vector<Candidate> autotune_candidates(int world, bool with_push) {
   if (world >= 4) {  // (2 ranks: "block" is the slab)
     add("block-S4-seq", "block", "rccl", 4, false);
     add("block-S4", "block", "rccl", 4, true);
+    add("block-S4-conc", "block", "rccl", 4, true, 0, true);  // (shells beside the interior)
     add("block-S4-sdma-seq", "block", "sdma", 4, false);
-    add("block-S4-sdma", "block", "sdma", 4, true);
+    add("block-S4-sdma", "block", "sdma", 4, true);            // (one copy stream)
+    add("block-S4-sdma-x2", "block", "sdma", 4, true, 2);     // (two copy streams: two engines)
     add("block-S3", "block", "rccl", 3, true);
     add("block-S1", "block", "rccl", 1, true);
   }
@@ -68,7 +71,8 @@ std::string signature(const GpuSolver& s) {
   // (the pass depth only matters to the schedules that fuse steps: a single-step schedule ignores it)
   const int depth = s.mode() == "single-step" ? 1 : s.options().temporal;
   return s.mode() + "/" + s.transport() + "/" + (s.overlapped() ? "ov" : "seq") + "/S" + std::to_string(depth) + "/" +
-         std::to_string(d.px) + "x" + std::to_string(d.py) + "x" + std::to_string(d.pz);
+         std::to_string(d.px) + "x" + std::to_string(d.py) + "x" + std::to_string(d.pz) + "/cs" +
+         std::to_string(s.sdma() ? s.copy_streams() : 0) + (s.overlapped() && s.options().shells_concurrent ? "/conc" : "");
 }
 }  // namespace
 
@@ -98,6 +102,8 @@ AutotuneResult autotune(const Problem& prob, const SolverOptions& base, int rank
     o.overlap = c.overlap;
     o.push = c.transport == "push";
     o.sdma = c.transport == "sdma";
+    if (c.sdma_streams > 0) o.sdma_streams = c.sdma_streams;
+    o.shells_concurrent = o.shells_concurrent || c.shells_concurrent;
     std::unique_ptr<GpuSolver> cand;
     std::string err;
     try {

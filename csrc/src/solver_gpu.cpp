@@ -379,6 +379,7 @@ GpuSolver::~GpuSolver() {
       if (l.flags) (void)hipIpcCloseMemHandle(l.flags);
     }
   if (xflags_) (void)hipFree(xflags_);
+  if (xvals_) (void)hipFree(xvals_);
   for (hipStream_t c : xcs_) (void)hipStreamDestroy(c);
   for (hipEvent_t e : xcev_) (void)hipEventDestroy(e);
   if (xfork_) (void)hipEventDestroy(xfork_);
@@ -686,7 +687,7 @@ void GpuSolver::unit_shell(int i) {
     if (needs_exchange(i) && !late_exchange()) {
       build_msgs(i);
       hipStream_t xs = xstream();
-      if (opt_.shells_concurrent > 0 || (opt_.shells_concurrent < 0 && block_tb_)) {
+      if (opt_.shells_concurrent) {
         W3D_HIP(hipEventRecord(ev_shell_, s0_));  // (the unit's inputs are ready: fork)
         W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
         for (const LBox& b : tb_shells(i)) tb_pass(u, b, kPhaseShell, xs);

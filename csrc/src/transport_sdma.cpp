@@ -105,8 +105,17 @@ void GpuSolver::sdma_alloc() {
   std::vector<unsigned> init(2 * n, 0u);
   for (size_t k = 0; k < n; ++k) init[2 * k + 1] = xend(1);
   W3D_HIP(hipMemcpy(xflags_, init.data(), init.size() * sizeof(unsigned), hipMemcpyHostToDevice));
-  // copy streams (W3D_SDMA_STREAMS, default 4; at most one per link)
-  int ns = 4;
+  {
+    const int K1 = prob_.K + 1;
+    std::vector<unsigned> v(static_cast<size_t>(2 * K1));
+    for (int par = 0; par < 2; ++par)
+      for (int i = 0; i < K1; ++i) v[static_cast<size_t>(par * K1 + i)] = (par ? 0x10000u : 0u) + static_cast<unsigned>(i + 1);
+    W3D_HIP(hipMalloc(&xvals_, v.size() * sizeof(unsigned)));
+    W3D_HIP(hipMemcpy(xvals_, v.data(), v.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+  }
+  // copy streams (SolverOptions::sdma_streams, env W3D_SDMA_STREAMS; at most one per link): each has its own engine,
+  // and with s0 and s1 at most 4 streams fit the hardware queues a process gets (GPU_MAX_HW_QUEUES)
+  int ns = opt_.sdma_streams > 0 ? opt_.sdma_streams : block_tb_ ? 1 : 2;
   if (const char* v = std::getenv("W3D_SDMA_STREAMS")) ns = std::max(1, std::atoi(v));
   ns = std::min<int>(ns, static_cast<int>(std::max<size_t>(1, xlinks_.size())));
   int lo = 0, hi = 0;
@@ -219,21 +228,18 @@ void GpuSolver::unit_exchange_sdma(int i) {
     const int s = units_[static_cast<size_t>(i) + 1].steps;
     if (block_tb_) pack_halo(xs);  // (build_msgs set deep_s_ = s)
     // per copy stream: wait until its links' receivers have finished with the regions the copies overwrite, copy,
-    // then raise the links' "arrived" words (stream order: after the copies have completed)
+    // then raise the links' "arrived" words with 4-byte copy-engine writes behind the data (stream order: after the
+    // copies have completed; no compute queue is held while the copies run)
     W3D_HIP(hipEventRecord(xfork_, xs));
     const size_t P = static_cast<size_t>(lay_.plane), nc = xcs_.size();
     for (size_t c = 0; c < nc; ++c) {
       hipStream_t cs = xcs_[c];
       W3D_HIP(hipStreamWaitEvent(cs, xfork_, 0));
-      FlagOp w, sig, none;
+      FlagOp w, none;
       w.value = i == 0 ? xend(1 - xpar_) : xval(i - 1);
       w.status = reinterpret_cast<unsigned*>(errlog_);
       w.ticks = flag_ticks();
-      sig.value = xval(i);
-      for (size_t k = c; k < xlinks_.size(); k += nc) {
-        w.addr[w.n++] = xflags_ + 2 * k + 1;
-        sig.addr[sig.n++] = xsig(xlinks_[k], 0);
-      }
+      for (size_t k = c; k < xlinks_.size(); k += nc) w.addr[w.n++] = xflags_ + 2 * k + 1;
       launch_flag_sync(w, none, cs);
       for (size_t k = c; k < xlinks_.size(); k += nc) {
         const XLink& l = xlinks_[k];
@@ -254,7 +260,9 @@ void GpuSolver::unit_exchange_sdma(int i) {
           }
         }
       }
-      launch_flag_sync(none, sig, cs);
+      const unsigned* val = xvals_ + xpar_ * (prob_.K + 1) + i;  // (= xval(i))
+      for (size_t k = c; k < xlinks_.size(); k += nc)
+        W3D_HIP(hipMemcpyAsync(xsig(xlinks_[k], 0), val, sizeof(unsigned), hipMemcpyDeviceToDeviceNoCU, cs));
       W3D_HIP(hipEventRecord(xcev_[c], cs));
       W3D_HIP(hipStreamWaitEvent(xs, xcev_[c], 0));
     }

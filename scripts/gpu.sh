@@ -121,9 +121,11 @@ run_fakesweep() {
 
 run_transports() {
   local fr v
+  local vs=("--no-overlap" "" "--transport sdma" "--transport sdma --no-overlap")
+  [ -n "${W3D_TRANSPORTS_VARIANTS:-}" ] && IFS=';' read -r -a vs <<< "$W3D_TRANSPORTS_VARIANTS"
   for fr in 512:0.001:1/8:slab 512:0.001:0/2:slab 512:0.001:3/8:2x2x2 2048:0.00025:3/8:2x2x2; do
     IFS=: read -r N tau r dec <<< "$fr"
-    for v in "--no-overlap" "" "--transport sdma" "--transport sdma --no-overlap"; do
+    for v in "${vs[@]}"; do
       echo "== N=$N fake $r --decomp $dec $v"
       timeout -k 5 120 ./bin/wave3d "$N" "$tau" 20 1 --fake-rank "$r" --decomp "$dec" --repeat 7 --warmup 2 --quiet $v \
         | grep -E "Total time|Throughput" || return 1

@@ -81,6 +81,21 @@ def test_sdma_group_block_bitexact(gpu, world, decomp, overlap, K, check_every, 
         assert torch.equal(g.global_field(1), f1)
 
 
+@pytest.mark.parametrize("streams", ["1", "2", "4"])
+def test_sdma_copy_streams(gpu, monkeypatch, streams):
+    """The links spread over 1, 2 or 4 copy streams (one SDMA engine each): same bit-exact fields."""
+    monkeypatch.setenv("W3D_SDMA_STREAMS", streams)
+    spec = ProblemSpec(N=66, tau=1e-3, K=20)
+    r1, f0, _ = _ref(spec)
+    for decomp, world in (("2x2x2", 8), ("slab", 3)):
+        g = Solver(spec, backend="hip", transport="sdma", world=world, rank=0, decomp=decomp, device=0,
+                   poison_ghosts=True, tb_min_planes=8)
+        for _ in range(2):
+            r = g.run()
+            _same(r, r1)
+            assert torch.equal(g.global_field(0), f0)
+
+
 def test_sdma_needs_lds_passes(gpu):
     spec = ProblemSpec(N=40, tau=1e-3, K=10)
     with pytest.raises(Exception, match="sdma transport"):

@@ -141,8 +141,18 @@ struct TbGeom {
   static constexpr int PLP = PL + 2 * W0 + 2;
   static constexpr int DUMMY = PL + W0 + 1;
   static constexpr int QR = (NR + NT - 1) / NT;
-  // levels 0..S−1 × 2 parity slots; the analytic start adds a φ level (two parity slots) after them
-  static constexpr int lds_doubles(bool init = false) { return (S + (init ? 1 : 0)) * 2 * PLP; }
+  // The stage levels 1..S−1 live in COMPACT planes: position idx = tid + q·NT (row a = idx / H1, column b = idx % H1)
+  // at COFF + idx, row stride H1, no ring and no gap between rows, so the 16 lanes of every LDS access phase touch 16
+  // consecutive doubles (all 32 banks once). In the W0-strided layout a group that straddled a row end skipped the
+  // 2-column gap and hit 2 banks twice: 26 % of the LDS cycles were bank conflicts (PMC, profiles/r1_pmc_production_512.md).
+  // Only level 0 (u^n, stage 1's input) needs the ring and keeps the W0 layout. Neighbours ±1, ±H1 of every lane of a
+  // running wave (indices up to NPR − 1) stay inside the plane; the values read for positions outside a stage's region
+  // are garbage and never used, as before.
+  static constexpr int NPR = (NP + 63) / 64 * 64;
+  static constexpr int COFF = H1 + 1;
+  static constexpr int PLC = COFF + NPR + H1 + 1;
+  // level 0 × 2 parity slots, levels 1..S−1 × 2 compact slots; the analytic start adds a φ level (two W0-layout slots)
+  static constexpr int lds_doubles(bool init = false) { return 2 * PLP + (S - 1) * 2 * PLC + (init ? 2 * PLP : 0); }
 };
 
 // + sin tables (error check, analytic start): y and z over the u^n region ± 1, x over the planes the pass touches ± 1.
@@ -348,7 +358,9 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     double Lm[Q][2] = {};    // u^{n−1}
     double Rg[QR][2] = {};   // u^n ring
     const int i0 = x0 - S + 1, i1 = x1 + S - 2;
-    auto lds_plane = [&](int j, int par) { return lds + (j * 2 + par) * PLP; };
+    auto lds_plane = [&](int j, int par) { return lds + par * PLP; };  // (level 0 only)
+    (void)lds_plane;
+    auto lds_cplane = [&](int k, int par) { return lds + 2 * PLP + ((k - 1) * 2 + par) * G::PLC + G::COFF; };
 
     // plane x of u^n: owned positions into L[0][q][slot], ring into Rg[r][rs]
     const int wbase_r = __builtin_amdgcn_readfirstlane(tid & ~63);
@@ -362,7 +374,12 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
           if (g) return g + static_cast<i64>(xs < 0 ? xs + p.pT : xs - p.pnx) * P;
         }
       }
+#ifdef W3D_EXPERIMENT_NOLOAD
+      // (perf attribution only, results wrong: every plane load hits one of 4 cache-resident planes)
+      return (const gdouble*)(fld) + static_cast<i64>(((xs + 1) & 3) + 1) * P;
+#else
       return (const gdouble*)(fld) + static_cast<i64>(xs + 1) * P;
+#endif
     };
     auto load_cur = [&](auto slot_c, auto rs_c, int x, auto bkc) {
       constexpr int slot = decltype(slot_c)::value, rs = decltype(rs_c)::value;
@@ -439,7 +456,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         }
       }
     }
-    auto lds_phi = [&](int par) { return lds + (S * 2 + par) * PLP; };
+    auto lds_phi = [&](int par) { return lds + 2 * PLP + (S - 1) * 2 * G::PLC + par * PLP; };
     // φ of plane x (owned positions and ring) into φ slot `par`
     auto phi_plane = [&](int x, int par) {
       double* d = lds_phi(par);
@@ -488,8 +505,9 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       constexpr int k = decltype(kc)::value, D = decltype(dc)::value;
       constexpr bool BK = decltype(bkc)::value;
       constexpr int sm = (D + 3) & 3, s0 = D, sp = (D + 1) & 3;
-      const double* nb = lds_plane(k - 1, D & 1);
-      double* dst = lds_plane(k < S ? k : 0, D & 1);
+      // stage 1 reads u^n (level 0, W0 layout); later stages read level k − 1 and write level k in compact planes
+      const double* nb = k == 1 ? lds_plane(0, D & 1) : lds_cplane(k > 1 ? k - 1 : 1, D & 1);
+      double* dst = lds_cplane(k < S ? k : 1, D & 1);
       const bool xreal = BK || (xp >= p.sx0 && xp < p.sx1 && inside(p.gx0 + xp));
       const bool xown = BK || (xp >= x0 && xp < x1);
       constexpr bool kChk = (CM >> (k - 1)) & 1;
@@ -518,7 +536,13 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         if (!((wm >> (k - 1)) & 1)) continue;
         const int li = lid[q];
         const double c = L[k - 1][q][s0];
-        const double lap = d2sum(c, L[k - 1][q][sm], L[k - 1][q][sp], nb[li - W0], nb[li + W0], nb[li - 1], nb[li + 1]);
+        double lap;
+        if constexpr (k == 1) {
+          lap = d2sum(c, L[k - 1][q][sm], L[k - 1][q][sp], nb[li - W0], nb[li + W0], nb[li - 1], nb[li + 1]);
+        } else {
+          const int lc = tid + q * NT;  // (compact index: the position itself)
+          lap = d2sum(c, L[k - 1][q][sm], L[k - 1][q][sp], nb[lc - H1], nb[lc + H1], nb[lc - 1], nb[lc + 1]);
+        }
         double o;
         if constexpr (k == 1)
           o = Lm[q][D & 1];
@@ -528,7 +552,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         const double v = (xreal && (gof[q] & kReal)) ? leapfrog(c, o, lap, tau2) : 0.0;
         if constexpr (k < S) {
           L[k][q][s0] = v;
-          dst[li] = v;
+          dst[tid + q * NT] = v;
         }
         const bool own = xown && (g & kOwn);
         if constexpr (k >= S - 1) {

@@ -19,6 +19,7 @@ struct Args {
   bool cpu = false;
   int threads = 0;
   bool overlap = true;
+  bool fused_pack = true;
   bool graph = true;
   bool timers = false;
   bool debug_sync = false;

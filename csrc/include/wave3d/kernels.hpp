@@ -119,6 +119,18 @@ struct TbPush {
   unsigned long long spin_ticks = 0;  // wait bound (100 MHz wall clock)
 };
 
+// Fused z-face pack of a 3-D block pass that precedes an exchange: stages S−1 and S store the owned
+// nodes of the two z-face message parts (deep_plan.hpp: direction (0, 0, ∓1), w = the next pass's depth deep for
+// u^{n+S}, w − 1 for u^{n+S−1}) straight into the send staging next to their field store. The z faces are the strided
+// ones — rows of w ≤ 4 doubles one pitch apart, which a pack kernel reads at a fraction of the copy rate; x / y faces,
+// edges and corners are whole-row copies and stay with k_box_copy. Send-region nodes on the global boundary are never
+// computed and never written: the receiving pass loads the zero slot for them, not their ghosts (kernel `ld`).
+struct TbPack {
+  double* zf[2][2] = {};  // [low / high z face][field 0: u^{n+S}, 1: u^{n+S−1}]: the part in the send staging (or null)
+  int w = 0;              // band width of u^{n+S}; u^{n+S−1}: w − 1
+  int ny = 0, nz = 0;     // owned box
+};
+
 // Stage-real ranges of an LDS pass: per axis, where the intermediate levels hold real values (S−1 nodes into the
 // S-deep ghosts towards neighbouring ranks); lo > hi: the axis default (x: compute box, y/z: no restriction).
 inline LBox tb_default_real() { return LBox{1, 0, 1, 0, 1, 0}; }
@@ -135,7 +147,8 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
                         double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
                         Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream,
                         const LBox& real = tb_default_real(), bool analytic_start = false, int level_stride = 0,
-                        int grid_blocks = 0, const TbPush* push = nullptr, const TbPush* push_dev = nullptr);
+                        int grid_blocks = 0, const TbPush* push = nullptr, const TbPush* push_dev = nullptr,
+                        const TbPack* pack = nullptr, const TbPack* pack_dev = nullptr);
 
 // Error of a stored field vs φ·ct over `box` (step 1 / standalone check). Writes leapfrog-compatible partials and
 // returns how many.
@@ -168,7 +181,8 @@ struct BoxCopyTable {
   BoxJob* jobs = nullptr;  // device
   int njobs = 0, nblocks = 0;
 };
-BoxCopyTable make_box_copy_table(const DeepPlan& plan, bool recv_side);
+// skip_zfaces: leave out the parts of the pure z-face messages (direction (0, 0, ±1)): the pass packs them (TbPack)
+BoxCopyTable make_box_copy_table(const DeepPlan& plan, bool recv_side, bool skip_zfaces = false);
 void free_box_copy_table(BoxCopyTable& t);
 void launch_box_copy(const Layout& l, const BoxCopyTable& t, int mode, double* u_s, double* u_s1, double* buf,
                      hipStream_t stream);

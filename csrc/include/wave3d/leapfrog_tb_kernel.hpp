@@ -71,6 +71,9 @@ struct TbParams {
   int pnx, pT;         // push: this rank's planes, ghost depth
   unsigned ptag;       // push: the tag the table entry must carry
   int pacq;            // push: acquire at the pass start (TbPush::acquire)
+  // fused z-face pack (TbPack; nullptr: none): nodes with z outside [pkza, pkzb) lie in a z send band of width w
+  const TbPack* pk;
+  int pkza, pkzb;
 };
 
 // Push transport memory protocol. The staging is fine-grained device memory (hipDeviceMallocFinegrained; W3D_PUSH_STAGING=
@@ -152,15 +155,19 @@ struct TbGeom {
   static constexpr int COFF = H1 + 1;
   static constexpr int PLC = COFF + NPR + H1 + 1;
   // level 0 × 2 parity slots, levels 1..S−1 × 2 compact slots; the analytic start adds a φ level (two W0-layout slots)
-  static constexpr int lds_doubles(bool init = false) { return 2 * PLP + (S - 1) * 2 * PLC + (init ? 2 * PLP : 0); }
+  static constexpr int lds_planes(bool init) { return 2 * PLP + (S - 1) * 2 * PLC + (init ? 2 * PLP : 0); }
+  // + (fac: checked passes that load u^n) the check's (s_y, s_z) factor pair of every position, compact and thread-
+  // private: position idx = tid + q·NT at pair idx, read at an immediate offset from the thread's own base address
+  static constexpr int lds_doubles(bool init = false, bool fac = false) { return lds_planes(init) + (fac ? 2 * NP : 0); }
+  static_assert(lds_planes(false) % 2 == 0 && lds_planes(true) % 2 == 0, "factor pairs must be 16-B aligned");
 };
 
 // + sin tables (error check, analytic start): y and z over the u^n region ± 1, x over the planes the pass touches ± 1.
 // In LDS because a global load of the per-plane x factor would be a vector load (the table may alias the outputs, so
 // no scalar load) whose wait drains the prefetch queue. nxo = tb_nx_table(x1 − x0) or 0 (no table needed).
-template <int S, int T, int NT, bool INIT = false>
+template <int S, int T, int NT, bool INIT = false, bool FAC = false>
 constexpr size_t tb_lds_bytes(int nxo = 0) {
-  return (static_cast<size_t>(TbGeom<S, T, NT>::lds_doubles(INIT)) + (2 + 2 * S) * (T + 2 * S + 2) +
+  return (static_cast<size_t>(TbGeom<S, T, NT>::lds_doubles(INIT, FAC)) + (2 + 2 * S) * (T + 2 * S + 2) +
           static_cast<size_t>(nxo)) *
          sizeof(double);
 }
@@ -183,6 +190,10 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
   constexpr int kReal = 1 << 29;  // gof flag: stage values are real at this node (interior ∩ stage-real range)
   constexpr int kLd = 1 << 28;    // gof flag: node inside the global interior and the allocation (loaded)
   constexpr int kOff = kLd - 1;   // gof bits of the in-plane offset
+  // the check's per-position (s_y, s_z) pairs in LDS (TbGeom::lds_doubles): a checked node then costs one LDS read and
+  // the check's own f64 operations; recomputing the table indices from the position (divisions by W0, clamps, address
+  // arithmetic) cost more VALU instructions than the check itself, and at S = 4 no registers are left to hold them
+  constexpr bool kFac = CM != 0 && !INIT;
   extern __shared__ double lds[];
   const int tid = static_cast<int>(threadIdx.x);
   int blk = static_cast<int>(blockIdx.x);
@@ -202,6 +213,8 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     tzi = (x - (x / nbz) * nbz) * p.bbz + (w - (w / p.bbz) * p.bbz);
   }
   const int ty0 = p.y0 + tyi * T, tz0 = p.z0 + tzi * T;
+  // fused z-face pack: this tile's owned nodes reach into a z send band (wave-uniform)
+  const bool pk_tile = p.pk != nullptr && (tz0 < p.pkza || imin(tz0 + T, p.z1) > p.pkzb);
   const int wx0 = CH ? p.x0 + chunk * p.xlen : p.x0;  // this block's output x range
   const int wx1 = CH ? imin(p.x1, wx0 + p.xlen) : p.x1;
   const int N = p.N;
@@ -291,7 +304,8 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     // sin tables: syw[j] = s[y] for y = ty0 − S − 1 + j (the u^n region ± 1), szw likewise, sxw[i] = s[x] for
     // x = x0 − S − 1 + i; indices clamped into −1..N+1 (only nodes of the interior, and their neighbours, use them)
     constexpr int NYW = T + 2 * S + 2;
-    double* syw = lds + G::lds_doubles(INIT);
+    double* syw = lds + G::lds_doubles(INIT, kFac);
+    double2* fac = reinterpret_cast<double2*>(lds + G::lds_planes(INIT));  // (kFac)
     double* szw = syw + NYW;
     double* rowt = szw + NYW;  // per checked level, two plane-parity slots of NYW row factors s_x·s_y
     double* sxw = rowt + 2 * S * NYW;
@@ -304,6 +318,11 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       static_assert(offsetof(TbPush, gcur) == offsetof(TbPush, fwd1) + 6 * sizeof(void*), "TbPush pointer block");
       if (tid < 8) pbk[tid] = reinterpret_cast<const volatile unsigned long long*>(&p.push->fwd1[0])[tid];
     }
+    // fused z-face pack: the TbPack block (4 staging pointers, w, ny, nz) likewise in LDS, read where used (a global
+    // load there would wait behind the prefetch queue); first read after the march's first barrier
+    unsigned long long* pkb = pbk + (PUSH ? 8 : 0);
+    static_assert(sizeof(TbPack) == 6 * sizeof(unsigned long long), "TbPack block");
+    if (p.pk != nullptr && tid < 6) pkb[tid] = reinterpret_cast<const volatile unsigned long long*>(p.pk)[tid];
     if (p.check_mask || INIT || PUSH) {
       auto sc = [&](int g) { return p.s[g < -1 ? -1 : g > N + 1 ? N + 1 : g]; };
       for (int t = tid; t < NYW && (p.check_mask || INIT); t += NT) {
@@ -314,11 +333,19 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         for (int i = tid; i < tb_nx_table<S>(wx1 - wx0); i += NT) sxw[i] = sc(p.gx0 + wx0 - S - 1 + i);
       __syncthreads();
     }
+    (void)fac;
     // table indices of an LDS position li (u^n-region coordinates): y ↔ li / W0 + 1, z ↔ li % W0 + 1 (the pad's dummy
     // node is clamped into the table)
     auto ytab = [&](int li) { return imin(li / W0 + 1, W0); };
     auto ztab = [&](int li) { return li - (li / W0) * W0 + 1; };
     const int xtab0 = S + 1 - wx0;  // x ↔ sxw[x + xtab0]
+    if constexpr (kFac) {
+      if (p.check_mask) {  // (each thread writes and later reads only its own pairs: no barrier)
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+          if (tid + q * NT < G::NP) fac[tid + q * NT] = make_double2(syw[ytab(lid[q])], szw[ztab(lid[q])]);
+      }
+    }
     // staging pointer i of the pass (0, 1: fwd1 lo/hi; 2, 3: fwd2; 4, 5: gprev; 6, 7: gcur), wave-uniform
     auto push_ptr = [&](int i) -> gdouble* {
       typedef __attribute__((address_space(3))) const volatile unsigned long long lds_u64;  // (a ds_read, not FLAT)
@@ -441,7 +468,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     auto fzq = [&](int q) { return kFacReg ? fz[q] : szw[ztab(lid[q])]; };
     auto fyrr = [&](int r) { return kFacReg ? fyr[r] : syw[ytab(lrid[r])]; };
     auto fzrr = [&](int r) { return kFacReg ? fzr[r] : szw[ztab(lrid[r])]; };
-    if constexpr ((INIT || CM != 0) && kFacReg) {
+    if constexpr ((INIT || (CM != 0 && !kFac)) && kFacReg) {
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         yix[q] = ytab(lid[q]);
@@ -499,6 +526,30 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       }
     };
 
+    // fused z-face pack (TbPack): an owned node of field f (0: u^{n+S}, 1: u^{n+S−1}) in the low / high z band of
+    // width w − f goes to its place in that face's message part (C order (x, y, z) over nx × ny × (w − f))
+    auto pack_store = [&](int f, int x, int idx, double v) {
+      const int a = idx / H1;
+      const int z = tz0 - (S - 1) + (idx - a * H1);
+      if (z >= p.pkza && z < p.pkzb) return;  // (outside both bands of width w ⊇ w − 1: no LDS read)
+      typedef __attribute__((address_space(3))) const volatile unsigned long long lds_u64;  // (a ds_read, not FLAT)
+      const unsigned long long wy = ((lds_u64*)pkb)[4];  // w | ny << 32
+      const int ny = static_cast<int>(wy >> 32), nz = static_cast<int>(((lds_u64*)pkb)[5] & 0xFFFFFFFFu);
+      const int wf = static_cast<int>(wy & 0xFFFFFFFFu) - f;
+      const int y = ty0 - (S - 1) + a;
+      // staging part of face `side`, field f (the same in every lane: no readfirstlane, whose scalar result would make
+      // the wave wait for all its outstanding LDS reads; null: no neighbour on that side)
+      auto part = [&](int side) { return (gdouble*)(((lds_u64*)pkb)[side * 2 + f]); };
+      if (z < wf) {
+        gdouble* d = part(0);
+        if (d) d[(x * ny + y) * wf + z] = v;
+      }
+      if (z >= nz - wf) {
+        gdouble* d = part(1);
+        if (d) d[(x * ny + y) * wf + z - (nz - wf)] = v;
+      }
+    };
+
     // stage k at plane xp; D = (xp − i0) & 3 (static), parity of xp = D & 1
     // BK (bulk): plane xp is real and owned for every stage (the x tests are compile-time true)
     auto stage = [&](auto kc, auto dc, auto bkc, int xp) {
@@ -513,9 +564,16 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       constexpr bool kChk = (CM >> (k - 1)) & 1;
       const bool chk = kChk && ((p.check_mask >> (k - 1)) & 1);
       double* outp = (k == S ? p.out2 : p.out1) + static_cast<i64>(xp + 1) * P;
-      // the check's (s_x·s_y) row factor of plane xp, tabulated one iteration ahead (row_tables), slot F & 1
+      // the check's (s_x·s_y) row factor of plane xp, tabulated one iteration ahead (row_tables), slot F & 1 (!kFac);
+      // kFac: s_x of plane xp (wave-uniform), times each position's s_y from its factor pair
       const double* rowk = rowt + ((k - 1) * 2 + ((D + k - 1) & 1)) * NYW;
+      double sxk = 0.0;
+      if constexpr (kFac && kChk)
+        if (chk) sxk = sxw[xp + xtab0];
+      (void)sxk;
       (void)xown;
+      // fused z-face pack: stages S−1 and S of a tile next to a z face (scalar test)
+      const bool pks = k >= S - 1 && pk_tile;
       // push transport: the face planes a neighbour reads as ghosts (u^{n+S}: T deep, u^{n+S−1}: T − 1 deep) also go
       // straight into its staging; the plane's destination is found once per stage (scalar), not per position
       gdouble* fwd = nullptr;
@@ -558,14 +616,21 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         if constexpr (k >= S - 1) {
           if (own && xreal) {
             __builtin_nontemporal_store(v, outp + (g & kOff));
+            if (pks) pack_store(k == S ? 0 : 1, xp, tid + q * NT, v);
             if constexpr (PUSH && !BK)
               if (fwd) __hip_atomic_store(fwd + (g & kOff), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           }
         }
         if constexpr (kChk) {
           if (chk && own && xreal) {
-            const double e = fabs(v - (rowk[kFacReg ? yix[q] : ytab(li)] * (kFacReg ? fz[q] : szw[ztab(li)])) *
-                                          p.ct[k - 1]);
+            double a;
+            if constexpr (kFac) {
+              const double2 f = fac[tid + q * NT];
+              a = ((sxk * f.x) * f.y) * p.ct[k - 1];
+            } else {
+              a = (rowk[kFacReg ? yix[q] : ytab(li)] * (kFacReg ? fz[q] : szw[ztab(li)])) * p.ct[k - 1];
+            }
+            const double e = fabs(v - a);
             emax[k - 1] = fmax(e, emax[k - 1]);  // = (e > m ? e : m) for every non-NaN e; a NaN shows in the sum
             esum[k - 1] += e * e;
           }
@@ -577,7 +642,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
     // ((s_x·s_y)·s_z)·ct (same operands and order: bit-identical), tabulated once per plane by the first NYW threads
     // instead of once per node; iteration i fills slot ((i − i0) + 1) & 1 for the planes its successor checks
     auto row_tables = [&](int i, int slot) {
-      if constexpr (CM != 0) {
+      if constexpr (CM != 0 && !kFac) {
         if (p.check_mask && tid < NYW) {
 #pragma unroll
           for (int k = 1; k <= S; ++k)
@@ -826,7 +891,8 @@ constexpr size_t max_dyn_lds() {
 // returns that limit
 template <int S, int NT, int CM, bool INIT, bool CH, bool PUSH>
 size_t prepare_cfg() {
-  static_assert(tb_lds_bytes<S, kTile, NT, INIT>() <= max_dyn_lds<NT>(), "leapfrog_tb tile does not fit in LDS");
+  static_assert(tb_lds_bytes<S, kTile, NT, INIT, (CM != 0 && !INIT)>() <= max_dyn_lds<NT>(),
+                "leapfrog_tb tile does not fit in LDS");
   static const size_t limit = [] {
     const void* fn = reinterpret_cast<const void*>(k_leapfrog_tb<S, kTile, NT, CM, INIT, CH, PUSH>);
     hipFuncAttributes fa{};
@@ -842,8 +908,10 @@ size_t prepare_cfg() {
 
 template <int S, int NT, int CM, bool INIT, bool PUSH>
 void launch_cfg(const TbParams& p, int nblocks, hipStream_t st) {
-  const size_t shmem = tb_lds_bytes<S, kTile, NT, INIT>((p.check_mask || INIT) ? tb_nx_table<S>(p.xlen) : 0) +
-                       (PUSH ? 8 * sizeof(unsigned long long) : 0);  // (the push block: staging pointers)
+  const size_t shmem = tb_lds_bytes<S, kTile, NT, INIT, (CM != 0 && !INIT)>(
+                           (p.check_mask || INIT) ? tb_nx_table<S>(p.xlen) : 0) +
+                       (PUSH ? 8 * sizeof(unsigned long long) : 0) +  // (the push block: staging pointers)
+                       sizeof(TbPack);                                 // (the fused-pack block)
   if (p.nxc > 1) {
     const size_t lim = prepare_cfg<S, NT, CM, INIT, true, PUSH>();
     W3D_REQUIRE(shmem <= lim, "leapfrog_tb: too many planes for the LDS sin table");

@@ -65,11 +65,13 @@ struct SolverOptions {
   bool push = false;
   // Copy-engine ("sdma") transport (deep-tb slab and block ranks): the halo regions are copied into the neighbours'
   // memory (IPC-mapped: their field buffers' ghost planes for slabs, their staging buffers for blocks) by
-  // hipMemcpyAsync(..., hipMemcpyDeviceToDeviceNoCU) on the side stream — the SDMA engines move them, no compute unit
-  // is taken from the LDS passes — and cross-rank order is kept by flag words in uncached device memory, written and
-  // waited for by the command processors (hipStreamWriteValue32 / hipStreamWaitValue32, graph-capturable on HIP 7.2).
-  // See transport_sdma.cpp for the protocol.
+  // hipMemcpyAsync(..., hipMemcpyDeviceToDeviceNoCU) on copy streams — the SDMA engines move them, no compute unit is
+  // taken from the LDS passes — and cross-rank order is kept by flag words in uncached device memory (waits: one-
+  // workgroup kernels; "arrived": a 4-byte copy-engine write behind the data). See transport_sdma.cpp for the protocol.
   bool sdma = false;
+  // 3-D block LDS passes: the pass stores the z-face message parts of the next exchange straight into the send staging
+  // (TbPack, kernels.hpp); the pack kernel then copies only the x / y faces, edges and corners (A/B: --no-fused-pack)
+  bool fused_pack = true;
   // deep-tb with overlap: the shell boxes run on the side stream concurrently with the interior (true), or on s0 before
   // it (false: they get the whole GPU and finish first, so the exchange starts earlier — measured faster with the copy
   // engines at 512³ and 2048³; concurrent helps the small block shells when no transfer follows; env W3D_SHELLS)
@@ -275,6 +277,8 @@ class GpuSolver {
   bool block_tb_ = false;         // deep-tb on a 3-D block decomposition (S-deep ghosts on every split axis)
   DeepPlan deep_[5];              // block_tb_: exchange plan before a pass of s steps (index s = 2..temporal)
   BoxCopyTable pack_tab_[5], unpack_tab_[5];  // ... and its device job tables (send / receive regions)
+  TbPack pk_host_[5];                          // fused z-face pack per exchange depth (fused_pack; w = 0: none)
+  TbPack* pk_dev_ = nullptr;                   // ... the same five entries in device memory
   i64 deep_max_ = 0;              // largest staging buffer of those plans (doubles)
   int deep_s_ = 2;                // depth of the exchange being issued
   std::vector<int> n_dshell_;     // partials per deep shell launch

@@ -437,6 +437,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("push_cp_wait", &SolverOptions::push_cp_wait)
       .def_readwrite("sdma", &SolverOptions::sdma)
       .def_readwrite("shells_concurrent", &SolverOptions::shells_concurrent)
+      .def_readwrite("fused_pack", &SolverOptions::fused_pack)
       .def_readwrite("sdma_streams", &SolverOptions::sdma_streams)
       .def_readwrite("push_no_collective", &SolverOptions::push_no_collective)
       .def_readwrite("temporal", &SolverOptions::temporal)

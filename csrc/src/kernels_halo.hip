@@ -126,11 +126,12 @@ __global__ __launch_bounds__(kBoxThreads) void k_box_copy(const BoxCopyParams p)
 
 }  // namespace
 
-BoxCopyTable make_box_copy_table(const DeepPlan& plan, bool recv_side) {
+BoxCopyTable make_box_copy_table(const DeepPlan& plan, bool recv_side, bool skip_zfaces) {
   std::vector<BoxJob> jobs;
   int blk = 0;
   for (const DeepPeer& q : plan.peers)
     for (const DeepPart& part : q.parts) {
+      if (skip_zfaces && q.dir[0] == 0 && q.dir[1] == 0) continue;
       const LBox& b = recv_side ? part.recv : part.send;
       const i64 cnt = b.count();
       if (cnt == 0) continue;

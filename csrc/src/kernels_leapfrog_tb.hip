@@ -83,7 +83,7 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
                         double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
                         Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, const LBox& real,
                         bool analytic_start, int level_stride, int grid_blocks, const TbPush* push,
-                        const TbPush* push_dev) {
+                        const TbPush* push_dev, const TbPack* pack, const TbPack* pack_dev) {
   W3D_REQUIRE(out1 != out2 && (analytic_start || (prev != out1 && prev != out2 && cur != out1 && cur != out2)),
               "leapfrog_tb needs four distinct buffers");
   TbPlan pl = make_plan_tb(l, box, t, real);
@@ -100,6 +100,13 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
     p.pT = push->T;
     p.ptag = push->tag;
     p.pacq = push->acquire;
+  }
+  if (pack != nullptr) {  // fused z-face pack: the host copy gives the band limits, the kernel reads the rest on use
+    W3D_REQUIRE(pack_dev != nullptr && pack->w >= 2 && pack->w <= kTile && pack->ny == l.ny && pack->nz == l.nz,
+                "leapfrog_tb pack: bad parameters");
+    p.pk = pack_dev;
+    p.pkza = pack->zf[0][0] ? pack->w : 0;
+    p.pkzb = pack->zf[1][0] ? pack->nz - pack->w : pack->nz;
   }
   // a padded grid (several launches sharing one level's partial slots, each of grid_blocks entries): the extra
   // workgroups have no tile and write (0, 0) partials, so every slot entry a reduction reads is written

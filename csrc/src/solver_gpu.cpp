@@ -146,6 +146,11 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
       loopback_(loopback) {
   prob_.validate();
   W3D_HIP(hipGetDevice(&dev_));
+  // (perf studies: tiling overrides of the LDS S-step kernel; W3D_TB_TARGET=B splits the x march into chunks when the
+  // tile grid has fewer than B tiles, W3D_TB_MINCHUNK its minimum planes, W3D_TB_XCDBLOCKS=1 square XCD blocks)
+  if (const char* v = std::getenv("W3D_TB_TARGET")) opt_.tiling_tb.target_blocks = std::atoi(v);
+  if (const char* v = std::getenv("W3D_TB_MINCHUNK")) opt_.tiling_tb.min_chunk = std::atoi(v);
+  if (const char* v = std::getenv("W3D_TB_XCDBLOCKS")) opt_.tiling_tb.xcd_blocks = *v == '1';
   W3D_REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
   W3D_REQUIRE(world == 1 || comm_ || loopback_ || opt_.fake_comm || ((opt_.push || opt_.sdma) && opt_.push_no_collective),
               "world > 1 needs an RCCL communicator (or the loopback group, or the push / sdma transport without one)");
@@ -322,13 +327,30 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   if (stage > 0) {
     W3D_HIP(hipMalloc(&send_buf_, static_cast<size_t>(stage) * sizeof(double)));
     W3D_HIP(hipMalloc(&recv_buf_, static_cast<size_t>(stage) * sizeof(double)));
+    W3D_HIP(hipMemset(send_buf_, 0, static_cast<size_t>(stage) * sizeof(double)));
   }
   if (sdma_) sdma_alloc();
-  if (block_tb_)
+  if (block_tb_) {
+    // fused z-face pack (its message parts live in send_buf_, zeroed once: nodes on the global boundary are never
+    // written and never read, see TbPack)
+    const bool fused = opt_.fused_pack && opt_.tb;
     for (int st = 2; st <= opt_.temporal; ++st) {
-      pack_tab_[st] = make_box_copy_table(deep_[st], false);
+      pack_tab_[st] = make_box_copy_table(deep_[st], false, fused);
       unpack_tab_[st] = make_box_copy_table(deep_[st], true);
+      if (!fused) continue;
+      TbPack& k = pk_host_[st];
+      k.w = st;
+      k.ny = static_cast<int>(lay_.ny);
+      k.nz = static_cast<int>(lay_.nz);
+      for (const DeepPeer& q : deep_[st].peers)
+        if (q.dir[0] == 0 && q.dir[1] == 0)
+          for (const DeepPart& part : q.parts) k.zf[q.dir[2] > 0 ? 1 : 0][part.field] = send_buf_ + q.buf_off + part.off;
     }
+    if (fused) {
+      W3D_HIP(hipMalloc(&pk_dev_, sizeof(pk_host_)));
+      W3D_HIP(hipMemcpy(pk_dev_, pk_host_, sizeof(pk_host_), hipMemcpyHostToDevice));
+    }
+  }
   n_full_ = leapfrog_blocks(lay_, &full_, 1, opt_.tiling);
   n_shell_ = leapfrog_blocks(lay_, shell_.data(), static_cast<int>(shell_.size()), opt_.tiling);
   n_int_ = leapfrog_blocks(lay_, &interior_, 1, opt_.tiling);
@@ -385,6 +407,7 @@ GpuSolver::~GpuSolver() {
   if (xfork_) (void)hipEventDestroy(xfork_);
   for (BoxCopyTable& t : pack_tab_) free_box_copy_table(t);
   for (BoxCopyTable& t : unpack_tab_) free_box_copy_table(t);
+  if (pk_dev_) (void)hipFree(pk_dev_);
   for (double* p : {u_[0], u_[1], u_[2], u_[3], d_s_, send_buf_, recv_buf_})
     if (p) (void)hipFree(p);
   if (partials_) (void)hipFree(partials_);
@@ -797,10 +820,13 @@ void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase, hipStream_t s
         if (qh->wait_side[side] && qh->cp_wait > 0)
           W3D_HIP(hipStreamWaitValue32(s0_, flags_ + side, qh->cp_wait, hipStreamWaitValueGte, 0xFFFFFFFFu));
   }
+  // fused z-face pack of the exchange that follows this unit (its depth: deep_s_, set by build_msgs before the passes)
+  const bool pk = pk_dev_ != nullptr && needs_exchange(cur_unit_) && pk_host_[deep_s_].w == deep_s_;
   timed(phase, st, [&] {
     // (every launch fills its whole slot of n_tb_ partials: shell and interior boxes may have fewer x chunks)
     launch_leapfrog_tb(lay_, coef_, u_[old_], u_[cur_], u_[uf_[0]], u_[uf_[1]], box, d_s_ + 1, cts, mask, part, t,
-                       st, real, u.analytic, slots * n_tb_, n_tb_, qh, qd);
+                       st, real, u.analytic, slots * n_tb_, n_tb_, qh, qd, pk ? &pk_host_[deep_s_] : nullptr,
+                       pk ? pk_dev_ + deep_s_ : nullptr);
   });
   if (mask) ++tb_slots_;
 }

@@ -93,7 +93,7 @@ class Solver:
                  tiling_tb: dict | None = None,
                  debug_sync: bool = False, poison_ghosts: bool = False, deep_min_planes: int | None = None,
                  tb_min_planes: int | None = None, rccl: bool = True, autotune: bool = False,
-                 autotune_rounds: int = 5, copy_engines: bool = False):
+                 autotune_rounds: int = 5, copy_engines: bool = False, fused_pack: bool = True):
         import torch.distributed as dist
 
         if not spec.cfl_ok and not force:
@@ -121,6 +121,7 @@ class Solver:
         if self.backend == "hip" and self.transport in ("loopback", "rccl-self", "push", "sdma", "multi-device"):
             opts = self._options(C, decomp, spec, overlap, graph, tiling, temporal, tiling2, init2, tb, tiling_tb)
             opts.timers, opts.debug_sync, opts.poison_ghosts = timers, debug_sync, poison_ghosts
+            opts.fused_pack = fused_pack
             if deep_min_planes is not None:
                 opts.deep_min_planes = deep_min_planes
             if tb_min_planes is not None:
@@ -133,6 +134,7 @@ class Solver:
 
             opts = self._options(C, decomp, spec, overlap, graph, tiling, temporal, tiling2, init2, tb, tiling_tb)
             opts.timers, opts.debug_sync, opts.poison_ghosts = timers, debug_sync, poison_ghosts
+            opts.fused_pack = fused_pack
             if deep_min_planes is not None:
                 opts.deep_min_planes = deep_min_planes
             if tb_min_planes is not None:

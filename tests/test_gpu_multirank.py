@@ -279,3 +279,24 @@ def test_block_overlap_geometries(gpu, world, decomp, N, transport):
         r = g.run()
         _same(r, r1)
         assert torch.equal(g.global_field(0), f0)
+
+
+@pytest.mark.parametrize("transport", ["loopback", "rccl-self", "sdma"])
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("world,decomp,N,overlap", [(8, "2x2x2", 70, True), (4, "1x2x2", 66, False),
+                                                    (12, "3x2x2", 100, True), (27, "3x3x3", 100, False)])
+def test_block_fused_zface_pack(gpu, world, decomp, N, overlap, transport, fused):
+    """The z-face message parts are written by the pass itself (TbPack) or, with fused_pack=False,
+    gathered by the pack kernel like the x / y faces: both bit-identical to one GPU with NaN-poisoned ghosts (a z-face
+    node the pass failed to store would arrive as a stale value of an earlier pass)."""
+    spec = ProblemSpec(N=N, tau=1e-3, K=20)
+    ref = Solver(spec, backend="hip", device=0, temporal=1)
+    r1 = ref.run()
+    f0 = ref.global_field(0)
+    g = Solver(spec, backend="hip", transport=transport, world=world, rank=0, decomp=decomp, device=0,
+               overlap=overlap, poison_ghosts=transport != "rccl-self", fused_pack=fused)
+    assert g.native.mode() == "deep-tb-block"
+    for _ in range(2):
+        r = g.run()
+        _same(r, r1)
+        assert torch.equal(g.global_field(0), f0)

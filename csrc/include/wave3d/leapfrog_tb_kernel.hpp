@@ -156,7 +156,7 @@ struct TbGeom {
   static constexpr int PLC = COFF + NPR + H1 + 1;
   // level 0 × 2 parity slots, levels 1..S−1 × 2 compact slots; the analytic start adds a φ level (two W0-layout slots)
   static constexpr int lds_planes(bool init) { return 2 * PLP + (S - 1) * 2 * PLC + (init ? 2 * PLP : 0); }
-  // + (fac: checked passes that load u^n) the check's (s_y, s_z) factor pair of every position, compact and thread-
+  // + (fac: checked passes that load u^n) the check's (s_z, row index) pair of every position, compact and thread-
   // private: position idx = tid + q·NT at pair idx, read at an immediate offset from the thread's own base address
   static constexpr int lds_doubles(bool init = false, bool fac = false) { return lds_planes(init) + (fac ? 2 * NP : 0); }
   static_assert(lds_planes(false) % 2 == 0 && lds_planes(true) % 2 == 0, "factor pairs must be 16-B aligned");
@@ -190,9 +190,10 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
   constexpr int kReal = 1 << 29;  // gof flag: stage values are real at this node (interior ∩ stage-real range)
   constexpr int kLd = 1 << 28;    // gof flag: node inside the global interior and the allocation (loaded)
   constexpr int kOff = kLd - 1;   // gof bits of the in-plane offset
-  // the check's per-position (s_y, s_z) pairs in LDS (TbGeom::lds_doubles): a checked node then costs one LDS read and
-  // the check's own f64 operations; recomputing the table indices from the position (divisions by W0, clamps, address
-  // arithmetic) cost more VALU instructions than the check itself, and at S = 4 no registers are left to hold them
+  // the check's per-position (s_z, row-table index) pairs in LDS (TbGeom::lds_doubles): a checked node then costs one
+  // pair read, one row-factor read and the check's own f64 operations (one product, difference, max, fma); recomputing
+  // the table indices from the position (divisions by W0, clamps, address arithmetic) cost more VALU instructions than
+  // the check itself, and at S = 4 no registers are left to hold them
   constexpr bool kFac = CM != 0 && !INIT;
   extern __shared__ double lds[];
   const int tid = static_cast<int>(threadIdx.x);
@@ -343,7 +344,8 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       if (p.check_mask) {  // (each thread writes and later reads only its own pairs: no barrier)
 #pragma unroll
         for (int q = 0; q < Q; ++q)
-          if (tid + q * NT < G::NP) fac[tid + q * NT] = make_double2(syw[ytab(lid[q])], szw[ztab(lid[q])]);
+          if (tid + q * NT < G::NP)
+            fac[tid + q * NT] = make_double2(szw[ztab(lid[q])], __longlong_as_double(ytab(lid[q])));
       }
     }
     // staging pointer i of the pass (0, 1: fwd1 lo/hi; 2, 3: fwd2; 4, 5: gprev; 6, 7: gcur), wave-uniform
@@ -564,13 +566,8 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       constexpr bool kChk = (CM >> (k - 1)) & 1;
       const bool chk = kChk && ((p.check_mask >> (k - 1)) & 1);
       double* outp = (k == S ? p.out2 : p.out1) + static_cast<i64>(xp + 1) * P;
-      // the check's (s_x·s_y) row factor of plane xp, tabulated one iteration ahead (row_tables), slot F & 1 (!kFac);
-      // kFac: s_x of plane xp (wave-uniform), times each position's s_y from its factor pair
+      // the check's row factor (s_x·s_y)·ct of plane xp, tabulated one iteration ahead (row_tables), slot F & 1
       const double* rowk = rowt + ((k - 1) * 2 + ((D + k - 1) & 1)) * NYW;
-      double sxk = 0.0;
-      if constexpr (kFac && kChk)
-        if (chk) sxk = sxw[xp + xtab0];
-      (void)sxk;
       (void)xown;
       // fused z-face pack: stages S−1 and S of a tile next to a z face (scalar test)
       const bool pks = k >= S - 1 && pk_tile;
@@ -615,7 +612,9 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         const bool own = xown && (g & kOwn);
         if constexpr (k >= S - 1) {
           if (own && xreal) {
+#ifndef W3D_EXPERIMENT_NOSTORE  // (perf attribution only, results wrong: the pass writes nothing to HBM)
             __builtin_nontemporal_store(v, outp + (g & kOff));
+#endif
             if (pks) pack_store(k == S ? 0 : 1, xp, tid + q * NT, v);
             if constexpr (PUSH && !BK)
               if (fwd) __hip_atomic_store(fwd + (g & kOff), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -623,31 +622,33 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         }
         if constexpr (kChk) {
           if (chk && own && xreal) {
+            // u_a = ((s_x·s_y)·ct)·s_z (stencil.hpp::analytic_row): one product per node
             double a;
             if constexpr (kFac) {
-              const double2 f = fac[tid + q * NT];
-              a = ((sxk * f.x) * f.y) * p.ct[k - 1];
+              const double2 f = fac[tid + q * NT];  // (s_z, row-table index)
+              a = rowk[static_cast<int>(__double_as_longlong(f.y))] * f.x;
             } else {
-              a = (rowk[kFacReg ? yix[q] : ytab(li)] * (kFacReg ? fz[q] : szw[ztab(li)])) * p.ct[k - 1];
+              a = rowk[kFacReg ? yix[q] : ytab(li)] * (kFacReg ? fz[q] : szw[ztab(li)]);
             }
             const double e = fabs(v - a);
             emax[k - 1] = fmax(e, emax[k - 1]);  // = (e > m ? e : m) for every non-NaN e; a NaN shows in the sum
-            esum[k - 1] += e * e;
+            esum[k - 1] = err_sq_acc(e, esum[k - 1]);
           }
         }
       }
     };
 
-    // check row factors: rowt[k][slot][j] = s_x(plane of stage k) · s_y(j), the first product of the check's
-    // ((s_x·s_y)·s_z)·ct (same operands and order: bit-identical), tabulated once per plane by the first NYW threads
-    // instead of once per node; iteration i fills slot ((i − i0) + 1) & 1 for the planes its successor checks
+    // check row factors: rowt[k][slot][j] = (s_x(plane of stage k) · s_y(j))·ct_k, the row factor of the check's
+    // ((s_x·s_y)·ct)·s_z (stencil.hpp::analytic_row, same operands and order: bit-identical), tabulated once per plane
+    // by the first NYW threads instead of once per node; iteration i fills slot ((i − i0) + 1) & 1 for the planes its
+    // successor checks
     auto row_tables = [&](int i, int slot) {
-      if constexpr (CM != 0 && !kFac) {
+      if constexpr (CM != 0) {
         if (p.check_mask && tid < NYW) {
 #pragma unroll
           for (int k = 1; k <= S; ++k)
             if (((CM & p.check_mask) >> (k - 1)) & 1)
-              rowt[((k - 1) * 2 + slot) * NYW + tid] = sxw[imax(i - (k - 1) + xtab0, 0)] * syw[tid];
+              rowt[((k - 1) * 2 + slot) * NYW + tid] = analytic_row(sxw[imax(i - (k - 1) + xtab0, 0)], syw[tid], p.ct[k - 1]);
         }
       }
     };

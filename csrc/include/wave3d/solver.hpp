@@ -279,7 +279,9 @@ class GpuSolver {
   BoxCopyTable pack_tab_[5], unpack_tab_[5];  // ... and its device job tables (send / receive regions)
   TbPack pk_host_[5];                          // fused z-face pack per exchange depth (fused_pack; w = 0: none)
   TbPack* pk_dev_ = nullptr;                   // ... the same five entries in device memory
-  i64 deep_max_ = 0;              // largest staging buffer of those plans (doubles)
+  i64 deep_max_ = 0;              // largest staging buffer of those plans (doubles): the receive staging
+  i64 sbase_[5] = {};             // send staging: the region of depth s starts at sbase_[s] (one region per depth)
+  i64 send_total_ = 0;            // ... and its size (doubles)
   int deep_s_ = 2;                // depth of the exchange being issued
   std::vector<int> n_dshell_;     // partials per deep shell launch
   int n_dint_ = 0;

@@ -5,6 +5,8 @@
 // domain decomposition (the reference's "1-GPU log == 2-GPU log" property, report.pdf p.15-16 §4.3.1-4.3.2).
 #pragma once
 
+#include <cmath>
+
 #include "wave3d/common.hpp"
 
 namespace wave3d {
@@ -29,16 +31,40 @@ W3D_HD double d2sum(double c, double xm, double xp, double ym, double yp, double
 }
 
 // Leapfrog update u^{n+1} = 2u^n − u^{n−1} + τ² Δ_h u^n (report.pdf p.5 §2.2(3)), with s = d2sum and lam = τ²/h².
+// The τ²-term is fused: (2c − old) + lam·s rounded once (one v_fma_f64: 10 instead of 11 f64 operations per node and
+// step). Host and device round identically (std::fma is the IEEE fused operation); the printed 128³ / 512³ logs keep
+// every digit of the reference's (checked for N = 128, 256, 512 and L = 1, π: profiles/r3/fma_forms.md).
 W3D_HD double leapfrog(double c, double old, double s, double lam) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_fma(2.0, c, -old) + lam * s;
+  return __builtin_fma(lam, s, __builtin_fma(2.0, c, -old));
 #else
-  return (2.0 * c - old) + lam * s;
+  return std::fma(lam, s, 2.0 * c - old);
 #endif
 }
 
 // Second-order first step u^1 = u^0 + τ²/2 Δ_h u^0, using ∂u/∂t = 0 (report.pdf p.5 §2.2(2)); half_lam = τ²/(2h²).
-W3D_HD double first_step(double c, double s, double half_lam) { return c + half_lam * s; }
+// (fused like leapfrog)
+W3D_HD double first_step(double c, double s, double half_lam) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_fma(half_lam, s, c);
+#else
+  return std::fma(half_lam, s, c);
+#endif
+}
+
+// IEEE fused multiply-add on the host (bindings: the numpy emulators' rounding primitive)
+inline double fma_exact(double a, double b, double c) { return std::fma(a, b, c); }
+
+// The error check's analytic value u_a = φ·cos(a_t t) at a node: ((s_x·s_y)·ct)·s_z. The row factor (s_x·s_y)·ct is
+// shared by a whole z row (one product per node), and the squared error is accumulated with one fma (err_acc).
+W3D_HD double analytic_row(double sx, double sy, double ct) { return (sx * sy) * ct; }
+W3D_HD double err_sq_acc(double e, double acc) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_fma(e, e, acc);
+#else
+  return std::fma(e, e, acc);
+#endif
+}
 
 // φ at a global node from the separable table (boundary entries are exact zeros, see problem.hpp::sin_table).
 W3D_HD double phi(const double* s, i64 gi, i64 gj, i64 gk) { return (s[gi] * s[gj]) * s[gk]; }

@@ -13,6 +13,7 @@
 #include "wave3d/problem.hpp"
 #include "wave3d/runtime.hpp"
 #include "wave3d/solver.hpp"
+#include "wave3d/stencil.hpp"
 
 namespace py = pybind11;
 using namespace wave3d;
@@ -113,6 +114,16 @@ PYBIND11_MODULE(_C, m) {
     return darr(static_cast<py::ssize_t>(v.size()), v.data());
   });
   m.def("time_factor", &time_factor);
+  // elementwise IEEE fused multiply-add (the rounding of stencil.hpp's leapfrog / first_step / err_sq_acc), for the
+  // numpy emulators that must reproduce the kernels bit for bit (numpy has no fma)
+  m.def("fma_array", [](const darr& a, const darr& b, const darr& c) {
+    W3D_REQUIRE(a.size() == b.size() && a.size() == c.size(), "fma_array: sizes differ");
+    darr out(a.size());
+    double* o = out.mutable_data();
+    const double *pa = a.data(), *pb = b.data(), *pc = c.data();
+    for (py::ssize_t i = 0; i < a.size(); ++i) o[i] = fma_exact(pa[i], pb[i], pc[i]);
+    return out;
+  });
 
   py::class_<Dims>(m, "Dims")
       .def(py::init([](int px, int py_, int pz) { return Dims{px, py_, pz}; }))

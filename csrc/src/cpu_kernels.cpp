@@ -64,7 +64,7 @@ void leapfrog_impl(const Layout& l, const Coeffs& c, const double* cur, double* 
     double emax = 0.0, esum = 0.0;
     const double sx = s[l.gx0 + ix];
     for (i64 iy = b.y0; iy < b.y1; ++iy) {
-      const double sxy = sx * s[l.gy0 + iy];
+      const double sxy = analytic_row(sx, s[l.gy0 + iy], ct);
       const i64 row = l.off(ix, iy, 0);
       const double* cr = cur + row;
       double* orow = out + row;
@@ -75,9 +75,9 @@ void leapfrog_impl(const Layout& l, const Coeffs& c, const double* cur, double* 
         const double v = leapfrog(u, orow[iz], lap, c.lam);
         orow[iz] = v;
         if (CHECK) {
-          const double e = std::fabs(v - (sxy * s[l.gz0 + iz]) * ct);
+          const double e = std::fabs(v - sxy * s[l.gz0 + iz]);
           emax = e > emax ? e : emax;
-          esum += e * e;
+          esum = err_sq_acc(e, esum);
         }
       }
     }
@@ -111,11 +111,11 @@ void cpu_error(const Layout& l, const double* u, const LBox& b, const double* s,
     double emax = 0.0, esum = 0.0;
     const double sx = s[l.gx0 + ix];
     for (i64 iy = b.y0; iy < b.y1; ++iy) {
-      const double sxy = sx * s[l.gy0 + iy];
+      const double sxy = analytic_row(sx, s[l.gy0 + iy], ct);
       for (i64 iz = b.z0; iz < b.z1; ++iz) {
-        const double e = std::fabs(u[l.off(ix, iy, iz)] - (sxy * s[l.gz0 + iz]) * ct);
+        const double e = std::fabs(u[l.off(ix, iy, iz)] - sxy * s[l.gz0 + iz]);
         emax = e > emax ? e : emax;
-        esum += e * e;
+        esum = err_sq_acc(e, esum);
       }
     }
     part[static_cast<size_t>(ix - b.x0)] = ErrAcc{emax, esum};

@@ -158,15 +158,16 @@ __global__ __launch_bounds__(64 * kWaves) void k_init_two(const Init2Params p) {
         p.u2[off + 1] = u2v.y;
       }
       if (CHECK && xown && y >= p.cy0 && y < p.cy1) {
+        const double ua = analytic_row(xc, yc, p.ct2);
         if (k0) {
-          const double er = fabs(u2v.x - u00 * p.ct2);
+          const double er = fabs(u2v.x - ua * Z[1]);
           emax = er > emax ? er : emax;
-          esum += er * er;
+          esum = err_sq_acc(er, esum);
         }
         if (k1) {
-          const double er = fabs(u2v.y - u01 * p.ct2);
+          const double er = fabs(u2v.y - ua * Z[2]);
           emax = er > emax ? er : emax;
-          esum += er * er;
+          esum = err_sq_acc(er, esum);
         }
       }
     }

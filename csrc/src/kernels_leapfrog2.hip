@@ -222,16 +222,16 @@ __global__ __launch_bounds__(64 * kWaves) __attribute__((amdgpu_waves_per_eu(OCC
           else if (ok1)
             dst[1] = v.y;
           if (CHECK) {
-            const double sxy = sx * sy[r];
+            const double sxy = analytic_row(sx, sy[r], p.ct2);
             if (ok0) {
-              const double er = fabs(v.x - (sxy * sz0) * p.ct2);
+              const double er = fabs(v.x - sxy * sz0);
               emax = er > emax ? er : emax;
-              esum += er * er;
+              esum = err_sq_acc(er, esum);
             }
             if (ok1) {
-              const double er = fabs(v.y - (sxy * sz1) * p.ct2);
+              const double er = fabs(v.y - sxy * sz1);
               emax = er > emax ? er : emax;
-              esum += er * er;
+              esum = err_sq_acc(er, esum);
             }
           }
         }

@@ -247,16 +247,16 @@ __global__ __launch_bounds__(kLanes* TY) void k_leapfrog_lds(const LfParams p) {
       else if (ok1)
         dst[1] = r.y;
       if (CHECK) {
-        const double sx = sxp * sxy;
+        const double sx = analytic_row(sxp, sxy, p.ct);
         if (ok0) {
-          const double e = fabs(r.x - (sx * sz0) * p.ct);
+          const double e = fabs(r.x - sx * sz0);
           emax = e > emax ? e : emax;
-          esum += e * e;
+          esum = err_sq_acc(e, esum);
         }
         if (ok1) {
-          const double e = fabs(r.y - (sx * sz1) * p.ct);
+          const double e = fabs(r.y - sx * sz1);
           emax = e > emax ? e : emax;
-          esum += e * e;
+          esum = err_sq_acc(e, esum);
         }
       }
     }
@@ -435,16 +435,16 @@ __global__ __launch_bounds__(64 * kWavesRq) __attribute__((amdgpu_waves_per_eu(R
         else if (ok1)
           dst[1] = v.y;
         if (CHECK) {
-          const double sxy = sx * sy[r];
+          const double sxy = analytic_row(sx, sy[r], p.ct);
           if (ok0) {
-            const double e = fabs(v.x - (sxy * sz0) * p.ct);
+            const double e = fabs(v.x - sxy * sz0);
             emax = e > emax ? e : emax;
-            esum += e * e;
+            esum = err_sq_acc(e, esum);
           }
           if (ok1) {
-            const double e = fabs(v.y - (sxy * sz1) * p.ct);
+            const double e = fabs(v.y - sxy * sz1);
             emax = e > emax ? e : emax;
-            esum += e * e;
+            esum = err_sq_acc(e, esum);
           }
         }
       }
@@ -595,9 +595,9 @@ __global__ __launch_bounds__(256) void k_error(const ErrParams p) {
   if (q < p.ny * p.nz) {
     const i64 y = p.y0 + q / p.nz, z = p.z0 + q % p.nz;
     const double v = p.u[(x + 1) * p.plane + (y + 1) * p.pitch + (z + 1 + p.zs)];
-    const double e = fabs(v - ((p.s[p.gx0 + x] * p.s[p.gy0 + y]) * p.s[p.gz0 + z]) * p.ct);
+    const double e = fabs(v - analytic_row(p.s[p.gx0 + x], p.s[p.gy0 + y], p.ct) * p.s[p.gz0 + z]);
     emax = e;
-    esum = e * e;
+    esum = err_sq_acc(e, 0.0);
   }
   wave_reduce(emax, esum);
   const int w = threadIdx.x >> 6;

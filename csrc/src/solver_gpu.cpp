@@ -256,9 +256,15 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   }
   // 3-D block passes: one plan (and device job tables) per pass depth that can follow an exchange
   if (block_tb_) {
+    // the send staging holds one region per depth (sbase_): the fused z-face pack writes only the real nodes of its
+    // message parts and leaves the global-boundary entries at their initial zero, which a region shared with the
+    // messages of another depth (whose parts land at other offsets) would overwrite — measured: a depth-3 exchange
+    // followed by a depth-4 one sent the depth-3 values of those entries as boundary ghosts
     for (int st = 2; st <= opt_.temporal; ++st) {
       deep_[st] = make_deep_plan(lay_, dims_, rank_, st);
       deep_max_ = imax(deep_max_, deep_[st].total);
+      sbase_[st] = send_total_;
+      send_total_ += round_up(deep_[st].total, 32);
     }
   }
 
@@ -325,14 +331,15 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   W3D_HIP(hipMemcpy(d_s_, s.data(), s.size() * sizeof(double), hipMemcpyHostToDevice));
   const i64 stage = imax(plan_.packed_doubles, deep_max_);
   if (stage > 0) {
-    W3D_HIP(hipMalloc(&send_buf_, static_cast<size_t>(stage) * sizeof(double)));
+    const i64 sstage = imax(stage, send_total_);
+    W3D_HIP(hipMalloc(&send_buf_, static_cast<size_t>(sstage) * sizeof(double)));
     W3D_HIP(hipMalloc(&recv_buf_, static_cast<size_t>(stage) * sizeof(double)));
-    W3D_HIP(hipMemset(send_buf_, 0, static_cast<size_t>(stage) * sizeof(double)));
+    W3D_HIP(hipMemset(send_buf_, 0, static_cast<size_t>(sstage) * sizeof(double)));
   }
   if (sdma_) sdma_alloc();
   if (block_tb_) {
     // fused z-face pack (its message parts live in send_buf_, zeroed once: nodes on the global boundary are never
-    // written and never read, see TbPack)
+    // written — each exchange depth has its own send region, sbase_ — and arrive as the zero boundary ghosts)
     const bool fused = opt_.fused_pack && opt_.tb;
     for (int st = 2; st <= opt_.temporal; ++st) {
       pack_tab_[st] = make_box_copy_table(deep_[st], false, fused);
@@ -344,7 +351,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
       k.nz = static_cast<int>(lay_.nz);
       for (const DeepPeer& q : deep_[st].peers)
         if (q.dir[0] == 0 && q.dir[1] == 0)
-          for (const DeepPart& part : q.parts) k.zf[q.dir[2] > 0 ? 1 : 0][part.field] = send_buf_ + q.buf_off + part.off;
+          for (const DeepPart& part : q.parts) k.zf[q.dir[2] > 0 ? 1 : 0][part.field] = send_buf_ + sbase_[st] + q.buf_off + part.off;
     }
     if (fused) {
       W3D_HIP(hipMalloc(&pk_dev_, sizeof(pk_host_)));
@@ -433,7 +440,8 @@ GpuSolver::~GpuSolver() {
 
 size_t GpuSolver::device_bytes() const {
   return static_cast<size_t>(nbuf_) * static_cast<size_t>(lay_.bytes()) +
-         2 * static_cast<size_t>(imax(plan_.packed_doubles, deep_max_)) * sizeof(double) +
+         static_cast<size_t>(imax(plan_.packed_doubles, deep_max_) + imax(plan_.packed_doubles, send_total_)) *
+             sizeof(double) +
          static_cast<size_t>(n_partials_) * sizeof(Partial) + static_cast<size_t>(prob_.N + 3) * sizeof(double) +
          static_cast<size_t>(kTbRegions) * 4 * kTbSlots * static_cast<size_t>(n_tb_) * sizeof(Partial);
 }
@@ -573,7 +581,7 @@ void GpuSolver::build_msgs(int i) {
     // one packed message per neighbour (faces, edges, corners): u^{n+S} s deep, then u^{n+S−1} s − 1 deep
     deep_s_ = units_[static_cast<size_t>(i) + 1].steps;
     for (const DeepPeer& q : deep_[deep_s_].peers)
-      msgs_.push_back(Msg{q.peer, 0, send_buf_ + q.buf_off, recv_buf_ + q.buf_off, q.count});
+      msgs_.push_back(Msg{q.peer, 0, send_buf_ + sbase_[deep_s_] + q.buf_off, recv_buf_ + q.buf_off, q.count});
     return;
   }
   if (mode_ == Mode::kDeepTb) {
@@ -747,7 +755,7 @@ bool GpuSolver::packs() const { return (mode_ == Mode::kSingleStep && plan_.pack
 
 void GpuSolver::pack_halo(hipStream_t st) {
   if (block_tb_)
-    launch_box_copy(lay_, pack_tab_[deep_s_], 0, u_[uf_[1]], u_[uf_[0]], send_buf_, st);
+    launch_box_copy(lay_, pack_tab_[deep_s_], 0, u_[uf_[1]], u_[uf_[0]], send_buf_ + sbase_[deep_s_], st);
   else if (mode_ == Mode::kSingleStep && plan_.packed_doubles > 0)
     launch_pack(lay_, plan_, post_exchange() ? u_[old_] : u_[cur_], send_buf_, st);
 }

@@ -245,7 +245,7 @@ void GpuSolver::unit_exchange_sdma(int i) {
         const XLink& l = xlinks_[k];
         if (block_tb_) {
           const DeepPeer& q = deep_[s].peers[k];
-          W3D_HIP(hipMemcpyAsync(l.recv + l.recv_off[s], send_buf_ + q.buf_off,
+          W3D_HIP(hipMemcpyAsync(l.recv + l.recv_off[s], send_buf_ + sbase_[s] + q.buf_off,
                                  static_cast<size_t>(q.count) * sizeof(double), hipMemcpyDeviceToDeviceNoCU, cs));
         } else {
           // u^{n+S} s planes deep and u^{n+S−1} s − 1 deep: this rank's planes next to the face → the peer's ghost

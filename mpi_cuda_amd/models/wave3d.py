@@ -114,7 +114,7 @@ def analytic(spec: ProblemSpec, n: int, dtype=torch.float64, device="cpu") -> to
     """u_a at step n on the full (N+1)³ node grid."""
     s = torch.as_tensor(sin_table(spec), dtype=dtype, device=device)
     ct = math.cos(spec.a_t * (n * spec.tau))
-    return (s[:, None, None] * s[None, :, None]) * s[None, None, :] * ct
+    return ((s[:, None, None] * s[None, :, None]) * ct) * s[None, None, :]  # stencil.hpp::analytic_row order
 
 
 # ----------------------------------------------------------------------------------------------------------------
@@ -156,6 +156,19 @@ def d2sum_torch(u: torch.Tensor) -> torch.Tensor:
             + (u[1:-1, 1:-1, 2:] - c2 + u[1:-1, 1:-1, :-2]))
 
 
+def fma_torch(a: float, b: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
+    """a·b + c rounded once (stencil.hpp's fused leapfrog / first step; torch has no fused multiply-add): the
+    elementwise IEEE fma of the native binding, on a host copy."""
+    from mpi_cuda_amd._native import load
+
+    bb, cc = torch.broadcast_tensors(b, c)
+    bn = bb.detach().to("cpu", torch.float64).contiguous().numpy().ravel()
+    cn = cc.detach().to("cpu", torch.float64).contiguous().numpy().ravel()
+    an = np.full_like(bn, a)
+    r = np.asarray(load().fma_array(an, bn, cn)).reshape(tuple(bb.shape))
+    return torch.from_numpy(r).to(b.device)
+
+
 def laplacian_torch(u: torch.Tensor, h: float) -> torch.Tensor:
     """7-point Δ_h on the interior of a full node grid."""
     return d2sum_torch(u) * (1.0 / (h * h))
@@ -171,7 +184,7 @@ def torch_reference_solve(spec: ProblemSpec, device="cpu", return_fields: bool =
     u1 = torch.zeros_like(u0)
     ih2 = 1.0 / (spec.h * spec.h)
     lam, half_lam = tau2 * ih2, (0.5 * tau2) * ih2  # problem.hpp::Coeffs: the coefficients of d2sum
-    u1[1:-1, 1:-1, 1:-1] = u0[1:-1, 1:-1, 1:-1] + half_lam * d2sum_torch(u0)
+    u1[1:-1, 1:-1, 1:-1] = fma_torch(half_lam, d2sum_torch(u0), u0[1:-1, 1:-1, 1:-1])
     denom = float(spec.N - 1) ** 3
     errs = {}
     checks = set(spec.check_steps())
@@ -186,7 +199,7 @@ def torch_reference_solve(spec: ProblemSpec, device="cpu", return_fields: bool =
     for n in range(1, spec.K):
         nxt = torch.zeros_like(cur)
         c = cur[1:-1, 1:-1, 1:-1]
-        nxt[1:-1, 1:-1, 1:-1] = (2.0 * c - prev[1:-1, 1:-1, 1:-1]) + lam * d2sum_torch(cur)
+        nxt[1:-1, 1:-1, 1:-1] = fma_torch(lam, d2sum_torch(cur), 2.0 * c - prev[1:-1, 1:-1, 1:-1])
         prev, cur = cur, nxt
         if n + 1 in checks:
             errs[n + 1] = err(cur, n + 1)

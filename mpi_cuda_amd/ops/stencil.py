@@ -191,5 +191,6 @@ def ref_leapfrog_grid(cur: torch.Tensor, old: torch.Tensor, ihx2: float, ihy2: f
     s = ((cur[x0 + 1:x1 + 1, y0:y1, z0:z1] - c2 + cur[x0 - 1:x1 - 1, y0:y1, z0:z1])
          + (cur[x0:x1, y0 + 1:y1 + 1, z0:z1] - c2 + cur[x0:x1, y0 - 1:y1 - 1, z0:z1])
          + (cur[x0:x1, y0:y1, z0 + 1:z1 + 1] - c2 + cur[x0:x1, y0:y1, z0 - 1:z1 - 1]))
+    # (unfused τ²-term: a plain-PyTorch reference, within one rounding of the kernels' fused leapfrog)
     out[x0:x1, y0:y1, z0:z1] = (2.0 * c - old[x0:x1, y0:y1, z0:z1]) + (tau2 * ihx2) * s
     return out

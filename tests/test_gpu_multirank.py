@@ -300,3 +300,23 @@ def test_block_fused_zface_pack(gpu, world, decomp, N, overlap, transport, fused
         r = g.run()
         _same(r, r1)
         assert torch.equal(g.global_field(0), f0)
+
+
+@pytest.mark.parametrize("transport", ["loopback", "sdma"])
+@pytest.mark.parametrize("world,decomp,K,temporal", [(2, "1x1x2", 10, 4), (8, "2x2x2", 10, 4), (2, "1x1x2", 20, 3),
+                                                     (4, "1x2x2", 11, 4)])
+def test_block_fused_zface_pack_mixed_depths(gpu, world, decomp, K, temporal, transport):
+    """Schedules whose exchanges change depth (K = 10: passes of 2, 3, 4 steps, exchanges of depth 3 then 4): the
+    fused z-face pack leaves the global-boundary entries of its message parts at their initial zero, so each depth
+    needs its own send region — a shared one carried the previous depth's values into those entries (a regression:
+    bit-identical before only for uniform-depth schedules)."""
+    spec = ProblemSpec(N=70, tau=1e-3, K=K)
+    ref = Solver(spec, backend="hip", device=0, temporal=1)
+    r1 = ref.run()
+    f0 = ref.global_field(0)
+    g = Solver(spec, backend="hip", transport=transport, world=world, rank=0, decomp=decomp, device=0, overlap=False,
+               poison_ghosts=True, fused_pack=True, temporal=temporal)
+    for _ in range(2):
+        r = g.run()
+        _same(r, r1)
+        assert torch.equal(g.global_field(0), f0)

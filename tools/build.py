@@ -38,7 +38,8 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unus
 HIP_FLAGS = COMMON + [f"--offload-arch={ARCH}", "-fno-gpu-rdc", "-munsafe-fp-atomics"]
 # (perf-attribution experiments only: e.g. W3D_EXTRA_DEFS=-DW3D_EXPERIMENT_NOLOAD builds a variant whose results are wrong)
 HIP_FLAGS += os.environ.get("W3D_EXTRA_DEFS", "").split()
-CPU_FLAGS = COMMON + ["-fopenmp", "-march=x86-64-v2"]
+# x86-64-v3: std::fma (stencil.hpp) is one vfmadd instruction, not a libm call
+CPU_FLAGS = COMMON + ["-fopenmp", "-march=x86-64-v3"]
 
 # (source, compiler kind). 'hip' = device code or HIP runtime host code, 'cpu' = plain C++ with OpenMP.
 LIB_SOURCES = [

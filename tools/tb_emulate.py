@@ -22,6 +22,16 @@ class Geom:
         return T + 2 * self.halo(j)
 
 
+def fma(a, b, c):
+    """IEEE a·b + c rounded once (stencil.hpp's fused leapfrog / first step), through the native binding."""
+    from mpi_cuda_amd._native import load
+
+    a, b, c = np.broadcast_arrays(np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64),
+                                  np.asarray(c, dtype=np.float64))
+    r = load().fma_array(a.ravel(), b.ravel(), c.ravel())
+    return np.asarray(r).reshape(a.shape)
+
+
 def lap7(c, xm, xp, ym, yp, zm, zp, ihx2, ihy2, ihz2):
     c2 = 2.0 * c  # stencil.hpp::d2sum (h²·Δ_h; the update coefficients carry 1/h²)
     return (xp - c2 + xm) + (yp - c2 + ym) + (zp - c2 + zm)
@@ -130,7 +140,7 @@ def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2:
                                (sxc * syw[ya + 1]) * sz, cy * szw[zb - 1], cy * szw[zb + 1], co.ihx2, co.ihy2, co.ihz2)
                     in_a = (y >= ay0) & (y < ay1) & (z >= az0) & (z < az1)
                     real = inside(gy0 + y) & inside(gz0 + z) & (1 <= gx0 + x <= N - 1) & in_a
-                    return np.where(real, c + co.half_lam * lap, 0.0)
+                    return np.where(real, fma(co.half_lam, lap, c), 0.0)
                 if ax0 <= x < ax1 and 1 <= gx0 + x <= N - 1:
                     # loaded wherever the rank holds the node (interior ∩ allocation); elsewhere the zero slot
                     in_a = (y >= ay0) & (y < ay1) & (z >= az0) & (z < az1)
@@ -163,7 +173,7 @@ def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2:
                 z = tz0 - hk + a[None, :] + 0 * a[:, None]
                 xreal = sx0 <= xp < sx1 and 1 <= gx0 + xp <= N - 1
                 real = xreal & inside(gy0 + y) & inside(gz0 + z) & (y >= sy0) & (y < sy1) & (z >= sz0) & (z < sz1)
-                v = np.where(real, (2.0 * c - o) + tau2 * lap, 0.0)
+                v = np.where(real, fma(tau2, lap, 2.0 * c - o), 0.0)
                 if k < S:
                     ring[k][xp % 3] = v
                 xown = x0 <= xp < x1
@@ -172,7 +182,7 @@ def run_pass(lay, co, prev: np.ndarray, cur: np.ndarray, out1: np.ndarray, out2:
                 if k >= S - 1 and own.any():
                     (out2 if k == S else out1)[goff(xp, y[own], z[own])] = v[own]
                 if k in errs and own.any():
-                    e = np.abs(v[own] - ((sget(gx0 + xp) * sget(gy0 + y[own])) * sget(gz0 + z[own])) * ct[k - 1])
+                    e = np.abs(v[own] - ((sget(gx0 + xp) * sget(gy0 + y[own])) * ct[k - 1]) * sget(gz0 + z[own]))
                     emax[k - 1] = max(emax[k - 1], float(e.max()))
                     esum[k - 1] += float((e * e).sum())
 

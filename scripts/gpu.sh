@@ -16,6 +16,8 @@
 #   scripts/gpu.sh transports                per-rank solve times (--fake-rank) of sequential / RCCL-overlap / copy-engine
 #                                            (sdma) schedules: 512^3 slab 1/8 + 1/2, 2x2x2 blocks at 512^3 and 2048^3
 #                                            -> gpurun_out/transports.log
+#   scripts/gpu.sh attrib                    LDS-pass kernel times: production, no checks, 768 threads, experiment builds
+#                                            build/ab/wave3d_noload / _nostore -> gpurun_out/attrib.txt
 #   scripts/gpu.sh probe                     tools/probes/sdma_probe (copy engines, memops, capture) -> gpurun_out/probe.log
 #   scripts/gpu.sh all                       test && cli && bench && profbench
 set -o pipefail
@@ -99,6 +101,32 @@ run_ab() {
   done
 }
 
+# perf attribution of the LDS passes: rocprofv3 kernel stats of the production solve, the same solve without error
+# checks, and the experiment builds build/ab/wave3d_<variant> (W3D_EXTRA_DEFS=-DW3D_EXPERIMENT_<VARIANT>, results
+# wrong) -> gpurun_out/attrib/<name>/ and gpurun_out/attrib.txt
+run_attrib() {
+  local name bin extra
+  rm -rf gpurun_out/attrib
+  mkdir -p gpurun_out/attrib
+  : > gpurun_out/attrib.txt
+  for spec in "base:build/ab/wave3d_base:" "prod:bin/wave3d:" "nocheck:bin/wave3d:--check-every 100" "t768:bin/wave3d:--tb-threads 768" \
+              "noload:build/ab/wave3d_noload:" "nostore:build/ab/wave3d_nostore:" "static:build/ab/wave3d_static:"; do
+    IFS=: read -r name bin extra <<< "$spec"
+    [ -x "$bin" ] || continue
+    timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/attrib/$name -o run -- \
+      "$bin" 512 0.001 20 1 --repeat 10 --warmup 2 --quiet $extra > gpurun_out/attrib/$name.log 2>&1 || return 1
+    echo "== $name $extra" >> gpurun_out/attrib.txt
+    python3 -c "
+import csv,glob
+for f in glob.glob('gpurun_out/attrib/$name/**/run_kernel_stats.csv', recursive=True):
+    for r in csv.DictReader(open(f)):
+        if 'leapfrog' in r['Name']:
+            print(r['Name'].split('(')[0][-60:], r['Calls'], 'avg', round(float(r['AverageNs'])/1e3,1), 'min', round(float(r['MinNs'])/1e3,1))
+" >> gpurun_out/attrib.txt
+  done
+  cat gpurun_out/attrib.txt
+}
+
 # compute-only strong-scaling projection of the 512^3 solve: one rank of P timed alone (--fake-rank, no transport
 # traffic) for the sequential slab and block schedules; one JSON line per point -> gpurun_out/fakesweep.jsonl
 run_fakesweep() {
@@ -151,6 +179,7 @@ case "$what" in
   prof) run_prof "$@" ;;
   profbench) run_profbench "$@" ;;
   pmc) run_pmc "$@" ;;
+  attrib) run_attrib ;;
   fakerank) run_fakerank > gpurun_out/fakerank.log 2>&1; rc=$?; cat gpurun_out/fakerank.log; exit $rc ;;
   all) run_test && run_cli && run_bench && run_profbench ;;
   *) echo "unknown step $what" >&2; exit 2 ;;

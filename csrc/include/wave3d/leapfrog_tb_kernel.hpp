@@ -424,11 +424,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         const gdouble* base = plane_ptr(bkc, p.cur, 6, xs);
 #pragma unroll
         for (int q = 0; q < Q; ++q)
-#ifdef W3D_EXPERIMENT_STATIC
-          L[0][q][slot] = base[gof[q] & kOff];
-#else
           if (wsm[q]) L[0][q][slot] = base[gof[q] & kOff];
-#endif
 #pragma unroll
         for (int r = 0; r < QR; ++r) Rg[r][rs] = base[grof[r] & kOff];
       }
@@ -444,11 +440,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         const gdouble* base = plane_ptr(bkc, p.prev, 4, xs);
 #pragma unroll
         for (int q = 0; q < Q; ++q)
-#ifdef W3D_EXPERIMENT_STATIC
-          Lm[q][slot] = base[gof[q] & kOff];
-#else
           if (wsm[q]) Lm[q][slot] = base[gof[q] & kOff];
-#endif
       }
     };
     auto commit_cur = [&](auto slot_c, auto rs_c, int par) {
@@ -596,15 +588,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         // boolean it became a lane mask whose negation the compiler re-formed with two VALU ops per use
         int wm = wsm[q];
         asm volatile("" : "+s"(wm));
-#ifdef W3D_EXPERIMENT_STATIC
-        // (perf attribution: every wave issues the same VMEM sequence each iteration, so the compiler can count vmcnt)
-        double vst = 0.0;
-        bool ost = false;
-        if ((wm >> (k - 1)) & 1) {
-#else
         if (!((wm >> (k - 1)) & 1)) continue;
-        {
-#endif
         const int li = lid[q];
         const double c = L[k - 1][q][s0];
         double lap;
@@ -626,18 +610,14 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
           dst[tid + q * NT] = v;
         }
         const bool own = xown && (g & kOwn);
-#ifdef W3D_EXPERIMENT_STATIC
-        vst = v;
-        ost = own && xreal;
-#endif
         if constexpr (k >= S - 1) {
           if (own && xreal) {
-#if !defined(W3D_EXPERIMENT_NOSTORE) && !defined(W3D_EXPERIMENT_STATIC)  // (perf attribution only)
+#if defined(W3D_EXPERIMENT_PLAINSTORE)  // (experiment: write-back stores instead of non-temporal ones)
+            outp[g & kOff] = v;
+#elif !defined(W3D_EXPERIMENT_NOSTORE)  // (perf attribution only, results wrong: the pass writes nothing to HBM)
             __builtin_nontemporal_store(v, outp + (g & kOff));
 #endif
-#ifndef W3D_EXPERIMENT_STATIC
             if (pks) pack_store(k == S ? 0 : 1, xp, tid + q * NT, v);
-#endif
             if constexpr (PUSH && !BK)
               if (fwd) __hip_atomic_store(fwd + (g & kOff), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           }
@@ -657,15 +637,6 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
             esum[k - 1] = err_sq_acc(e, esum[k - 1]);
           }
         }
-        }
-#ifdef W3D_EXPERIMENT_STATIC
-        if constexpr (k >= S - 1) {
-          // per-lane dummy slots (no two lanes or waves share an address): the boundary plane x = N of the output
-          double* dmy = (k == S ? p.out2 : p.out1) + static_cast<i64>(p.N + 1) * P +
-                        ((static_cast<int>(blockIdx.x) * (NT / 64) + (tid >> 6)) * 64 + (tid & 63)) % static_cast<int>(P);
-          __builtin_nontemporal_store(vst, ost ? outp + (gof[q] & kOff) : dmy);
-        }
-#endif
       }
     };
 

@@ -110,7 +110,7 @@ run_attrib() {
   mkdir -p gpurun_out/attrib
   : > gpurun_out/attrib.txt
   for spec in "base:build/ab/wave3d_base:" "prod:bin/wave3d:" "nocheck:bin/wave3d:--check-every 100" "t768:bin/wave3d:--tb-threads 768" \
-              "noload:build/ab/wave3d_noload:" "nostore:build/ab/wave3d_nostore:" "static:build/ab/wave3d_static:"; do
+              "noload:build/ab/wave3d_noload:" "nostore:build/ab/wave3d_nostore:" "static:build/ab/wave3d_static:" "plainstore:build/ab/wave3d_plainstore:"; do
     IFS=: read -r name bin extra <<< "$spec"
     [ -x "$bin" ] || continue
     timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/attrib/$name -o run -- \

@@ -33,3 +33,21 @@ def test_core_under_asan_ubsan(sanitized_binary):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "checks, 0 failed" in r.stdout
     assert "runtime error" not in r.stderr  # UBSan report
+
+
+def test_fma_array_rounds_once():
+    """The emulators' rounding primitive (bindings: fma_array) is the IEEE fused multiply-add of stencil.hpp: a·b + c
+    rounded once — it differs from the twice-rounded numpy a * b + c exactly where the product's rounding error
+    matters (here (1 + 2⁻³⁰)² − 1 keeps the 2⁻⁶⁰ term the plain product loses)."""
+    import numpy as np
+
+    from mpi_cuda_amd._native import load
+
+    e = 2.0 ** -30
+    a = np.array([1.0 + e, 3.0, 0.1])
+    b = np.array([1.0 + e, 7.0, 0.3])
+    c = np.array([-1.0, 1.0, -0.03])
+    r = np.asarray(load().fma_array(a, b, c))
+    assert r[0] == 2 * e + e * e and (a[0] * b[0] + c[0]) == 2 * e
+    assert r[1] == 22.0
+    assert abs(r[2] - (0.1 * 0.3 - 0.03)) <= 2 * np.spacing(0.03)

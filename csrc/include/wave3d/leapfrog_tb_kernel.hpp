@@ -132,17 +132,24 @@ __device__ __forceinline__ void tb_push_signal(const TbPush& q) {
   }
 }
 
-template <int S, int T, int NT>
+// RP (row-padded ring layout): the planes that keep the ring (level 0, the analytic start's φ level) get a row stride
+// RS = H1 + 32 instead of W0 = H1 + 2. Consecutive positions then skip 32 doubles, not 2, where they cross a row end,
+// so a half-wave that straddles a row still touches 32 distinct bank pairs: the ring-padded rows cost the
+// compute-bound analytic pass 15 % bank-conflict cycles (PMC, profiles/r3/pass_attribution.md). Used where the wider
+// planes fit: the analytic start at S ≤ 3 (its four ring-layout slots: 133 KiB at S = 3, with room for the 2048³ x
+// sin table); the 4-step pass keeps W0 (its 2048³ sin table would not fit next to the wider planes).
+template <int S, int T, int NT, bool RP = false>
 struct TbGeom {
   static constexpr int H1 = T + 2 * (S - 1);  // stage-1 region edge: the thread-owned positions
   static constexpr int NP = H1 * H1;
   static constexpr int Q = (NP + NT - 1) / NT;  // positions per thread
   static constexpr int W0 = T + 2 * S;          // u^n region edge = LDS plane edge (all levels share the indexing)
-  static constexpr int PL = W0 * W0;
-  static constexpr int NR = PL - NP;            // u^n halo ring (not thread-owned)
+  static constexpr int RS = RP ? H1 + 32 : W0;  // row stride of the ring-layout planes (≥ W0)
+  static constexpr int PL = W0 * RS;            // a ring-layout plane: W0 rows of RS
+  static constexpr int NR = W0 * W0 - NP;       // u^n halo ring (not thread-owned)
   // plane stride in LDS: the plane plus a pad holding a dummy node (and its 4 neighbours) for lanes without a position
-  static constexpr int PLP = PL + 2 * W0 + 2;
-  static constexpr int DUMMY = PL + W0 + 1;
+  static constexpr int PLP = PL + 2 * RS + 2;
+  static constexpr int DUMMY = PL + RS + 1;
   static constexpr int QR = (NR + NT - 1) / NT;
   // The stage levels 1..S−1 live in COMPACT planes: position idx = tid + q·NT (row a = idx / H1, column b = idx % H1)
   // at COFF + idx, row stride H1, no ring and no gap between rows, so the 16 lanes of every LDS access phase touch 16
@@ -165,9 +172,12 @@ struct TbGeom {
 // + sin tables (error check, analytic start): y and z over the u^n region ± 1, x over the planes the pass touches ± 1.
 // In LDS because a global load of the per-plane x factor would be a vector load (the table may alias the outputs, so
 // no scalar load) whose wait drains the prefetch queue. nxo = tb_nx_table(x1 − x0) or 0 (no table needed).
+template <bool INIT, int S>
+constexpr bool tb_row_pad = INIT && S <= 3;  // TbGeom::RP per pass kind
 template <int S, int T, int NT, bool INIT = false, bool FAC = false>
 constexpr size_t tb_lds_bytes(int nxo = 0) {
-  return (static_cast<size_t>(TbGeom<S, T, NT>::lds_doubles(INIT, FAC)) + (2 + 2 * S) * (T + 2 * S + 2) +
+  return (static_cast<size_t>(TbGeom<S, T, NT, tb_row_pad<INIT, S>>::lds_doubles(INIT, FAC)) +
+          (2 + 2 * S) * (T + 2 * S + 2) +
           static_cast<size_t>(nxo)) *
          sizeof(double);
 }
@@ -184,8 +194,8 @@ constexpr int tb_nx_table(int nx_box) {
 // re-reads instead of keeping live (measured: a computed range costs the S = 4 kernel 5 % in extra spills).
 template <int S, int T, int NT, int CM, bool INIT, bool CH, bool PUSH>
 __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
-  using G = TbGeom<S, T, NT>;
-  constexpr int Q = G::Q, QR = G::QR, H1 = G::H1, W0 = G::W0, PLP = G::PLP;
+  using G = TbGeom<S, T, NT, tb_row_pad<INIT, S>>;
+  constexpr int Q = G::Q, QR = G::QR, H1 = G::H1, W0 = G::W0, RS = G::RS, PLP = G::PLP;
   constexpr int kOwn = 1 << 30;   // gof flag: tile node inside the output box
   constexpr int kReal = 1 << 29;  // gof flag: stage values are real at this node (interior ∩ stage-real range)
   constexpr int kLd = 1 << 28;    // gof flag: node inside the global interior and the allocation (loaded)
@@ -256,7 +266,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
                       in_rng(z, p.az0, p.az1);
       const bool real = ld && in_rng(y, p.sy0, p.sy1) && in_rng(z, p.sz0, p.sz1);
       const bool own = real && a >= S - 1 && a < S - 1 + T && b >= S - 1 && b < S - 1 + T && y < p.y1 && z < p.z1;
-      lid[q] = valid ? (a + 1) * W0 + (b + 1) : G::DUMMY;
+      lid[q] = valid ? (a + 1) * RS + (b + 1) : G::DUMMY;
       gof[q] = ld ? (((y + ya) * R + z + za) | kLd | (real ? kReal : 0) | (own ? kOwn : 0)) : zero_off;
     }
     // wave-uniform stage masks: bit k−1 of wsm[q] is set when some lane of this wave's position set q lies inside stage
@@ -297,7 +307,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       }
       const int y = ty0 - S + a0, z = tz0 - S + b0;
       const bool valid = ridx < G::NR;
-      lrid[r] = valid ? a0 * W0 + b0 : G::DUMMY;
+      lrid[r] = valid ? a0 * RS + b0 : G::DUMMY;
       grof[r] = (valid && inside(p.gy0 + y) && inside(p.gz0 + z) && in_rng(y, p.ay0, p.ay1) && in_rng(z, p.az0, p.az1))
                     ? ((y + ya) * R + z + za) | kLd
                     : zero_off;
@@ -335,10 +345,10 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
       __syncthreads();
     }
     (void)fac;
-    // table indices of an LDS position li (u^n-region coordinates): y ↔ li / W0 + 1, z ↔ li % W0 + 1 (the pad's dummy
+    // table indices of an LDS position li (u^n-region coordinates): y ↔ li / RS + 1, z ↔ li % RS + 1 (the pad's dummy
     // node is clamped into the table)
-    auto ytab = [&](int li) { return imin(li / W0 + 1, W0); };
-    auto ztab = [&](int li) { return li - (li / W0) * W0 + 1; };
+    auto ytab = [&](int li) { return imin(li / RS + 1, W0); };
+    auto ztab = [&](int li) { return li - (li / RS) * RS + 1; };
     const int xtab0 = S + 1 - wx0;  // x ↔ sxw[x + xtab0]
     if constexpr (kFac) {
       if (p.check_mask) {  // (each thread writes and later reads only its own pairs: no barrier)
@@ -515,7 +525,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         const double f3 = (sx3 * fyq(q)) * fzq(q);   // φ(i+3)
         p3[li] = f3;
         const double c = p2[li];                     // φ(i+2)
-        const double lap = d2sum(c, f1, f3, p2[li - W0], p2[li + W0], p2[li - 1], p2[li + 1]);
+        const double lap = d2sum(c, f1, f3, p2[li - RS], p2[li + RS], p2[li - 1], p2[li + 1]);
         L[0][q][(F + 2) & 3] = ((gof[q] & kLd) && xin) ? first_step(c, lap, p.half_tau2) : 0.0;
         Lm[q][(F + 1) & 1] = f1;
       }
@@ -593,7 +603,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         const double c = L[k - 1][q][s0];
         double lap;
         if constexpr (k == 1) {
-          lap = d2sum(c, L[k - 1][q][sm], L[k - 1][q][sp], nb[li - W0], nb[li + W0], nb[li - 1], nb[li + 1]);
+          lap = d2sum(c, L[k - 1][q][sm], L[k - 1][q][sp], nb[li - RS], nb[li + RS], nb[li - 1], nb[li + 1]);
         } else {
           const int lc = tid + q * NT;  // (compact index: the position itself)
           lap = d2sum(c, L[k - 1][q][sm], L[k - 1][q][sp], nb[lc - H1], nb[lc + H1], nb[lc - 1], nb[lc + 1]);

@@ -137,7 +137,8 @@ __device__ __forceinline__ void tb_push_signal(const TbPush& q) {
 // so a half-wave that straddles a row still touches 32 distinct bank pairs: the ring-padded rows cost the
 // compute-bound analytic pass 15 % bank-conflict cycles (PMC, profiles/r3/pass_attribution.md). Used where the wider
 // planes fit: the analytic start at S ≤ 3 (its four ring-layout slots: 133 KiB at S = 3, with room for the 2048³ x
-// sin table); the 4-step pass keeps W0 (its 2048³ sin table would not fit next to the wider planes).
+// sin table). The 4-step pass keeps W0: on a whole 2048³ box its x sin table would not fit next to the wider planes,
+// and where it fits (512³) the wider layout moved a register to scratch inside the march and was measured slower.
 template <int S, int T, int NT, bool RP = false>
 struct TbGeom {
   static constexpr int H1 = T + 2 * (S - 1);  // stage-1 region edge: the thread-owned positions

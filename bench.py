@@ -80,7 +80,10 @@ def _args(argv=None):
                          "faces; sdma: copy engines move the halos into the peers' memory)")
     ap.add_argument("--no-rccl", action="store_true",
                     help="native ranks without an RCCL communicator (push / sdma only; host collectives through files)")
-    ap.add_argument("--timeout", type=float, default=900.0, help="seconds before a native rank is killed")
+    ap.add_argument("--autotune-sdma", action="store_true",
+                    help="several ranks: include the copy-engine candidates in the autotune (opt-in across GPUs)")
+    ap.add_argument("--timeout", type=float, default=420.0,
+                    help="seconds before a native rank is killed (below the driver's 600 s bench limit)")
     ap.add_argument("--out", default="", help="also append the JSON line to this file")
     return ap.parse_args(argv)
 
@@ -176,6 +179,8 @@ def run_native(a, rank: int, world: int, local: int) -> int:
             cmd.append("--no-rccl")
         if (multi or a.autotune) and not a.no_autotune and not a.no_rccl:
             cmd.append("--autotune")
+            if a.autotune_sdma:
+                cmd.append("--autotune-sdma")
         if not a.no_phases:
             cmd.append("--phases")
         if a.no_overlap:
@@ -257,7 +262,14 @@ def run_native(a, rank: int, world: int, local: int) -> int:
             "temporal_blocking": int(res.get("temporal", 1)) > 1 and not a.cpu,
             "schedule": sched if multi or a.cpu else f"fused-single-S{res.get('temporal', temporal)}",
             "mode": res.get("mode", ""),
+            # per candidate: the MEDIAN over rounds of the per-solve time of back-to-back solves (what decides), and
+            # the best round
             "autotune_ms": {k: round(v * 1e3, 4) for k, v in res.get("autotune_s", {}).items()} or None,
+            "autotune_best_ms": {k: round(v * 1e3, 4) for k, v in res.get("autotune_best_s", {}).items()} or None,
+            "autotune_rounds_x_reps": [res.get("autotune_rounds"), res.get("autotune_reps")]
+            if res.get("autotune_s") else None,
+            "autotune_wall_s": res.get("autotune_wall_s") if res.get("autotune_s") else None,
+            "autotune_rejected": res.get("autotune_rejected") or None,
         }
         extra = {
             "wall_clock_s": round(ms / 1e3, 6),

@@ -34,6 +34,9 @@ struct Args {
   int bench_steps = 0;                 // --bench-steps K: timed block of K solves (bench.py contract)
   bool autotune = false;               // --autotune: time the multi-rank schedule candidates, keep the fastest
   int autotune_rounds = 5;             // --autotune-rounds R: interleaved timing rounds
+  int autotune_reps = 5;               // --autotune-reps B: back-to-back solves per candidate and round
+  double autotune_budget = 120.0;      // --autotune-budget S: wall-time budget of the autotune (s)
+  bool autotune_sdma = false;          // --autotune-sdma (or W3D_AUTOTUNE_SDMA=1): copy-engine candidates too
   bool phases = false;                 // --phases: per-phase breakdown from a traced solve of the timed schedule
   std::string group_transport = "rccl-self";
   std::string transport = "rccl";      // --transport rccl | push (slab LDS passes: halos pushed by the passes)

@@ -72,7 +72,10 @@ constexpr Personality kPersonalities[] = {
                "  --autotune         time the multi-rank schedule candidates (slab / block x pass depth x overlap x RCCL /\n"
                "                     copy engines; push with --transport push) in interleaved rounds, keep the fastest\n"
                "                     (slowest rank decides; the simplest within 2%%)\n"
-               "  --autotune-rounds R  interleaved timing rounds of the autotune (default 5)\n"
+               "  --autotune-rounds R  interleaved timing rounds of the autotune (default 5); the median decides\n"
+               "  --autotune-reps B  back-to-back solves per candidate and round (default 5, as the bench runs them)\n"
+               "  --autotune-budget S  wall-time budget of the autotune in seconds (default 120; 0: none)\n"
+               "  --autotune-sdma    include the copy-engine candidates across GPUs (also W3D_AUTOTUNE_SDMA=1)\n"
                "  --phases           per-phase device times (init/compute/exchange/check) of the timed schedule\n"
                "  --variant V        leapfrog kernel: 1 = register-queue waves (default), 0 = LDS-staged tile\n"
                "  --tile-rows T      rows per wave (v1: 1,2,4,8) or per workgroup (v0: 4,8,16)\n"
@@ -141,6 +144,9 @@ Args parse(int argc, char** argv) {
     else if (s == "--bench-steps") a.bench_steps = std::stoi(next());
     else if (s == "--autotune") a.autotune = true;
     else if (s == "--autotune-rounds") a.autotune_rounds = std::stoi(next());
+    else if (s == "--autotune-reps") a.autotune_reps = std::stoi(next());
+    else if (s == "--autotune-budget") a.autotune_budget = std::stod(next());
+    else if (s == "--autotune-sdma") a.autotune_sdma = true;
     else if (s == "--phases") a.phases = true;
     else if (s == "--group-transport") a.group_transport = next();
     else if (s == "--transport") a.transport = next();

@@ -116,7 +116,8 @@ int run_gpu(const Args& a) {
   const int rccl_nranks = comm ? comm->count() : 0;
   // fault injection: W3D_FAULT_RANK=r makes rank r fail right after the communicator is up; its peers
   // then fail in their next collective (GPU-wait timeout W3D_TIMEOUT_S) instead of hanging
-  if (const char* fr = std::getenv("W3D_FAULT_RANK"); fr && std::atoi(fr) == rank) fail("injected fault");
+  if (const char* fr = std::getenv("W3D_FAULT_RANK"); fr && std::atoi(fr) == rank && !std::getenv("W3D_FAULT_AT_SOLVE"))
+    fail("injected fault");
   // host collectives: RCCL; files for ranks without a communicator (--no-rccl rehearsal, outside timed regions); none
   // for one rank or a fake rank
   const bool file_coll = !comm && world > 1 && !fake;
@@ -128,7 +129,14 @@ int run_gpu(const Args& a) {
                       (a.transport == "rccl" ? "" : "-" + a.transport);
   AutotuneResult tuned;
   if (a.autotune && (world > 1 || a.fake_rank < 0)) {
-    tuned = autotune(a.prob, base, rank, world, comm, hc, fake, a.transport == "push", a.autotune_rounds);
+    AutotuneOptions ao;
+    ao.with_push = a.transport == "push";
+    const char* es = std::getenv("W3D_AUTOTUNE_SDMA");
+    ao.with_sdma = a.autotune_sdma || a.transport == "sdma" || (es && *es == '1');
+    ao.rounds = a.autotune_rounds;
+    ao.reps = a.autotune_reps;
+    ao.budget_s = a.autotune_budget;
+    tuned = autotune(a.prob, base, rank, world, comm, hc, fake, ao);
     s = std::move(tuned.solver);
     sched = tuned.name;
   } else {
@@ -143,8 +151,14 @@ int run_gpu(const Args& a) {
   }
   RunResult r;
   double best = 1e30, sum = 0, first = 0;
+  // lost-peer injection: W3D_FAULT_RANK=r with W3D_FAULT_AT_SOLVE=i makes rank r vanish right after the barrier of
+  // solve i, so its peers run into that solve alone (their transport waits must end it within one bound)
+  const char* fas = std::getenv("W3D_FAULT_AT_SOLVE");
+  const char* frk = std::getenv("W3D_FAULT_RANK");
+  const int fault_at = fas && frk && std::atoi(frk) == rank ? std::atoi(fas) : -1;
   for (int i = 0; i < a.warmup + a.repeat; ++i) {
     hc.barrier();
+    if (i == fault_at) fail("injected fault: rank " + std::to_string(rank) + " lost before solve " + std::to_string(i));
     r = s->run();
     const double t = hc.max(r.solve_s);
     if (i == 0) first = t;
@@ -245,7 +259,11 @@ int run_gpu(const Args& a) {
         << ", \"warmup\": " << a.warmup << ", \"finite\": " << (r.finite ? "true" : "false") << ", \"autotune_s\": {";
       for (size_t i = 0; i < tuned.times.size(); ++i)
         j << (i ? ", " : "") << jstr(tuned.times[i].first) << ": " << jnum(tuned.times[i].second);
-      j << "}, \"autotune_rounds\": " << tuned.rounds << ", \"autotune_rejected\": {";
+      j << "}, \"autotune_best_s\": {";
+      for (size_t i = 0; i < tuned.best_times.size(); ++i)
+        j << (i ? ", " : "") << jstr(tuned.best_times[i].first) << ": " << jnum(tuned.best_times[i].second);
+      j << "}, \"autotune_rounds\": " << tuned.rounds << ", \"autotune_reps\": " << tuned.reps
+        << ", \"autotune_wall_s\": " << jnum(tuned.wall_s) << ", \"autotune_rejected\": {";
       for (size_t i = 0; i < tuned.rejected.size(); ++i)
         j << (i ? ", " : "") << jstr(tuned.rejected[i].first) << ": " << jstr(json_escape(tuned.rejected[i].second));
       j << "}";

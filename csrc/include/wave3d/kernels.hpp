@@ -199,6 +199,10 @@ struct FlagOp {
 };
 void launch_flag_sync(const FlagOp& wait, const FlagOp& signal, hipStream_t stream);
 
+// Order-independent hash of the owned nodes of field f (Σ mix64(bits ^ mix64(global index)) mod 2⁶⁴), added into *out
+// (zeroed by the caller): equal for bit-identical fields whatever the decomposition (GpuSolver::field_hash).
+void launch_field_hash(const Layout& l, const double* f, unsigned long long* out, hipStream_t stream);
+
 // Pack all strided faces of `plan` from `u` into `buf`, or unpack `buf` into the ghost layers of `u`.
 void launch_pack(const Layout& l, const HaloPlan& plan, const double* u, double* buf, hipStream_t stream);
 void launch_unpack(const Layout& l, const HaloPlan& plan, const double* buf, double* u, hipStream_t stream);

@@ -74,24 +74,37 @@ struct Candidate {
   int sdma_streams = 0;            // copy streams (0: the solver's default)
   bool shells_concurrent = false;  // overlap: shells beside the interior instead of before it
 };
-// the candidates for `world` ranks (fake: one rank of a `world`-rank job alone); push candidates only on request
-std::vector<Candidate> autotune_candidates(int world, bool with_push);
+// the candidates for `world` ranks (fake: one rank of a `world`-rank job alone); push and copy-engine candidates only on
+// request (neither has run between two GPUs yet)
+std::vector<Candidate> autotune_candidates(int world, bool with_push, bool with_sdma = false);
 // connect a solver's transport to its peers (IPC handles through hc.allgather; a fake rank connects to itself)
 void connect_transport(GpuSolver& s, const HostColl& hc, bool fake);
 struct AutotuneResult {
   std::unique_ptr<GpuSolver> solver;
   std::string name;
-  std::vector<std::pair<std::string, double>> times;  // best solve time (max over ranks) per timed candidate
+  std::vector<std::pair<std::string, double>> times;       // per timed candidate: median per-solve time (max over ranks)
+  std::vector<std::pair<std::string, double>> best_times;  // ... and its best round
   std::vector<std::pair<std::string, std::string>> rejected;  // candidate, reason
-  int rounds = 0;
+  int rounds = 0, reps = 0;
+  double wall_s = 0.0;  // the autotune's own wall time
+};
+struct AutotuneOptions {
+  bool with_push = false;   // the push transport's candidates (opt-in)
+  bool with_sdma = false;   // the copy-engine candidates (opt-in across devices; a fake rank always has them)
+  int rounds = 5;           // interleaved timing rounds
+  int reps = 5;             // back-to-back solves per candidate and round (the bench's pattern)
+  double tie = 0.02;        // a later candidate must beat the simplest by more than this (relative) to be chosen
+  double budget_s = 120.0;  // wall-time budget: no new candidate, and no new round, once spent (<= 0: none)
+  double flag_timeout_s = 10.0;  // in-kernel flag-wait bound of the candidates (copy engines; <= 0: the default)
 };
 // Build every candidate on every rank (a candidate one rank cannot build is skipped everywhere), drop clones (same
 // mode, transport, overlap, depth and decomposition as an earlier one), run each twice (eager + capture), reject any
-// whose error log differs from the first accepted candidate's (every schedule computes bit-identical fields), then time
-// the survivors in `rounds` interleaved rounds (one solve each per round, barrier before each) and keep the fastest —
-// or the simplest within `tie` (relative) of the fastest. The slowest rank decides every time. Candidates that do not
-// fit in device memory next to the others are timed alone right away (best of `rounds`).
+// whose log or fields differ from the first accepted candidate's (L∞ exact, RMS to 1e-12, u^K and u^{K−1} through the
+// decomposition-free field hash — every schedule computes bit-identical fields), then time the survivors in `rounds`
+// interleaved rounds of `reps` back-to-back solves each (barrier before each round) and keep the fastest MEDIAN — or
+// the simplest within `tie` of it. The slowest rank decides every time. Candidates that do not fit in device memory
+// next to the others are timed alone right away. The wall-time budget stops the candidate list and the rounds early.
 AutotuneResult autotune(const Problem& prob, const SolverOptions& base, int rank, int world, std::shared_ptr<Comm> comm,
-                        const HostColl& hc, bool fake, bool with_push, int rounds = 5, double tie = 0.02);
+                        const HostColl& hc, bool fake, const AutotuneOptions& opt);
 
 }  // namespace wave3d

@@ -79,6 +79,10 @@ struct SolverOptions {
   // copy-engine transport: copy streams (each gets its own SDMA engine; 0 = auto: one per slab face, one for a block
   // rank's messages — in a replayed graph a second copy stream made the 2048³ 2x2x2 rank slower, 48.8 vs 43.6 ms)
   int sdma_streams = 0;
+  // copy-engine transport: bound of one in-kernel flag wait in seconds (0 = min(W3D_TIMEOUT_S / 2, 60)); the autotune
+  // sets a short one so a candidate whose peer is lost costs seconds, not minutes. It is baked into the captured
+  // graphs. Half the host's own wait bound by default, so the device reports the lost peer before the host gives up.
+  double flag_timeout_s = 0.0;
   bool push_cp_wait = false;
   // push ranks without an end-of-solve collective (no RCCL communicator): the flag epochs run on over the solves
   // instead of being reset (eager launches: every launch carries its own epochs)
@@ -158,6 +162,10 @@ class GpuSolver {
 
   // Host copy of the local array holding u^K (which = 0) or u^{K−1} (which = 1), full padded layout.
   std::vector<double> download(int which) const;
+  // Order-independent 64-bit hash of the OWNED nodes of u^K (which = 0) or u^{K−1} (which = 1) after the last run():
+  // Σ mix(bits(u) ^ mix(global node index)) mod 2⁶⁴. Summed over the ranks (mod 2⁶⁴) it is the same for every
+  // decomposition and schedule that computes bit-identical fields — the autotune's field check (one read pass).
+  unsigned long long field_hash(int which) const;
   int device() const { return dev_; }  // the HIP device this rank's buffers and streams live on
 
   const Layout& layout() const { return lay_; }
@@ -389,6 +397,10 @@ class GpuSolver {
   void sdma_receive(int i);        // s0 before unit i ≥ 1: wait "arrived" (i − 1), unpack, signal "done" (i − 1)
   void sdma_finish();              // s0 after the last unit: "done" for the next solve's first exchange
   void sdma_poison(int i, const int uf[2]);  // --poison-ghosts: NaN into the regions exchange i fills
+  unsigned long long flag_ticks() const;     // bound of one in-kernel flag wait (wall-clock ticks)
+  // every link has the peer pointers its copies and signals use (connect_sdma / connect_sdma_self / a group): a
+  // solver used unconnected would make the copy engines and k_flag_sync write through null + offset (a GPU fault)
+  void sdma_check_connected() const;
 };
 
 // Per-phase device timers (SolverOptions::timers, eager launches only): every timed launch group is bracketed by two

@@ -450,6 +450,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("shells_concurrent", &SolverOptions::shells_concurrent)
       .def_readwrite("fused_pack", &SolverOptions::fused_pack)
       .def_readwrite("sdma_streams", &SolverOptions::sdma_streams)
+      .def_readwrite("flag_timeout_s", &SolverOptions::flag_timeout_s)
       .def_readwrite("push_no_collective", &SolverOptions::push_no_collective)
       .def_readwrite("temporal", &SolverOptions::temporal)
       .def_readwrite("init2", &SolverOptions::init2)
@@ -515,6 +516,9 @@ PYBIND11_MODULE(_C, m) {
              return darr(static_cast<py::ssize_t>(v.size()), v.data());
            },
            py::arg("which") = 0)
+      .def("field_hash", &GpuSolver::field_hash, py::arg("which") = 0,
+           "order-independent 64-bit hash of the owned nodes of u^K (0) / u^{K-1} (1); summed over the ranks it is "
+           "the same for every decomposition that computes bit-identical fields")
       .def_property_readonly("layout", &GpuSolver::layout)
       .def_property_readonly("dims", &GpuSolver::dims)
       .def_property_readonly("halo", &GpuSolver::halo)
@@ -536,13 +540,20 @@ PYBIND11_MODULE(_C, m) {
   m.def(
       "autotune",
       [](const Problem& p, const SolverOptions& o, int rank, int world, std::shared_ptr<Comm> c, bool fake,
-         bool with_push, int rounds, double tie) {
+         bool with_push, int rounds, double tie, bool with_sdma, int reps, double budget_s) {
         W3D_REQUIRE(world == 1 || fake || c, "autotune: world > 1 needs an RCCL communicator");
         const HostColl hc = c ? HostColl::rccl(c) : HostColl::single(rank);
+        AutotuneOptions ao;
+        ao.with_push = with_push;
+        ao.with_sdma = with_sdma;
+        ao.rounds = rounds;
+        ao.reps = reps;
+        ao.tie = tie;
+        ao.budget_s = budget_s;
         AutotuneResult r;
         {
           py::gil_scoped_release nogil;
-          r = autotune(p, o, rank, world, c, hc, fake, with_push, rounds, tie);
+          r = autotune(p, o, rank, world, c, hc, fake, ao);
         }
         py::dict times, rejected;
         for (const auto& [k, v] : r.times) times[py::str(k)] = v;
@@ -551,6 +562,7 @@ PYBIND11_MODULE(_C, m) {
       },
       py::arg("problem"), py::arg("options"), py::arg("rank") = 0, py::arg("world") = 1, py::arg("comm") = nullptr,
       py::arg("fake") = false, py::arg("with_push") = false, py::arg("rounds") = 5, py::arg("tie") = 0.02,
+      py::arg("with_sdma") = false, py::arg("reps") = 5, py::arg("budget_s") = 120.0,
       "time the schedule candidates (slab/block, pass depth, overlap, RCCL/copy engines) and return "
       "(GpuSolver, name, {name: seconds}, {name: reason rejected})");
 
@@ -574,6 +586,8 @@ PYBIND11_MODULE(_C, m) {
              auto v = g.rank(rank).download(which);
              return darr(static_cast<py::ssize_t>(v.size()), v.data());
            },
+           py::arg("rank"), py::arg("which") = 0)
+      .def("field_hash", [](GpuGroup& g, int rank, int which) { return g.rank(rank).field_hash(which); },
            py::arg("rank"), py::arg("which") = 0)
       .def("layout", [](GpuGroup& g, int rank) { return g.rank(rank).layout(); })
       .def("dims", [](GpuGroup& g) { return g.rank(0).dims(); })

@@ -206,11 +206,16 @@ void launch_unpack(const Layout& l, const HaloPlan& plan, const double* buf, dou
 __global__ __launch_bounds__(64) void k_flag_sync(const FlagOp w, const FlagOp s) {
   const int t = static_cast<int>(threadIdx.x);
   // wait until every watched word equals the value (bounded: after `ticks` of the 100 MHz wall clock the status word
-  // records a timeout and the kernel ends, so a lost peer turns into a host-side error instead of a hung queue)
+  // records a timeout and the kernel ends, so a lost peer turns into a host-side error instead of a hung queue).
+  // Once any wait of this solve has timed out (status set, by this kernel or an earlier one on any stream of the rank)
+  // the solve is lost: later waits return at once, so the rest of the solve drains in microseconds and a lost peer
+  // costs one bound per solve, not one per wait. The status word is re-read inside
+  // the spin too, so the lanes of one kernel (and concurrent kernels on the copy streams) give up together.
   if (t < w.n) {
+    auto lost = [&] { return __hip_atomic_load(w.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u; };
     const unsigned long long t0 = wall_clock64();
     unsigned* a = w.addr[t];
-    while (__hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != w.value) {
+    while (!lost() && __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != w.value) {
       if (wall_clock64() - t0 > w.ticks) {
         __hip_atomic_store(w.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
@@ -226,6 +231,42 @@ void launch_flag_sync(const FlagOp& wait, const FlagOp& signal, hipStream_t stre
   W3D_REQUIRE(wait.n <= FlagOp::kMax && signal.n <= FlagOp::kMax && wait.n >= 0 && signal.n >= 0, "flag op: too many");
   if (wait.n == 0 && signal.n == 0) return;
   hipLaunchKernelGGL(k_flag_sync, dim3(1), dim3(64), 0, stream, wait, signal);
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// Field hash (autotune field check): one workgroup per group of owned rows, a 64-bit sum that does not depend on the
+// order in which nodes are visited, so it is the same for any decomposition of the same global field.
+// ------------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {  // (splitmix64 finaliser)
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_field_hash(const double* f, const Layout l, unsigned long long* out) {
+  unsigned long long acc = 0;
+  const i64 rows = l.nx * l.ny, n1 = l.N + 1;
+  for (i64 r = blockIdx.x; r < rows; r += gridDim.x) {
+    const i64 x = r / l.ny, y = r - x * l.ny;
+    const double* row = f + l.off(x, y, 0);
+    const i64 g = ((l.gx0 + x) * n1 + (l.gy0 + y)) * n1 + l.gz0;
+    for (i64 z = threadIdx.x; z < l.nz; z += blockDim.x)
+      acc += mix64(static_cast<unsigned long long>(__double_as_longlong(row[z])) ^ mix64(static_cast<unsigned long long>(g + z)));
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
+}
+
+void launch_field_hash(const Layout& l, const double* f, unsigned long long* out, hipStream_t stream) {
+  const i64 rows = l.nx * l.ny;
+  if (rows <= 0 || l.nz <= 0) return;
+  const unsigned blocks = static_cast<unsigned>(imin(rows, static_cast<i64>(4096)));
+  hipLaunchKernelGGL(k_field_hash, dim3(blocks), dim3(256), 0, stream, f, l, out);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) fail(std::string("field hash launch: ") + hipGetErrorString(e));
 }
 
 }  // namespace wave3d

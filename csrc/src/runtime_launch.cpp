@@ -1,6 +1,8 @@
 // Job launch pieces of the native runtime: launcher environments, the --np self-spawn, the RCCL unique-id rendezvous
 // and host collectives. See wave3d/runtime.hpp. (The reference launches with `mpirun -np P` under LSF, report.pdf
 // p.12-15; here torchrun / mpiexec / srun environments or the built-in spawn)
+#include <signal.h>
+#include <sys/prctl.h>
 #include <sys/stat.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -127,15 +129,24 @@ std::vector<std::string> file_allgather(int rank, int world, const std::string& 
   return all;
 }
 
+// The ranks live and die with the spawner: each child asks the kernel for SIGKILL when its parent
+// exits (PR_SET_PDEATHSIG, before it touches the GPU), so a spawner killed by a timeout takes its ranks along instead
+// of leaving them spinning on the GPU; and once one rank has failed, the spawner gives the others W3D_SPAWN_GRACE_S
+// (default 20 s) to report their own error (a peer's lost-neighbour timeout) and then kills the rest.
 int spawn_ranks(int np) {
   std::ostringstream rf;
   rf << "/tmp/wave3d-rdzv-spawn-" << getpid() << "-" << static_cast<long long>(wall_s() * 1e6) << ".uid";
   const std::string rdzv = rf.str();
+  const pid_t parent = getpid();
   std::vector<pid_t> kids;
   for (int r = 0; r < np; ++r) {
     const pid_t pid = fork();
-    if (pid < 0) fail("fork failed");
+    if (pid < 0) {
+      for (pid_t k : kids) kill(k, SIGKILL);
+      fail("fork failed");
+    }
     if (pid == 0) {
+      if (prctl(PR_SET_PDEATHSIG, SIGKILL) != 0 || getppid() != parent) _exit(125);  // (parent already gone)
       setenv("RANK", std::to_string(r).c_str(), 1);
       setenv("LOCAL_RANK", std::to_string(r).c_str(), 1);
       setenv("WORLD_SIZE", std::to_string(np).c_str(), 1);
@@ -145,12 +156,32 @@ int spawn_ranks(int np) {
     }
     kids.push_back(pid);
   }
-  int rc = 0;
-  for (pid_t k : kids) {
+  double grace = 20.0;
+  if (const char* g = std::getenv("W3D_SPAWN_GRACE_S"); g && std::atof(g) >= 0.0) grace = std::atof(g);
+  int rc = 0, left = np;
+  double t_fail = -1.0;
+  std::vector<char> alive(static_cast<size_t>(np), 1);
+  while (left > 0) {
     int st = 0;
-    waitpid(k, &st, 0);
+    const pid_t k = waitpid(-1, &st, WNOHANG);
+    if (k < 0) break;  // (no children left)
+    if (k == 0) {
+      if (t_fail >= 0.0 && wall_s() - t_fail > grace) {
+        for (int r = 0; r < np; ++r)
+          if (alive[static_cast<size_t>(r)]) kill(kids[static_cast<size_t>(r)], SIGKILL);
+        t_fail = 1e300;  // (killed once; keep reaping)
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+      continue;
+    }
+    for (int r = 0; r < np; ++r)
+      if (kids[static_cast<size_t>(r)] == k) alive[static_cast<size_t>(r)] = 0;
+    --left;
     const int c = WIFEXITED(st) ? WEXITSTATUS(st) : 128 + (WIFSIGNALED(st) ? WTERMSIG(st) : 0);
-    if (c != 0 && rc == 0) rc = c;
+    if (c != 0 && rc == 0) {
+      rc = c;
+      if (t_fail < 0.0) t_fail = wall_s();
+    }
   }
   std::remove(rdzv.c_str());
   return rc;

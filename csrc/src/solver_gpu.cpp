@@ -988,7 +988,11 @@ void GpuSolver::flush_reduces() {
 }
 
 void GpuSolver::enqueue_solve() {
+  if (sdma_) sdma_check_connected();
   phase_init();
+  // copy-engine flag values are 16-bit unit indices under a parity bit (xval / xend): more units per solve would alias
+  // the end-of-solve word and the other parity's range
+  W3D_REQUIRE(!sdma_ || units_.size() < 0xFFFEu, "sdma transport: too many passes in one solve for the flag encoding");
   tb_region_ = 0;
   pending_.clear();
   const bool late = late_exchange();
@@ -1312,6 +1316,22 @@ std::vector<double> GpuSolver::download(int which) const {
   W3D_HIP(hipSetDevice(dev_));
   W3D_HIP(hipDeviceSynchronize());
   W3D_HIP(hipMemcpy(h.data(), src, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+  W3D_HIP(hipSetDevice(cur));
+  return h;
+}
+
+unsigned long long GpuSolver::field_hash(int which) const {
+  int cur = 0;
+  W3D_HIP(hipGetDevice(&cur));
+  W3D_HIP(hipSetDevice(dev_));
+  W3D_HIP(hipDeviceSynchronize());
+  unsigned long long* d = nullptr;
+  W3D_HIP(hipMalloc(&d, sizeof(unsigned long long)));
+  W3D_HIP(hipMemset(d, 0, sizeof(unsigned long long)));
+  launch_field_hash(lay_, u_[which == 0 ? final_buf_ : prev_buf_], d, nullptr);
+  unsigned long long h = 0;
+  W3D_HIP(hipMemcpy(&h, d, sizeof h, hipMemcpyDeviceToHost));
+  W3D_HIP(hipFree(d));
   W3D_HIP(hipSetDevice(cur));
   return h;
 }

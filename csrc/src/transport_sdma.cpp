@@ -205,20 +205,35 @@ void GpuSolver::connect_sdma_self() {
   }
 }
 
-namespace {
-// bound of one flag wait in wall-clock ticks: min(W3D_TIMEOUT_S (default 300), 60) s
-unsigned long long flag_ticks() {
-  static const unsigned long long t = [] {
-    const char* v = std::getenv("W3D_TIMEOUT_S");
-    double sec = v ? std::atof(v) : 0.0;
-    sec = sec > 0.0 ? std::min(sec, 60.0) : 60.0;
-    int khz = 100000;
-    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
-    return static_cast<unsigned long long>(sec * 1e3 * khz);
-  }();
-  return t;
+void GpuSolver::sdma_check_connected() const {
+  for (const XLink& l : xlinks_) {
+    bool ok = l.flags != nullptr;
+    if (block_tb_)
+      ok = ok && l.recv != nullptr;
+    else
+      for (int b = 0; b < nbuf_; ++b) ok = ok && l.u[b] != nullptr;
+    W3D_REQUIRE(ok, "sdma transport: neighbour " + std::to_string(l.peer) +
+                        " not connected (connect_sdma / connect_sdma_self before the first solve)");
+  }
 }
-}  // namespace
+
+// Bound of one flag wait in wall-clock ticks: SolverOptions::flag_timeout_s, else min(W3D_TIMEOUT_S (default 300) / 2,
+// 60) s — below the host's own wait bound (wait_stream), so a lost peer is reported by the device ("a flag wait timed
+// out") rather than by the host timer, and with k_flag_sync's early exit the whole solve then ends within one bound.
+unsigned long long GpuSolver::flag_ticks() const {
+  static const int khz = [] {
+    int k = 100000;
+    (void)hipDeviceGetAttribute(&k, hipDeviceAttributeWallClockRate, 0);
+    return k;
+  }();
+  double sec = opt_.flag_timeout_s;
+  if (sec <= 0.0) {
+    const char* v = std::getenv("W3D_TIMEOUT_S");
+    const double host = v && std::atof(v) > 0.0 ? std::atof(v) : 300.0;
+    sec = std::min(0.5 * host, 60.0);
+  }
+  return static_cast<unsigned long long>(sec * 1e3 * khz);
+}
 
 // Exchange i: on the side stream once the shells are written (overlap), else on s0 after the pass.
 void GpuSolver::unit_exchange_sdma(int i) {

@@ -241,6 +241,16 @@ class Solver:
     def native(self):
         return self._impl
 
+    def field_hash(self, which: int = 0) -> int:
+        """Order-independent 64-bit hash of u^K (which=0) / u^{K-1} (which=1) over the nodes this process owns (an
+        in-process group: over all its ranks), mod 2**64. Summed over the ranks of a job it does not depend on the
+        decomposition or schedule of a bit-identical solve (the autotune's field check, GpuSolver::field_hash)."""
+        if self.backend != "hip" or self.transport == "torch":
+            raise ValueError("field_hash needs the native HIP backend")
+        if isinstance(self._impl, load().GpuGroup):
+            return sum(self._impl.field_hash(r, which) for r in range(self._impl.world)) % (1 << 64)
+        return int(self._impl.field_hash(which))
+
     def global_field(self, which: int = 0) -> torch.Tensor:
         """The whole (N+1)³ field u^K (which=0) / u^{K-1} (which=1) on the CPU (single rank or loopback group)."""
         from .ops.stencil import grid_view

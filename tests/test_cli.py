@@ -101,6 +101,53 @@ def test_cpu_multiprocess_rank_failure_is_an_error():
     assert time.time() - t0 < 30
 
 
+def _children(pid):
+    try:
+        with open(f"/proc/{pid}/task/{pid}/children") as f:
+            return [int(c) for c in f.read().split()]
+    except OSError:
+        return []
+
+
+def _alive(pid):
+    """A process that exists and is not a zombie (an orphan's zombie waits for a reaper; it runs nothing)."""
+    try:
+        with open(f"/proc/{pid}/status") as f:
+            state = next(l for l in f if l.startswith("State:"))
+        return "Z" not in state.split()[1]
+    except (OSError, StopIteration):
+        return False
+
+
+def test_spawned_ranks_die_with_the_spawner():
+    """`--np P` ranks are forked children of the spawner; when the spawner is killed (a test or
+    bench timeout sends SIGKILL to the process it started, not to its children) the ranks must not keep running — each
+    child holds PR_SET_PDEATHSIG = SIGKILL."""
+    import signal
+    import time
+
+    p = subprocess.Popen([CLI, "96", "0.001", "20", "--cpu", "--np", "2", "--threads", "1", "--repeat", "100000",
+                          "--quiet"], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        t0 = time.time()
+        kids = []
+        while len(kids) < 2 and time.time() - t0 < 30:
+            kids = _children(p.pid)
+            time.sleep(0.05)
+        assert len(kids) == 2, kids
+        time.sleep(0.5)  # (mid-solve)
+        assert all(_alive(k) for k in kids)
+        os.kill(p.pid, signal.SIGKILL)
+        p.wait(timeout=10)
+        t1 = time.time()
+        while any(_alive(k) for k in kids) and time.time() - t1 < 10:
+            time.sleep(0.05)
+        assert not any(_alive(k) for k in kids), [k for k in kids if _alive(k)]
+    finally:
+        if p.poll() is None:
+            p.kill()
+
+
 def test_reference_program_personalities():
     """The build links the reference's program names to the CLI (tools/build.py); argv[0] picks the behaviour:
     `wave N tau K` sequential, `wave3dOMP N tau K T` / `mpiomp N tau K T` take OpenMP threads as the 4th argument,

@@ -96,3 +96,43 @@ def test_block_overlap_label_is_honest(gpu, tmp_path):
                         "--quiet", *extra], check=True, timeout=120)
         meta = json.loads(open(js).read())
         assert meta["mode"] == "deep-tb-block" and meta["overlap"] is want
+
+
+def test_autotune_times_medians_of_back_to_back_solves(gpu, tmp_path):
+    """each candidate is timed in rounds of back-to-back solves (the bench's pattern) and
+    chosen on the MEDIAN round, not the best one; the JSON carries both, the rounds x reps and the autotune's wall
+    time."""
+    meta, _ = _run(tmp_path, "128", "0.001", "20", "1", "--fake-rank", "1/4", "--autotune-rounds", "3",
+                   "--autotune-reps", "4")
+    med, best = meta["autotune_s"], meta["autotune_best_s"]
+    assert set(med) == set(best) and meta["autotune_rounds"] == 3 and meta["autotune_reps"] == 4
+    assert all(best[k] <= med[k] for k in med)
+    assert 0 < meta["autotune_wall_s"] < 120
+    _chosen_ok(meta)
+
+
+def test_autotune_wall_budget(gpu, tmp_path):
+    """once the wall-time budget is spent no further candidate is built (rejected with the
+    reason) and at least one round still times what was accepted."""
+    meta, _ = _run(tmp_path, "128", "0.001", "20", "1", "--fake-rank", "1/4", "--autotune-budget", "0.001")
+    rej = meta["autotune_rejected"]
+    assert any("budget" in v for v in rej.values())
+    assert len(meta["autotune_s"]) >= 1 and meta["autotune_rounds"] >= 1
+    assert meta["schedule"] in meta["autotune_s"]
+
+
+def test_field_hash_is_decomposition_free(gpu):
+    """The autotune's field check: the hash of u^K and u^{K-1} summed over the ranks equals the one-rank hash for slab
+    and block groups (bit-identical fields), and a different field (one step fewer) hashes differently."""
+    spec = ProblemSpec(N=66, tau=1e-3, K=20)
+    ref = Solver(spec, backend="hip", device=0)
+    ref.run()
+    h0, h1 = ref.field_hash(0), ref.field_hash(1)
+    assert h0 != h1
+    for decomp, world in (("slab", 3), ("2x2x2", 8)):
+        g = Solver(spec, backend="hip", transport="loopback", world=world, rank=0, decomp=decomp, device=0)
+        g.run()
+        assert g.field_hash(0) == h0 and g.field_hash(1) == h1
+    other = Solver(ProblemSpec(N=66, tau=1e-3, K=19), backend="hip", device=0)
+    other.run()
+    assert other.field_hash(0) != h0 and other.field_hash(0) == h1

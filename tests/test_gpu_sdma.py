@@ -172,3 +172,42 @@ def test_bench_two_ranks_sdma_rehearsal(gpu, tmp_path):
     assert line["n_gpus"] == 2 and line["distinct_gpus"] == 1 and "rehearsal" in line
     assert line["config"]["transport"] == "sdma" and line["config"]["schedule"].endswith("-sdma")
     assert line["correct"] is True and line["final_max_err"] == pytest.approx(3.960129e-09, rel=1e-6)
+
+
+def test_sdma_unconnected_solver_refuses_to_run(gpu):
+    """a copy-engine solver whose links were never connected (no connect_sdma / connect_sdma_self / group)
+    must fail on the host with a clear error instead of letting the copy engines and flag kernels write through null
+    peer pointers (a GPU memory fault)."""
+    from mpi_cuda_amd._native import load
+
+    C = load()
+    opts = C.SolverOptions()
+    opts.sdma = True
+    opts.push_no_collective = True  # (no communicator: the transport alone)
+    s = C.GpuSolver(ProblemSpec(N=66, tau=1e-3, K=20).native(), opts, 0, 2, None)
+    assert s.sdma and s.transport == "sdma"
+    with pytest.raises(Exception, match="not connected"):
+        s.run()
+
+
+def test_sdma_lost_peer_fails_within_one_bound(gpu, tmp_path):
+    """rank 1 of 2 copy-engine processes (sharing the GPU, no RCCL) vanishes right after the
+    barrier of its third solve. Rank 0 runs that solve alone: its first flag wait times out after the device bound
+    (W3D_TIMEOUT_S / 2), every later wait of the solve returns at once (k_flag_sync reads the status word), and the rank
+    reports the lost neighbour and exits non-zero — the whole job within 1.2 x W3D_TIMEOUT_S of the fault (before the
+    fix each of the solve's ~10 waits spun its full bound)."""
+    import time
+
+    T = 20.0
+    env = dict(ENV, W3D_SHARE_GPUS="1", W3D_TIMEOUT_S=str(T), W3D_FAULT_RANK="1", W3D_FAULT_AT_SOLVE="2",
+               W3D_SPAWN_GRACE_S="60")
+    env.pop("W3D_RDZV_FILE", None)
+    cmd = [CLI, "96", "0.001", "20", "1", "--np", "2", "--transport", "sdma", "--no-rccl", "--warmup", "1",
+           "--repeat", "4", "--quiet"]
+    t0 = time.perf_counter()
+    p = subprocess.run(cmd, env=env, timeout=120, capture_output=True, text=True)
+    dt = time.perf_counter() - t0
+    assert p.returncode != 0
+    assert "injected fault" in p.stderr
+    assert "flag wait timed out on rank 0" in p.stderr, p.stderr[-2000:]
+    assert dt < 1.2 * T + 10.0, f"{dt:.1f} s"  # (+ process start, RCCL-free setup and the two good solves)

@@ -156,10 +156,26 @@ int run_gpu(const Args& a) {
   const char* fas = std::getenv("W3D_FAULT_AT_SOLVE");
   const char* frk = std::getenv("W3D_FAULT_RANK");
   const int fault_at = fas && frk && std::atoi(frk) == rank ? std::atoi(fas) : -1;
+  // --verify-repeat: this rank's local error log and field hash after every solve against the first solve's
+  std::vector<double> ref_max, ref_rms;
+  unsigned long long ref_hash = 0;
+  int mismatches = 0;
   for (int i = 0; i < a.warmup + a.repeat; ++i) {
     hc.barrier();
     if (i == fault_at) fail("injected fault: rank " + std::to_string(rank) + " lost before solve " + std::to_string(i));
     r = s->run();
+    if (a.verify_repeat) {
+      const unsigned long long h = s->field_hash(0);
+      if (i == 0) {
+        ref_max = r.max_err;
+        ref_rms = r.rms_err;
+        ref_hash = h;
+      } else if (r.max_err != ref_max || r.rms_err != ref_rms || h != ref_hash) {
+        if (mismatches++ < 5)
+          std::fprintf(stderr, "wave3d: rank %d solve %d differs from solve 0 (field hash %016llx vs %016llx)\n", rank,
+                       i, h, ref_hash);
+      }
+    }
     const double t = hc.max(r.solve_s);
     if (i == 0) first = t;
     if (i >= a.warmup) {
@@ -212,6 +228,13 @@ int run_gpu(const Args& a) {
       r.rms_err[i] = std::sqrt(q);
     }
   }
+  if (a.verify_repeat) {
+    const int bad = static_cast<int>(hc.max(static_cast<double>(mismatches)));
+    if (rank == 0 || fake)
+      std::printf("Repeat check: %d solves per rank, %s\n", a.warmup + a.repeat,
+                  bad ? "SOME SOLVES DIFFER from the first" : "every solve bit-identical to the first on every rank");
+    if (bad) return 4;
+  }
   const double mean = sum / a.repeat;
   const double t_proc = wall_s() - t_proc0;
   const Dims d = s->dims();
@@ -232,6 +255,10 @@ int run_gpu(const Args& a) {
         " overlap %s\n",
         gcell, t_proc, t_comm, rccl_nranks, s->mode().c_str(), sched.c_str(), s->options().graph ? "on" : "off",
         s->overlapped() ? "on" : "off");
+    const GpuSolver::Traffic tr = s->traffic();
+    std::printf("Traffic%s: %.3f GB of compulsory field reads + writes per solve = %.0f GB/s effective; halo %.2f MB"
+                " sent per solve\n",
+                world > 1 ? " (this rank)" : "", tr.field_bytes / 1e9, tr.field_bytes / best / 1e9, tr.halo_bytes / 1e6);
     if (a.bench_steps > 0)
       std::printf("Bench: %d solves in %.6f s (%.6f s per solve, max over ranks)\n", a.bench_steps, bench_s,
                   bench_s / a.bench_steps);
@@ -250,6 +277,8 @@ int run_gpu(const Args& a) {
         << ", \"first_s\": " << jnum(first) << ", \"process_s\": " << jnum(t_proc) << ", \"rccl_init_s\": "
         << jnum(t_comm) << ", \"rccl_nranks\": " << rccl_nranks << ", \"rccl_version\": " << rccl_version()
         << ", \"hip_runtime\": " << hipv << ", \"gcell_per_s\": " << jnum(gcell)
+        << ", \"field_bytes\": " << jnum(tr.field_bytes) << ", \"halo_bytes\": " << jnum(tr.halo_bytes)
+        << ", \"effective_gbs\": " << jnum(tr.field_bytes / best / 1e9)
         << ", \"graph\": " << (s->options().graph ? "true" : "false") << ", \"overlap\": "
         << (s->overlapped() ? "true" : "false") << ", \"overlap_requested\": " << (s->options().overlap ? "true" : "false")
         << ", \"temporal\": " << s->options().temporal

@@ -204,6 +204,15 @@ class GpuSolver {
   }
   // halo transport actually in use: "none" (one rank), "rccl", "push", "sdma", "fake" (perf study, no transport)
   std::string transport() const;
+  // Bytes one solve moves, from the unit schedule (SURVEY.md §5.5 effective GB/s). field_bytes: the compulsory
+  // device-memory traffic over the nodes this rank updates — a fused pass reads u^n, u^{n−1} and writes two levels,
+  // an analytic-start pass only writes its two, a single step reads two and writes one, the init kernel writes two;
+  // tile-halo re-reads that miss L2 are not in it (rocprof FETCH_SIZE counts those). halo_bytes: what this rank sends
+  // its neighbours per solve (RCCL / copy-engine messages, or the push transport's forwarded face planes).
+  struct Traffic {
+    double field_bytes = 0.0, halo_bytes = 0.0;
+  };
+  Traffic traffic();
 
  private:
   friend class GpuGroup;

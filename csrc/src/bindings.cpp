@@ -501,6 +501,15 @@ PYBIND11_MODULE(_C, m) {
            "map every neighbour's buffers and flag words from all ranks' sdma_handles() (index = rank)")
       .def_property_readonly("overlapped", &GpuSolver::overlapped)
       .def_property_readonly("transport", &GpuSolver::transport)
+      .def("traffic",
+           [](GpuSolver& s) {
+             const GpuSolver::Traffic t = s.traffic();
+             py::dict d;
+             d["field_bytes"] = t.field_bytes;
+             d["halo_bytes"] = t.halo_bytes;
+             return d;
+           },
+           "bytes one solve of the last run()'s schedule moves: compulsory field reads + writes, halo bytes sent")
       .def("run",
            [](GpuSolver& s) {
              RunResult r;

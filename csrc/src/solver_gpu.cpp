@@ -474,6 +474,31 @@ std::string GpuSolver::transport() const {
   return "rccl";
 }
 
+// (the schedule of the last run(): units_ and analytic_ are rebuilt at the start of every solve)
+GpuSolver::Traffic GpuSolver::traffic() {
+  Traffic t;
+  const double node_bytes = static_cast<double>(lay_.cx1 - lay_.cx0) * static_cast<double>(lay_.cy1 - lay_.cy0) *
+                            static_cast<double>(lay_.cz1 - lay_.cz0) * sizeof(double);
+  if (!analytic_ && resume_n_ == 0) t.field_bytes += 2.0 * node_bytes;  // init kernel: u¹, u² (or u⁰, u¹)
+  for (const Unit& u : units_) t.field_bytes += node_bytes * (u.analytic ? 2.0 : u.fused() ? 4.0 : 3.0);
+  if (push_) {  // each pass but the last forwards T planes of u^{n+S} and T − 1 of u^{n+S−1} per face
+    const double T = static_cast<double>(lay_.xg);
+    t.halo_bytes = static_cast<double>(plan_.faces.size()) * (2.0 * T - 1.0) * static_cast<double>(lay_.plane) *
+                   sizeof(double) * static_cast<double>(units_.empty() ? 0 : units_.size() - 1);
+    return t;
+  }
+  const std::vector<Msg> keep = msgs_;
+  const int keep_s = deep_s_;
+  for (int i = 0; i < static_cast<int>(units_.size()); ++i) {
+    if (!needs_exchange(i)) continue;
+    build_msgs(i);
+    for (const Msg& m : msgs_) t.halo_bytes += static_cast<double>(m.count) * sizeof(double);
+  }
+  msgs_ = keep;
+  deep_s_ = keep_s;
+  return t;
+}
+
 std::string GpuSolver::mode() const {
   switch (mode_) {
     case Mode::kFusedSingle: return "fused-single";

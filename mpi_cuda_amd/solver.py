@@ -241,6 +241,14 @@ class Solver:
     def native(self):
         return self._impl
 
+    def traffic(self) -> dict:
+        """Bytes one solve of the last run()'s schedule moves on this rank (native HIP backend, one rank or a
+        process-per-rank job): ``field_bytes`` = compulsory field reads + writes of the pass schedule (SURVEY.md §5.5:
+        divide by the solve time for the effective GB/s), ``halo_bytes`` = what this rank sends its neighbours."""
+        if self.backend != "hip" or self.transport == "torch" or not hasattr(self._impl, "traffic"):
+            raise ValueError("traffic needs the native HIP backend with one solver per process")
+        return dict(self._impl.traffic())
+
     def field_hash(self, which: int = 0) -> int:
         """Order-independent 64-bit hash of u^K (which=0) / u^{K-1} (which=1) over the nodes this process owns (an
         in-process group: over all its ranks), mod 2**64. Summed over the ranks of a job it does not depend on the

@@ -211,3 +211,27 @@ def test_sdma_lost_peer_fails_within_one_bound(gpu, tmp_path):
     assert "injected fault" in p.stderr
     assert "flag wait timed out on rank 0" in p.stderr, p.stderr[-2000:]
     assert dt < 1.2 * T + 10.0, f"{dt:.1f} s"  # (+ process start, RCCL-free setup and the two good solves)
+
+
+def test_sdma_halo_visibility_stress(gpu, tmp_path):
+    """the copy-engine protocol relies on the receiver's next pass dropping stale L2 lines of the
+    ghost regions the copy engines wrote (transport_sdma.cpp header). At N = 48 every field is L2-resident and each
+    pass reads its ghost planes right before the peer's copy overwrites them for the next pass; 2 processes share the
+    GPU, every step is checked, and each of 60 solves per process must reproduce the first solve's error log and u^K
+    field hash bit for bit (--verify-repeat) — one invocation, not repeated runs."""
+    N, K = 48, 40
+    r1, f1 = _single(N, K, check_every=1)
+    prefix, js = str(tmp_path / "v"), str(tmp_path / "v.json")
+    env = dict(ENV, W3D_SHARE_GPUS="1")
+    env.pop("W3D_RDZV_FILE", None)
+    cmd = [CLI, str(N), "0.001", str(K), "1", "--np", "2", "--transport", "sdma", "--no-rccl", "--check-every", "1",
+           "--warmup", "10", "--repeat", "50", "--verify-repeat", "--dump", prefix, "--json", js, "--quiet"]
+    p = subprocess.run(cmd, timeout=150, env=env, capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "every solve bit-identical to the first on every rank" in p.stdout
+    meta = json.loads(open(js).read())
+    assert meta["transport"] == "sdma" and meta["graph"] is True
+    _assert_same_field(_read_dump(prefix, 2, N), f1)
+    assert [s[0] for s in meta["steps"]] == r1.steps
+    for (n, m, e), m1, e1 in zip(meta["steps"], r1.max_err, r1.rms_err):
+        assert m == pytest.approx(m1, rel=1e-9) and e == pytest.approx(e1, rel=1e-9)

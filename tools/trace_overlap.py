@@ -6,11 +6,19 @@ from the trace of a run, how much of the copy time ran while a k_leapfrog_tb pas
 transport: no compute unit is taken from the pass), and a per-kind time table.
 
     python tools/trace_overlap.py gpurun_out/trace_sdma        # a rocprofv3 -d directory (searched recursively)
+    python tools/trace_overlap.py gpurun_out/trace_sdma --json run.json --solves 12
+
+The memory-copy CSV of rocprofv3 (ROCm 7.2) carries no size column, so the copy volume comes from the solver's own
+schedule: ``--json`` names the ``bin/wave3d --json`` output of the traced run (``halo_bytes`` = bytes this rank sends
+per solve, GpuSolver::traffic) and ``--solves`` the number of solves in the trace (warmup included). A CSV that does
+carry a size column (``Bytes`` / ``Size`` / ``Copy_Bytes``) is summed directly.
 """
 from __future__ import annotations
 
+import argparse
 import csv
 import glob
+import json
 import os
 import re
 import sys
@@ -62,25 +70,41 @@ def analyse(d: str) -> dict:
         per_kind[k][1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     tot = ov = 0
     nbytes = 0
+    size_key = next((k for k in ("Bytes", "Size", "Copy_Bytes") if copies and k in copies[0]), None)
     for r in copies:
         a = (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
         tot += a[1] - a[0]
         ov += _overlap(a, merged)
-        nbytes += int(r.get("Bytes", 0) or 0)
+        if size_key:
+            nbytes += int(r.get(size_key, 0) or 0)
         k = "copy " + r.get("Direction", "?")
         per_kind[k][0] += 1
         per_kind[k][1] += a[1] - a[0]
-    return {"copies": len(copies), "copy_ns": tot, "copy_ns_during_pass": ov, "copy_bytes": nbytes,
+    return {"copies": len(copies), "copy_ns": tot, "copy_ns_during_pass": ov,
+            "copy_bytes": nbytes if size_key else None,
             "pass_ns": sum(b - a for a, b in merged), "per_kind": dict(per_kind)}
 
 
+def copy_volume(r: dict, json_path: str | None, solves: int | None) -> str:
+    """The copy-volume cell: bytes from the trace itself, else from the solver's schedule (--json/--solves)."""
+    if r["copy_bytes"] is not None:
+        return f"{r['copy_bytes'] / 1e6:.1f} MB (trace)"
+    if json_path and solves:
+        with open(json_path) as f:
+            halo = float(json.load(f)["halo_bytes"])
+        return f"{halo * solves / 1e6:.1f} MB ({solves} solves x {halo / 1e6:.2f} MB from the schedule)"
+    return "size not in the trace (pass --json/--solves)"
+
+
 def main(argv: list[str]) -> int:
-    if not argv:
-        print(__doc__)
-        return 2
-    r = analyse(argv[0])
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("trace_dir")
+    ap.add_argument("--json", help="bin/wave3d --json output of the traced run (halo_bytes per solve)")
+    ap.add_argument("--solves", type=int, help="solves in the trace (warmup included)")
+    a = ap.parse_args(argv)
+    r = analyse(a.trace_dir)
     print(f"| item | value |\n|---|---|")
-    print(f"| memory copies | {r['copies']} ({r['copy_bytes'] / 1e6:.1f} MB) |")
+    print(f"| memory copies | {r['copies']} ({copy_volume(r, a.json, a.solves)}) |")
     print(f"| copy time | {r['copy_ns'] / 1e6:.3f} ms |")
     frac = r["copy_ns_during_pass"] / r["copy_ns"] if r["copy_ns"] else 0.0
     print(f"| copy time while a k_leapfrog_tb pass ran | {r['copy_ns_during_pass'] / 1e6:.3f} ms ({100 * frac:.1f} %) |")

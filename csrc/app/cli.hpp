@@ -38,6 +38,7 @@ struct Args {
   double autotune_budget = 120.0;      // --autotune-budget S: wall-time budget of the autotune (s)
   bool autotune_sdma = false;          // --autotune-sdma (or W3D_AUTOTUNE_SDMA=1): copy-engine candidates too
   bool phases = false;                 // --phases: per-phase breakdown from a traced solve of the timed schedule
+  bool serve = false;                  // --serve: keep the solver up, one command per stdin line (Python runtime="process")
   bool verify_repeat = false;          // --verify-repeat: every solve's error log and field hash equal the first's
   std::string group_transport = "rccl-self";
   std::string transport = "rccl";      // --transport rccl | push (slab LDS passes: halos pushed by the passes)

@@ -77,6 +77,8 @@ constexpr Personality kPersonalities[] = {
                "  --autotune-budget S  wall-time budget of the autotune in seconds (default 120; 0: none)\n"
                "  --autotune-sdma    include the copy-engine candidates across GPUs (also W3D_AUTOTUNE_SDMA=1)\n"
                "  --phases           per-phase device times (init/compute/exchange/check) of the timed schedule\n"
+               "  --serve            keep the solver up: run / hash W / traffic / dump P / quit, one per stdin line,\n"
+               "                     one JSON reply line each (the Python Solver(runtime=\"process\") rank process)\n"
                "  --verify-repeat    every solve (warmup included) must reproduce the first one's error log and u^K\n"
                "                     field hash on this rank bit for bit (exit 4 otherwise): halo-visibility stress\n"
                "  --variant V        leapfrog kernel: 1 = register-queue waves (default), 0 = LDS-staged tile\n"
@@ -151,6 +153,7 @@ Args parse(int argc, char** argv) {
     else if (s == "--autotune-sdma") a.autotune_sdma = true;
     else if (s == "--phases") a.phases = true;
     else if (s == "--verify-repeat") a.verify_repeat = true;
+    else if (s == "--serve") a.serve = true;
     else if (s == "--group-transport") a.group_transport = next();
     else if (s == "--transport") a.transport = next();
     else if (s == "--push-cp-wait") a.push_cp_wait = true;

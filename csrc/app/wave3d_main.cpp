@@ -38,6 +38,101 @@ using namespace wave3d::cli;
 
 namespace {
 
+// Ranks without a communicator (--no-rccl): the solve's error log over all ranks through the host collectives (L∞:
+// max; RMS: from the per-rank Σe² shares)
+void combine_logs(RunResult& r, const HostColl& hc) {
+  std::string mine;
+  for (size_t i = 0; i < r.steps.size(); ++i) {
+    const double v[2] = {r.max_err[i], r.rms_err[i] * r.rms_err[i]};
+    mine.append(reinterpret_cast<const char*>(v), sizeof v);
+  }
+  const std::vector<std::string> all = hc.allgather(mine);
+  for (size_t i = 0; i < r.steps.size(); ++i) {
+    double m = 0.0, q = 0.0;
+    for (const std::string& b : all) {
+      double v[2];
+      std::memcpy(v, b.data() + i * sizeof v, sizeof v);
+      m = v[0] > m || std::isnan(v[0]) ? v[0] : m;
+      q += v[1];
+    }
+    r.max_err[i] = m;
+    r.rms_err[i] = std::sqrt(q);
+  }
+}
+
+// --serve: the rank's solver stays up and takes one command per stdin line, answering each with one JSON line on
+// stdout — the native rank process behind the Python Solver(runtime="process") (mpi_cuda_amd/parallel/native_proc.py):
+// a torch process cannot capture the multi-rank schedules (HIP 7.0 runtime, see multistream_capture_safe), this
+// process's ROCm 7.2 runtime can. Every rank must receive the same command sequence (run and quit are collective).
+//   run            one solve (barrier first): {"solve_s" (max over ranks), "local_s", "graph", "finite", "steps"}
+//   hash W         field_hash of u^K (W = 0) / u^{K−1} (W = 1) over this rank's owned nodes
+//   traffic        GpuSolver::traffic of the last solve's schedule
+//   dump PREFIX    write u^K of this rank (wave3d-dump-v1)
+//   quit           leave the loop (exit status 0)
+int serve(const Args& a, GpuSolver& s, const HostColl& hc, bool file_coll, const std::string& sched) {
+  auto jx = [](double v) {  // (every digit: the Python side compares logs and byte counts exactly)
+    char b[40];
+    std::snprintf(b, sizeof b, "%.17g", v);
+    return std::string(b);
+  };
+  auto reply = [](const std::string& line) {
+    std::fputs(line.c_str(), stdout);
+    std::fputc('\n', stdout);
+    std::fflush(stdout);
+  };
+  const Dims d = s.dims();
+  {
+    std::ostringstream o;
+    o << "{\"ready\": true, \"rank\": " << s.rank() << ", \"world\": " << s.world() << ", \"dims\": [" << d.px
+      << ", " << d.py << ", " << d.pz << "], \"schedule\": " << jstr(sched) << ", \"mode\": " << jstr(s.mode())
+      << ", \"transport\": " << jstr(s.transport()) << "}";
+    reply(o.str());
+  }
+  std::string line;
+  while (std::getline(std::cin, line)) {
+    std::istringstream in(line);
+    std::string cmd;
+    in >> cmd;
+    std::ostringstream o;
+    try {
+      if (cmd == "run") {
+        hc.barrier();
+        RunResult r = s.run();
+        const double t = hc.max(r.solve_s);
+        if (file_coll) combine_logs(r, hc);
+        o << "{\"solve_s\": " << jx(t) << ", \"local_s\": " << jx(r.solve_s) << ", \"graph\": "
+          << (s.options().graph ? "true" : "false") << ", \"overlap\": " << (s.overlapped() ? "true" : "false")
+          << ", \"finite\": " << (r.finite ? "true" : "false") << ", \"steps\": [";
+        for (size_t i = 0; i < r.steps.size(); ++i)
+          o << (i ? ", " : "") << "[" << r.steps[i] << ", " << jx(r.max_err[i]) << ", " << jx(r.rms_err[i]) << "]";
+        o << "]}";
+      } else if (cmd == "hash") {
+        int w = 0;
+        in >> w;
+        o << "{\"hash\": \"" << std::to_string(s.field_hash(w)) << "\"}";
+      } else if (cmd == "traffic") {
+        const GpuSolver::Traffic tr = s.traffic();
+        o << "{\"field_bytes\": " << jx(tr.field_bytes) << ", \"halo_bytes\": " << jx(tr.halo_bytes) << "}";
+      } else if (cmd == "dump") {
+        std::string prefix;
+        in >> prefix;
+        write_dump(prefix, a.prob, s.layout(), s.download(0), s.rank(), s.world(), d);
+        o << "{\"dump\": " << jstr(prefix) << "}";
+      } else if (cmd == "quit") {
+        reply("{\"bye\": true}");
+        return 0;
+      } else {
+        o << "{\"error\": " << jstr("unknown command: " + cmd) << "}";
+      }
+    } catch (const std::exception& e) {
+      reply("{\"error\": " + jstr(json_escape(e.what())) + "}");
+      return 1;  // (a failed collective leaves the peers to their own timeouts: this rank is gone)
+    }
+    reply(o.str());
+  }
+  return 0;  // (stdin closed: the parent is gone)
+}
+
 int run_group(const Args& a, const SolverOptions& o, const hipDeviceProp_t& prop) {
   GpuGroup g(a.prob, o, a.group, a.group_transport);
   if (!a.resume.empty()) {
@@ -149,6 +244,13 @@ int run_gpu(const Args& a) {
     const int n0 = load_checkpoint(a.resume, a.prob, prev, cur);
     s->set_state(prev.data(), cur.data(), n0);
   }
+  if (a.serve) {
+    const int rc = serve(a, *s, hc, file_coll, sched);
+    if ((s->push() || s->sdma()) && !comm && !fake)
+      std::remove((rdzv_path() + (s->push() ? ".push" : ".sdma") + std::to_string(rank)).c_str());
+    hc.cleanup();
+    return rc;
+  }
   RunResult r;
   double best = 1e30, sum = 0, first = 0;
   // lost-peer injection: W3D_FAULT_RANK=r with W3D_FAULT_AT_SOLVE=i makes rank r vanish right after the barrier of
@@ -160,10 +262,12 @@ int run_gpu(const Args& a) {
   std::vector<double> ref_max, ref_rms;
   unsigned long long ref_hash = 0;
   int mismatches = 0;
+  std::vector<double> times;  // this rank's solve times, warmup included (--json solve_times_s: tails, parity patterns)
   for (int i = 0; i < a.warmup + a.repeat; ++i) {
     hc.barrier();
     if (i == fault_at) fail("injected fault: rank " + std::to_string(rank) + " lost before solve " + std::to_string(i));
     r = s->run();
+    times.push_back(r.solve_s);
     if (a.verify_repeat) {
       const unsigned long long h = s->field_hash(0);
       if (i == 0) {
@@ -209,25 +313,7 @@ int run_gpu(const Args& a) {
     ph.check_ms = hc.max(ph.check_ms);
     ph.gather_ms = hc.max(ph.gather_ms);
   }
-  if (file_coll) {  // the last solve's error log over all ranks (L∞: max; RMS: from the per-rank Σe² shares)
-    std::string mine;
-    for (size_t i = 0; i < r.steps.size(); ++i) {
-      const double v[2] = {r.max_err[i], r.rms_err[i] * r.rms_err[i]};
-      mine.append(reinterpret_cast<const char*>(v), sizeof v);
-    }
-    const std::vector<std::string> all = hc.allgather(mine);
-    for (size_t i = 0; i < r.steps.size(); ++i) {
-      double m = 0.0, q = 0.0;
-      for (const std::string& b : all) {
-        double v[2];
-        std::memcpy(v, b.data() + i * sizeof v, sizeof v);
-        m = v[0] > m || std::isnan(v[0]) ? v[0] : m;
-        q += v[1];
-      }
-      r.max_err[i] = m;
-      r.rms_err[i] = std::sqrt(q);
-    }
-  }
+  if (file_coll) combine_logs(r, hc);
   if (a.verify_repeat) {
     const int bad = static_cast<int>(hc.max(static_cast<double>(mismatches)));
     if (rank == 0 || fake)
@@ -301,7 +387,9 @@ int run_gpu(const Args& a) {
           << jnum(pp.interior_ms + pp.shell_ms) << ", \"shell\": " << jnum(pp.shell_ms) << ", \"exchange\": "
           << jnum(pp.comm_ms) << ", \"check\": " << jnum(pp.check_ms) << ", \"gather\": " << jnum(pp.gather_ms)
           << "}";
-      j << ", \"steps\": [";
+      j << ", \"solve_times_s\": [";
+      for (size_t i = 0; i < times.size(); ++i) j << (i ? ", " : "") << jnum(times[i]);
+      j << "], \"steps\": [";
       for (size_t i = 0; i < r.steps.size(); ++i)
         j << (i ? ", " : "") << "[" << r.steps[i] << ", " << jnum(r.max_err[i]) << ", " << jnum(r.rms_err[i]) << "]";
       j << "]}\n";

@@ -27,10 +27,15 @@ cpu        native      C++ CpuSolver, OpenMP (the reference's sequential / OpenM
 cpu        torch       Python step loop, native OpenMP kernels, halos over torch.distributed gloo (MPI analogue)
 torch      -           plain PyTorch fp64 reference solver (oracle), world == 1
 =========  ==========  =============================================================================================
+
+``runtime="process"`` (hip with rccl / sdma / push, one process per rank): the rank's production GpuSolver runs in a
+``bin/wave3d --serve`` child that stays up between ``run()`` calls and graph-captures the multi-rank schedule, which a
+torch process's HIP 7.0 runtime cannot (``parallel/native_proc.py``).
 """
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -93,7 +98,8 @@ class Solver:
                  tiling_tb: dict | None = None,
                  debug_sync: bool = False, poison_ghosts: bool = False, deep_min_planes: int | None = None,
                  tb_min_planes: int | None = None, rccl: bool = True, autotune: bool = False,
-                 autotune_rounds: int = 5, copy_engines: bool = False, fused_pack: bool = True):
+                 autotune_rounds: int = 5, copy_engines: bool = False, fused_pack: bool = True,
+                 runtime: str = "inproc"):
         import torch.distributed as dist
 
         if not spec.cfl_ok and not force:
@@ -108,6 +114,12 @@ class Solver:
         self.backend, self.transport = _resolve(backend, transport, world)
         self.decomp = decomp
         self._impl = None
+        if runtime not in ("inproc", "process"):
+            raise ValueError("runtime is 'inproc' (this process) or 'process' (a native bin/wave3d rank process)")
+        self.runtime = runtime
+        if runtime == "process":
+            self._init_process(device, decomp, temporal, overlap, graph, rccl, autotune, group)
+            return
         C = load()
         if self.backend == "hip":
             if not torch.cuda.is_available():
@@ -181,6 +193,30 @@ class Solver:
         else:
             self.dims = (1, 1, 1)
 
+    def _init_process(self, device, decomp, temporal, overlap, graph, rccl, autotune, group) -> None:
+        """runtime="process": this rank's production solver in a ``bin/wave3d --serve`` child (graph-captured under
+        the system ROCm runtime, which a torch process cannot do for multi-rank schedules; parallel/native_proc.py).
+        Transports: rccl, sdma / sdma-ipc (copy engines), push / push-ipc; one process per rank (torchrun)."""
+        from .parallel.native_proc import NativeRankProcess
+
+        if self.backend != "hip":
+            raise ValueError("runtime='process' runs the native HIP backend")
+        self.transport = {"sdma": "sdma-ipc", "push": "push-ipc"}.get(self.transport, self.transport)
+        if device is None:
+            device = self.rank % max(1, torch.cuda.device_count())  # (device_count does not initialise the GPU)
+        self.device = torch.device("cuda", device)
+        self.comm = None
+        self._impl = NativeRankProcess(self.spec, self.rank, self.world, device, self.transport, decomp, temporal,
+                                       overlap, graph, rccl, autotune, group)
+        self.dims = tuple(self._impl.info["dims"])
+        self.schedule = self._impl.info["schedule"]
+        self.autotune_times, self.autotune_rejected = {}, {}
+
+    def close(self) -> None:
+        """Stop the native rank process (runtime="process"); a no-op otherwise."""
+        if self.runtime == "process" and self._impl is not None:
+            self._impl.close()
+
     @staticmethod
     def _options(C, decomp, spec, overlap, graph, tiling, temporal=4, tiling2=None, init2=True, tb=True,
                  tiling_tb=None):
@@ -229,6 +265,8 @@ class Solver:
 
         if self.backend == "torch":
             raise ValueError("the torch reference solver has no resume")
+        if self.runtime == "process":
+            raise ValueError("runtime='process' has no resume from Python (use bin/wave3d --resume)")
         if self.transport == "torch":
             to_t = (lambda a: a if isinstance(a, torch.Tensor) else torch.from_numpy(np.asarray(a)))
             self._impl.set_state(to_t(prev), to_t(cur), int(step))
@@ -255,6 +293,8 @@ class Solver:
         decomposition or schedule of a bit-identical solve (the autotune's field check, GpuSolver::field_hash)."""
         if self.backend != "hip" or self.transport == "torch":
             raise ValueError("field_hash needs the native HIP backend")
+        if self.runtime == "process":
+            return self._impl.field_hash(which)
         if isinstance(self._impl, load().GpuGroup):
             return sum(self._impl.field_hash(r, which) for r in range(self._impl.world)) % (1 << 64)
         return int(self._impl.field_hash(which))
@@ -280,6 +320,21 @@ class Solver:
         """This rank's owned nodes of u^K (which=0) or u^{K-1} (which=1) as a CPU (nx, ny, nz) float64 tensor."""
         from .ops.stencil import grid_view
 
+        if self.runtime == "process":  # through a wave3d-dump-v1 file of the rank process (u^K only)
+            import json
+            import tempfile
+
+            import numpy as np
+
+            if which != 0:
+                raise ValueError("runtime='process' downloads u^K (which=0) only")
+            with tempfile.TemporaryDirectory() as d:
+                prefix = os.path.join(d, "f")
+                self._impl.dump(prefix)
+                tag = f".rank{self.rank}" if self.world > 1 else ""
+                meta = json.loads(open(prefix + tag + ".json").read())
+                a = np.fromfile(prefix + tag + ".bin", dtype=np.float64).reshape(meta["shape"])
+            return torch.from_numpy(a)
         if self.transport == "torch":
             return self._impl.owned_field(which)
         if self.backend == "hip":

@@ -18,6 +18,7 @@
 #                                            -> gpurun_out/transports.log
 #   scripts/gpu.sh attrib                    LDS-pass kernel times: production, no checks, 768 threads, experiment builds
 #                                            build/ab/wave3d_noload / _nostore -> gpurun_out/attrib.txt
+#   scripts/gpu.sh sdmatail                  per-solve times of the copy-engine fake ranks + a copy/kernel trace -> sdmatail/
 #   scripts/gpu.sh probe                     tools/probes/sdma_probe (copy engines, memops, capture) -> gpurun_out/probe.log
 #   scripts/gpu.sh all                       test && cli && bench && profbench
 set -o pipefail
@@ -160,6 +161,27 @@ run_transports() {
     done
   done
 }
+# SDMA tail study: per-solve times of the copy-engine fake ranks (--json solve_times_s), then
+# a kernel + memory-copy trace of 12 back-to-back solves of the 512^3 slab rank 1/8 -> gpurun_out/sdmatail/
+run_sdmatail() {
+  local d=gpurun_out/sdmatail fr v tag
+  rm -rf "$d"
+  mkdir -p "$d"
+  for fr in 512:0.001:1/8:slab 512:0.001:3/8:2x2x2; do
+    IFS=: read -r N tau r dec <<< "$fr"
+    for v in "--transport sdma" "--transport sdma --no-overlap" "--no-overlap"; do
+      tag="$(echo "$N-$r-$dec-$v" | tr ' /' '_-')"
+      echo "== N=$N fake $r --decomp $dec $v"
+      timeout -k 5 120 ./bin/wave3d "$N" "$tau" 20 1 --fake-rank "$r" --decomp "$dec" --repeat 20 --warmup 2 --quiet $v \
+        --json "$d/$tag.json" | grep -E "Total time" || return 1
+      python3 -c "import json;t=json.load(open('$d/$tag.json'))['solve_times_s'];print(' '.join('%.2f'%(x*1e3) for x in t))"
+    done
+  done
+  timeout -k 10 180 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$d/trace" -o run -- \
+    ./bin/wave3d 512 0.001 20 1 --fake-rank 1/8 --decomp slab --transport sdma --repeat 10 --warmup 2 --quiet \
+    --json "$d/trace.json" > "$d/trace.log" 2>&1 || return 1
+  python3 tools/trace_overlap.py "$d/trace" --json "$d/trace.json" --solves 12
+}
 run_probe() {
   [ -x build/sdma_probe ] || { echo "build/sdma_probe missing" >&2; return 1; }
   timeout -k 10 120 build/sdma_probe > gpurun_out/probe.log 2>&1
@@ -170,6 +192,7 @@ run_probe() {
 
 case "$what" in
   transports) run_transports > gpurun_out/transports.log 2>&1; rc=$?; cat gpurun_out/transports.log; exit $rc ;;
+  sdmatail) run_sdmatail > gpurun_out/sdmatail.log 2>&1; rc=$?; cat gpurun_out/sdmatail.log; exit $rc ;;
   probe) run_probe ;;
   fakesweep) run_fakesweep ;;
   ab) run_ab "$@" > gpurun_out/ab.log 2>&1; rc=$?; cat gpurun_out/ab.log; exit $rc ;;

@@ -1181,6 +1181,10 @@ RunResult GpuSolver::run() {
       fail("solve schedule failed while being captured: " + thrown);
     }
     if (ok) ok = hipGraphInstantiate(&gx, g, nullptr, nullptr, 0) == hipSuccess;
+    // upload the executable graph now: measured, the first replay of a freshly instantiated copy-engine graph took
+    // 9-11 ms against 1.6-2.2 ms later (one outlier in the first 2-4 solves of every 60-solve run, never after;
+    // profiles/r4/sdma_streams.md) — the "3.6x tail" of round 3 was that outlier inside 7 timed solves after 2 warmups
+    if (ok) ok = hipGraphUpload(gx, s0_) == hipSuccess;
     if (g) (void)hipGraphDestroy(g);
     (void)hipGetLastError();
     if (!ok) {
@@ -1685,7 +1689,7 @@ RunResult GpuGroup::run() {
     if (ok) {
       const hipError_t e = hipGraphInstantiate(&exec_, g, nullptr, nullptr, 0);
       if (dbg) std::fprintf(stderr, "[group] instantiate: %s\n", hipGetErrorString(e));
-      ok = e == hipSuccess;
+      ok = e == hipSuccess && hipGraphUpload(exec_, gs_) == hipSuccess;  // (see GpuSolver::run)
     }
     if (g) (void)hipGraphDestroy(g);
     (void)hipGetLastError();

@@ -114,8 +114,11 @@ void GpuSolver::sdma_alloc() {
     W3D_HIP(hipMemcpy(xvals_, v.data(), v.size() * sizeof(unsigned), hipMemcpyHostToDevice));
   }
   // copy streams (SolverOptions::sdma_streams, env W3D_SDMA_STREAMS; at most one per link): each has its own engine,
-  // and with s0 and s1 at most 4 streams fit the hardware queues a process gets (GPU_MAX_HW_QUEUES)
-  int ns = opt_.sdma_streams > 0 ? opt_.sdma_streams : block_tb_ ? 1 : 2;
+  // and with s0 and s1 at most 4 streams fit the hardware queues a process gets (GPU_MAX_HW_QUEUES). Defaults: slab
+  // ranks one per face; block ranks exchanging after the pass (s0 + 3 copy streams) three — the 512³ 2x2x2 rank 3/8
+  // runs 1.51 / 1.70 ms best / mean of 60 solves with three against 2.14 / 2.29 with one (profiles/r4/sdma_streams.md);
+  // overlapped block ranks one (with two, the graph executor queued the 2048³ core pass behind a copy branch, r3)
+  int ns = opt_.sdma_streams > 0 ? opt_.sdma_streams : block_tb_ ? (opt_.overlap ? 1 : 3) : 2;
   if (const char* v = std::getenv("W3D_SDMA_STREAMS")) ns = std::max(1, std::atoi(v));
   ns = std::min<int>(ns, static_cast<int>(std::max<size_t>(1, xlinks_.size())));
   int lo = 0, hi = 0;

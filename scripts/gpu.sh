@@ -18,6 +18,7 @@
 #                                            -> gpurun_out/transports.log
 #   scripts/gpu.sh attrib                    LDS-pass kernel times: production, no checks, 768 threads, experiment builds
 #                                            build/ab/wave3d_noload / _nostore -> gpurun_out/attrib.txt
+#   scripts/gpu.sh abn BIN...               same-box interleaved A/B/n of any binaries + their kernel stats -> abn.log
 #   scripts/gpu.sh sdmatail                  per-solve times of the copy-engine fake ranks + a copy/kernel trace -> sdmatail/
 #   scripts/gpu.sh probe                     tools/probes/sdma_probe (copy engines, memops, capture) -> gpurun_out/probe.log
 #   scripts/gpu.sh all                       test && cli && bench && profbench
@@ -99,6 +100,32 @@ run_ab() {
       echo "== round $r $b $extra"
       timeout -k 5 120 "$b" 512 0.001 20 1 --repeat 20 --warmup 2 --quiet $extra "$@" | grep -i "time" || return 1
     done
+  done
+}
+
+# same-box A/B/n of the reference-config CLI over any binaries: interleaved rounds of best-of-20 solves, then the
+# rocprofv3 kernel stats of each (leapfrog passes, avg / min us) -> gpurun_out/abn.log
+run_abn() {
+  local r b n
+  for r in 1 2 3; do
+    for b in "$@"; do
+      echo "== round $r $b"
+      timeout -k 5 120 "$b" 512 0.001 20 1 --repeat 20 --warmup 2 --quiet | grep -i "total time" || return 1
+    done
+  done
+  for b in "$@"; do
+    n=$(basename "$b")
+    rm -rf "gpurun_out/abn/$n"
+    timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/abn/$n" -o run -- \
+      "$b" 512 0.001 20 1 --repeat 10 --warmup 2 --quiet > /dev/null 2>&1 || return 1
+    echo "== kernels $n"
+    python3 -c "
+import csv,glob
+for f in glob.glob('gpurun_out/abn/$n/**/run_kernel_stats.csv', recursive=True):
+    for r in csv.DictReader(open(f)):
+        if 'leapfrog' in r['Name']:
+            print(r['Name'].split('(')[0][-60:], r['Calls'], 'avg', round(float(r['AverageNs'])/1e3,1), 'min', round(float(r['MinNs'])/1e3,1))
+"
   done
 }
 
@@ -196,6 +223,7 @@ case "$what" in
   probe) run_probe ;;
   fakesweep) run_fakesweep ;;
   ab) run_ab "$@" > gpurun_out/ab.log 2>&1; rc=$?; cat gpurun_out/ab.log; exit $rc ;;
+  abn) run_abn "$@" > gpurun_out/abn.log 2>&1; rc=$?; cat gpurun_out/abn.log; exit $rc ;;
   test) run_test "$@" ;;
   bench) run_bench "$@" ;;
   cli) run_cli "$@" ;;

@@ -166,6 +166,9 @@ def run_native(a, rank: int, world: int, local: int) -> int:
     log_path = os.path.join(tmp, f"wave3d-bench-{nonce}.rank{rank}.log")
     multi = world > 1
     warm = max(a.warmup, 2 if multi else 1)
+    if a.native_transport == "sdma" or a.autotune_sdma:
+        # copy-engine runs: one 9-12 ms solve among the first 2-7 of every run, never later (profiles/r4/sdma_streams.md)
+        warm = max(warm, 8)
     temporal = 1 if a.no_temporal else a.temporal
     cmd = [CLI, str(a.N), repr(a.tau), str(a.K), repr(a.L), "--quiet", "--json", out_json,
            "--warmup", str(warm - 1), "--repeat", "1", "--bench-steps", str(a.steps),

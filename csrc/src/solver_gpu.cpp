@@ -1181,9 +1181,8 @@ RunResult GpuSolver::run() {
       fail("solve schedule failed while being captured: " + thrown);
     }
     if (ok) ok = hipGraphInstantiate(&gx, g, nullptr, nullptr, 0) == hipSuccess;
-    // upload the executable graph now: measured, the first replay of a freshly instantiated copy-engine graph took
-    // 9-11 ms against 1.6-2.2 ms later (one outlier in the first 2-4 solves of every 60-solve run, never after;
-    // profiles/r4/sdma_streams.md) — the "3.6x tail" of round 3 was that outlier inside 7 timed solves after 2 warmups
+    // (upload now rather than at the first replay; the copy-engine runs still show one 9-12 ms solve among their first
+    // 2-7 — never later — with or without it: profiles/r4/sdma_streams.md. bench.py warms copy-engine runs up longer)
     if (ok) ok = hipGraphUpload(gx, s0_) == hipSuccess;
     if (g) (void)hipGraphDestroy(g);
     (void)hipGetLastError();

@@ -122,8 +122,12 @@ std::vector<std::string> file_allgather(int rank, int world, const std::string& 
           break;
         }
       }
-      if (wall_s() - t0 > 120.0) fail("timed out waiting for " + path(r));  // (a peer that died)
-      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+      const double waited = wall_s() - t0;
+      if (waited > 120.0) fail("timed out waiting for " + path(r));  // (a peer that died)
+      // poll fast first: this is also the per-solve barrier of ranks without a communicator, and a rank leaving it
+      // 20 ms after its peer made the peer's solve wait that long for its flags (solve-time mean 3x the best, measured
+      // on 2 processes sharing one GPU: profiles/r4/proc_parity.md); back off once a peer is clearly slow
+      std::this_thread::sleep_for(waited < 0.25 ? std::chrono::microseconds(50) : std::chrono::microseconds(20000));
     }
   }
   return all;

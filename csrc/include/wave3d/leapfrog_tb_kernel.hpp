@@ -39,6 +39,16 @@ __device__ __forceinline__ void wave_reduce(double& m, double& s) {
   }
 }
 
+// A y/z neighbour read from an LDS plane: one ds_read_b64 each. Plain reads of one base were paired by the compiler
+// into ds_read2_b64 (13 per bulk iteration of the 4-step pass), which gfx950 serves at half the rate of two
+// ds_read_b64 (32 banks x 4 B per cycle instead of 64: MI355X_MICROARCH.md §LDS); a volatile LDS-address-space read is
+// never paired. Measured on one box, interleaved: 4-step pass 995 vs 1029 µs avg, analytic pass 772 vs 796 µs
+// (profiles/r4/lds_read2.md); bit-identical (same operands, same operation order).
+__device__ __forceinline__ double lds_rd(const double* p) {
+  typedef __attribute__((address_space(3))) const volatile double lds_vd;  // (a ds_read, not FLAT)
+  return *(lds_vd*)p;
+}
+
 struct TbParams {
   const double* prev;  // u^{n−1}
   const double* cur;   // u^n
@@ -526,7 +536,8 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         const double f3 = (sx3 * fyq(q)) * fzq(q);   // φ(i+3)
         p3[li] = f3;
         const double c = p2[li];                     // φ(i+2)
-        const double lap = d2sum(c, f1, f3, p2[li - RS], p2[li + RS], p2[li - 1], p2[li + 1]);
+        const double lap =
+            d2sum(c, f1, f3, lds_rd(p2 + li - RS), lds_rd(p2 + li + RS), lds_rd(p2 + li - 1), lds_rd(p2 + li + 1));
         L[0][q][(F + 2) & 3] = ((gof[q] & kLd) && xin) ? first_step(c, lap, p.half_tau2) : 0.0;
         Lm[q][(F + 1) & 1] = f1;
       }
@@ -604,10 +615,12 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         const double c = L[k - 1][q][s0];
         double lap;
         if constexpr (k == 1) {
-          lap = d2sum(c, L[k - 1][q][sm], L[k - 1][q][sp], nb[li - RS], nb[li + RS], nb[li - 1], nb[li + 1]);
+          lap = d2sum(c, L[k - 1][q][sm], L[k - 1][q][sp], lds_rd(nb + li - RS), lds_rd(nb + li + RS),
+                      lds_rd(nb + li - 1), lds_rd(nb + li + 1));
         } else {
           const int lc = tid + q * NT;  // (compact index: the position itself)
-          lap = d2sum(c, L[k - 1][q][sm], L[k - 1][q][sp], nb[lc - H1], nb[lc + H1], nb[lc - 1], nb[lc + 1]);
+          lap = d2sum(c, L[k - 1][q][sm], L[k - 1][q][sp], lds_rd(nb + lc - H1), lds_rd(nb + lc + H1),
+                      lds_rd(nb + lc - 1), lds_rd(nb + lc + 1));
         }
         double o;
         if constexpr (k == 1)

@@ -105,19 +105,22 @@ run_ab() {
 
 # same-box A/B/n of the reference-config CLI over any binaries: interleaved rounds of best-of-20 solves, then the
 # rocprofv3 kernel stats of each (leapfrog passes, avg / min us) -> gpurun_out/abn.log
+# (a spec BIN@ARGS passes ARGS to that binary only, e.g. bin/wave3d@--tb-threads,768 — commas become spaces)
 run_abn() {
-  local r b n
+  local r b n spec extra
   for r in 1 2 3; do
-    for b in "$@"; do
-      echo "== round $r $b"
-      timeout -k 5 120 "$b" 512 0.001 20 1 --repeat 20 --warmup 2 --quiet | grep -i "total time" || return 1
+    for spec in "$@"; do
+      b=${spec%%@*}; extra=""; [ "$spec" != "$b" ] && extra=${spec#*@}; extra=${extra//,/ }
+      echo "== round $r $b $extra"
+      timeout -k 5 120 "$b" 512 0.001 20 1 --repeat 20 --warmup 2 --quiet $extra | grep -i "total time" || return 1
     done
   done
-  for b in "$@"; do
-    n=$(basename "$b")
+  for spec in "$@"; do
+    b=${spec%%@*}; extra=""; [ "$spec" != "$b" ] && extra=${spec#*@}; extra=${extra//,/ }
+    n=$(basename "$b")$(echo "$extra" | tr -d ' -')
     rm -rf "gpurun_out/abn/$n"
     timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/abn/$n" -o run -- \
-      "$b" 512 0.001 20 1 --repeat 10 --warmup 2 --quiet > /dev/null 2>&1 || return 1
+      "$b" 512 0.001 20 1 --repeat 10 --warmup 2 --quiet $extra > /dev/null 2>&1 || return 1
     echo "== kernels $n"
     python3 -c "
 import csv,glob
@@ -125,6 +128,12 @@ for f in glob.glob('gpurun_out/abn/$n/**/run_kernel_stats.csv', recursive=True):
     for r in csv.DictReader(open(f)):
         if 'leapfrog' in r['Name']:
             print(r['Name'].split('(')[0][-60:], r['Calls'], 'avg', round(float(r['AverageNs'])/1e3,1), 'min', round(float(r['MinNs'])/1e3,1))
+for f in glob.glob('gpurun_out/abn/$n/**/run_kernel_trace.csv', recursive=True):
+    seen=set()
+    for r in csv.DictReader(open(f)):
+        k=r['Kernel_Name'].split('(')[0][-50:]
+        if 'leapfrog' in k and k not in seen:
+            seen.add(k); print('  regs', k, 'vgpr', r['VGPR_Count'], 'agpr', r.get('Accum_VGPR_Count'), 'sgpr', r['SGPR_Count'], 'scratch', r['Scratch_Size'], 'lds', r['LDS_Block_Size'])
 "
   done
 }

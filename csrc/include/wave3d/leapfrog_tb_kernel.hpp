@@ -429,7 +429,9 @@ __global__ __launch_bounds__(tb_block_threads<NT>) void k_leapfrog_tb(const TbPa
     (void)lds_plane;
     auto lds_cplane = [&](int k, int par) { return lds + 2 * PLP + ((k - 1) * 2 + par) * G::PLC + G::COFF; };
     // (store wave) u^{n+S} staging slot par: compact like the stage planes
-    auto lds_splane = [&](int par) { return lds + 2 * PLP + ((S - 1) * 2 + par) * G::PLC + G::COFF; };
+    auto lds_splane = [&](int par) {
+      return lds + 2 * PLP + ((S - 1) * 2 + par) * G::PLC + (INIT ? 2 * PLP : 0) + G::COFF;
+    };
     (void)lds_splane;
     if constexpr (SWV) {
       if (storer) {

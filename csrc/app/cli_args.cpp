@@ -51,7 +51,7 @@ constexpr Personality kPersonalities[] = {
                "  --no-tb            two-step register-queue passes instead of the LDS S-step kernel\n"
                "  --tb-min-planes M  slab ranks: LDS S-step passes with S-deep halos from M owned planes (default 16)\n"
                "  --deep-min-planes M  slab ranks without the LDS kernel: two-step passes from M planes (default 96)\n"
-               "  --tb-threads T     LDS S-step kernel workgroup size (768, 1024, or 960 = 15 compute waves + a store wave)\n"
+               "  --tb-threads T     LDS S-step kernel workgroup size (768 or 1024; default 1024)\n"
                "  --tb-init-threads T  ... of the analytic-start pass (768 or 1024; default 768)\n"
                "  --no-init2         start from u0,u1 + a first step instead of analytic u1,u2\n"
                "  --debug-sync       synchronize after every step (race triage)\n"

@@ -78,7 +78,7 @@ void launch_leapfrog2(const Layout& l, const Coeffs& c, const double* prev, cons
 constexpr int kTbTile = 32;  // (y, z) tile edge of the LDS S-step passes (leapfrog_tb_kernel.hpp tbk::kTile)
 struct LeapfrogTbTiling {
   int stages = 4;         // 2, 3 or 4 steps per pass
-  int threads = 1024;     // workgroup size (768 or 1024; 960 = 15 compute waves + a store wave, plain 4-step passes)
+  int threads = 1024;     // workgroup size (768 or 1024)
   int init_threads = 768; // ... of the analytic-start pass (measured at 512³, S = 3: 768 → 932 µs, 1024 → 1027 µs;
                           // the S = 4 passes go the other way: 768 → 1123 µs, 1024 → 1076 µs)
   bool xcd_remap = true;  // (stores are always non-temporal: measured faster at every S)

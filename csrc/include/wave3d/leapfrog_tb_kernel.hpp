@@ -149,17 +149,6 @@ __device__ __forceinline__ void tb_push_signal(const TbPush& q) {
 // planes fit: the analytic start at S ≤ 3 (its four ring-layout slots: 133 KiB at S = 3, with room for the 2048³ x
 // sin table). The 4-step pass keeps W0: on a whole 2048³ box its x sin table would not fit next to the wider planes,
 // and where it fits (512³) the wider layout moved a register to scratch inside the march and was measured slower.
-// Store-wave variant (NT = 960): 15 compute waves own the positions as usual and a 16th wave (threads 960..1023)
-// writes the pass's two output levels to HBM from LDS — u^{n+S−1} from its compact stage plane, u^{n+S} from a staging
-// plane the compute waves fill instead of storing — one iteration behind, as whole tile rows (64 lanes = two 32-node
-// rows per store). On gfx950 loads and stores share one in-order vector-memory counter, so a compute wave's wait for
-// its next plane's loads also waited for its own earlier stores to be acknowledged; the compute waves now issue loads
-// only. The store wave joins every barrier.
-template <int NT>
-constexpr bool tb_store_wave = NT == 960;
-template <int NT>
-constexpr int tb_block_threads = tb_store_wave<NT> ? NT + 64 : NT;
-
 template <int S, int T, int NT, bool RP = false>
 struct TbGeom {
   static constexpr int H1 = T + 2 * (S - 1);  // stage-1 region edge: the thread-owned positions
@@ -184,10 +173,7 @@ struct TbGeom {
   static constexpr int COFF = H1 + 1;
   static constexpr int PLC = COFF + NPR + H1 + 1;
   // level 0 × 2 parity slots, levels 1..S−1 × 2 compact slots; the analytic start adds a φ level (two W0-layout slots)
-  // (+ the store-wave variant's u^{n+S} staging: two compact slots after the other planes)
-  static constexpr int lds_planes(bool init) {
-    return 2 * PLP + (S - 1) * 2 * PLC + (init ? 2 * PLP : 0) + (tb_store_wave<NT> ? 2 * PLC : 0);
-  }
+  static constexpr int lds_planes(bool init) { return 2 * PLP + (S - 1) * 2 * PLC + (init ? 2 * PLP : 0); }
   // + (fac: checked passes that load u^n) the check's (s_z, row index) pair of every position, compact and thread-
   // private: position idx = tid + q·NT at pair idx, read at an immediate offset from the thread's own base address
   static constexpr int lds_doubles(bool init = false, bool fac = false) { return lds_planes(init) + (fac ? 2 * NP : 0); }
@@ -218,7 +204,7 @@ constexpr int tb_nx_table(int nx_box) {
 // CH: x-chunked launch (small boxes). Without it the block's x range is the kernel argument itself, which the compiler
 // re-reads instead of keeping live (measured: a computed range costs the S = 4 kernel 5 % in extra spills).
 template <int S, int T, int NT, int CM, bool INIT, bool CH, bool PUSH>
-__global__ __launch_bounds__(tb_block_threads<NT>) void k_leapfrog_tb(const TbParams p) {
+__global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
   using G = TbGeom<S, T, NT, tb_row_pad<INIT, S>>;
   constexpr int Q = G::Q, QR = G::QR, H1 = G::H1, W0 = G::W0, RS = G::RS, PLP = G::PLP;
   constexpr int kOwn = 1 << 30;   // gof flag: tile node inside the output box
@@ -232,9 +218,6 @@ __global__ __launch_bounds__(tb_block_threads<NT>) void k_leapfrog_tb(const TbPa
   constexpr bool kFac = CM != 0 && !INIT;
   extern __shared__ double lds[];
   const int tid = static_cast<int>(threadIdx.x);
-  constexpr bool SWV = tb_store_wave<NT>;
-  static_assert(!SWV || (!INIT && !PUSH && S >= 2), "store wave: plain passes only");
-  const bool storer = SWV && tid >= NT;  // (the store wave)
   int blk = static_cast<int>(blockIdx.x);
   if (p.xcd_remap) {  // XCD k (= blockIdx % 8 in dispatch order) takes the k-th contiguous range of xper blocks
     const int j = blk >> 3;
@@ -382,7 +365,7 @@ __global__ __launch_bounds__(tb_block_threads<NT>) void k_leapfrog_tb(const TbPa
       if (p.check_mask) {  // (each thread writes and later reads only its own pairs: no barrier)
 #pragma unroll
         for (int q = 0; q < Q; ++q)
-          if (tid + q * NT < G::NP && !storer)
+          if (tid + q * NT < G::NP)
             fac[tid + q * NT] = make_double2(szw[ztab(lid[q])], __longlong_as_double(ytab(lid[q])));
       }
     }
@@ -428,49 +411,6 @@ __global__ __launch_bounds__(tb_block_threads<NT>) void k_leapfrog_tb(const TbPa
     auto lds_plane = [&](int j, int par) { return lds + par * PLP; };  // (level 0 only)
     (void)lds_plane;
     auto lds_cplane = [&](int k, int par) { return lds + 2 * PLP + ((k - 1) * 2 + par) * G::PLC + G::COFF; };
-    // (store wave) u^{n+S} staging slot par: compact like the stage planes
-    auto lds_splane = [&](int par) {
-      return lds + 2 * PLP + ((S - 1) * 2 + par) * G::PLC + (INIT ? 2 * PLP : 0) + G::COFF;
-    };
-    (void)lds_splane;
-    if constexpr (SWV) {
-      if (storer) {
-        // lane l stores tile rows r0 + 2m (m = 0..15, r0 = l / 32) at column c = l % 32: one store instruction per two
-        // 32-node rows (four whole 128-B lines); bit m of `own` = that node is an output node of this rank (the
-        // compute waves' kOwn test: inside the output box, the global interior, the allocation and the real range)
-        const int l = tid - NT, c = l & 31, r0 = l >> 5;
-        const int z = tz0 + c;
-        int own = 0;
-#pragma unroll
-        for (int m = 0; m < T / 2; ++m) {
-          const int y = ty0 + r0 + 2 * m;
-          const bool ok = y < p.y1 && z < p.z1 && inside(p.gy0 + y) && inside(p.gz0 + z) && in_rng(y, p.ay0, p.ay1) &&
-                          in_rng(z, p.az0, p.az1) && in_rng(y, p.sy0, p.sy1) && in_rng(z, p.sz0, p.sz1);
-          own |= ok ? 1 << m : 0;
-        }
-        const int goff0 = (ty0 + r0 + ya) * R + z + za;         // + 2m rows
-        const int lidx0 = (r0 + S - 1) * H1 + (c + S - 1);      // compact index, + 2m rows
-        auto store_plane = [&](const double* src, double* outp) {
-#pragma unroll
-          for (int m = 0; m < T / 2; ++m)
-            if ((own >> m) & 1) __builtin_nontemporal_store(src[lidx0 + 2 * m * H1], outp + goff0 + 2 * m * R);
-        };
-        // the stage S−1 and S planes the compute waves finished in iteration i − 1 (written before this barrier)
-        auto flush = [&](int i) {
-          const int x3 = i - 1 - (S - 2), x4 = i - 1 - (S - 1);
-          auto out_plane = [&](int x) { return x >= x0 && x < x1 && x >= p.sx0 && x < p.sx1 && inside(p.gx0 + x); };
-          if (out_plane(x3)) store_plane(lds_cplane(S - 1, (x3 - i0) & 1), p.out1 + static_cast<i64>(x3 + 1) * P);
-          if (out_plane(x4)) store_plane(lds_splane((x4 - i0) & 1), p.out2 + static_cast<i64>(x4 + 1) * P);
-        };
-        for (int i = i0; i <= i1; ++i) {
-          __syncthreads();  // (the compute waves' barrier of iteration i)
-          flush(i);
-        }
-        __syncthreads();  // (their closing barrier)
-        flush(i1 + 1);
-        continue;  // (one segment: no push)
-      }
-    }
 
     // plane x of u^n: owned positions into L[0][q][slot], ring into Rg[r][rs]
     const int wbase_r = __builtin_amdgcn_readfirstlane(tid & ~63);
@@ -694,9 +634,7 @@ __global__ __launch_bounds__(tb_block_threads<NT>) void k_leapfrog_tb(const TbPa
           dst[tid + q * NT] = v;
         }
         const bool own = xown && (g & kOwn);
-        if constexpr (SWV && k == S) {
-          lds_splane(D & 1)[tid + q * NT] = v;  // (the store wave writes it; u^{n+S−1} is in its stage plane)
-        } else if constexpr (k >= S - 1 && !SWV) {
+        if constexpr (k >= S - 1) {
           if (own && xreal) {
 #if defined(W3D_EXPERIMENT_PLAINSTORE)  // (experiment: write-back stores instead of non-temporal ones)
             outp[g & kOff] = v;
@@ -832,7 +770,6 @@ __global__ __launch_bounds__(tb_block_threads<NT>) void k_leapfrog_tb(const TbPa
         iteration(std::integral_constant<int, 3>{}, Gen{}, ib + 3);
       }
     }
-    if constexpr (SWV) __syncthreads();  // the last iteration's stage S−1 / S planes → the store wave
     }  // segments
   }
   if constexpr (PUSH) tb_push_signal(*p.push);
@@ -845,7 +782,7 @@ __global__ __launch_bounds__(tb_block_threads<NT>) void k_leapfrog_tb(const TbPa
     double m = emax[k], sm = esum[k];
     wave_reduce(m, sm);
     __syncthreads();
-    if ((tid & 63) == 0 && tid < NT) {  // (the store wave holds no partials)
+    if ((tid & 63) == 0) {
       red_m[tid >> 6] = m;
       red_s[tid >> 6] = sm;
     }
@@ -870,9 +807,8 @@ struct TbPlan {
 // takes the default (x: the compute box; y, z: the whole allocation, i.e. no restriction besides the global interior).
 inline TbPlan make_plan_tb(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, LBox real) {
   W3D_REQUIRE(t.stages >= 2 && t.stages <= 4, "leapfrog_tb: stages must be 2, 3 or 4");
-  W3D_REQUIRE((t.threads == 768 || t.threads == 960 || t.threads == 1024) &&
-                  (t.init_threads == 768 || t.init_threads == 1024),
-              "leapfrog_tb: threads must be 768, 960 (+ the store wave) or 1024");
+  W3D_REQUIRE((t.threads == 768 || t.threads == 1024) && (t.init_threads == 768 || t.init_threads == 1024),
+              "leapfrog_tb: threads must be 768 or 1024");
   const LBox full = compute_box(l);
   if (real.x0 > real.x1) {
     real.x0 = full.x0;
@@ -1008,13 +944,11 @@ void launch_cfg(const TbParams& p, int nblocks, hipStream_t st) {
   if (p.nxc > 1) {
     const size_t lim = prepare_cfg<S, NT, CM, INIT, true, PUSH>();
     W3D_REQUIRE(shmem <= lim, "leapfrog_tb: too many planes for the LDS sin table");
-    hipLaunchKernelGGL((k_leapfrog_tb<S, kTile, NT, CM, INIT, true, PUSH>), dim3(nblocks), dim3(tb_block_threads<NT>),
-                       shmem, st, p);
+    hipLaunchKernelGGL((k_leapfrog_tb<S, kTile, NT, CM, INIT, true, PUSH>), dim3(nblocks), dim3(NT), shmem, st, p);
   } else {
     const size_t lim = prepare_cfg<S, NT, CM, INIT, false, PUSH>();
     W3D_REQUIRE(shmem <= lim, "leapfrog_tb: too many planes for the LDS sin table");
-    hipLaunchKernelGGL((k_leapfrog_tb<S, kTile, NT, CM, INIT, false, PUSH>), dim3(nblocks), dim3(tb_block_threads<NT>),
-                       shmem, st, p);
+    hipLaunchKernelGGL((k_leapfrog_tb<S, kTile, NT, CM, INIT, false, PUSH>), dim3(nblocks), dim3(NT), shmem, st, p);
   }
 }
 
@@ -1039,26 +973,11 @@ void launch_nt(const TbParams& p, int nblocks, hipStream_t st) {
     launch_cfg<S, NT, kFull<S>, INIT, PUSH>(p, nblocks, st);
 }
 
-// the store-wave 4-step pass needs its u^{n+S} staging next to everything else in LDS (at 512³ 157 of 160 KiB); a
-// longer x sin table (bigger boxes) falls back to 1024 threads
-inline bool store_wave_fits(const TbParams& p) {
-  constexpr int CMF = kFull<4>;
-  const size_t need = tb_lds_bytes<4, kTile, 960, false, true>(p.check_mask ? tb_nx_table<4>(p.xlen) : 0) + sizeof(TbPack);
-  return need <= prepare_cfg<4, 960, CMF, false, false, false>();
-}
-
 // workgroup size per pass kind: LeapfrogTbTiling::threads, or init_threads for the analytic-start pass
 template <int S, bool PUSH>
 void launch_s(const TbParams& p, int nblocks, const LeapfrogTbTiling& t, bool init, hipStream_t st) {
   // 768 threads: 12 waves (3 per SIMD, 168 VGPRs each) for the 38² = 1444 stage-1 positions of an S = 4 tile, two sets
   // per thread with 6 % idle slots; 1024: 16 waves (128 VGPRs), 30 % of the second set idle
-  if constexpr (S == 4 && !PUSH) {
-    // the store-wave variant (tb_store_wave): plain 4-step passes whose LDS (staging + x sin table) fits
-    if (!init && t.threads == 960 && p.pk == nullptr && store_wave_fits(p)) {
-      launch_nt<S, 960, false, false>(p, nblocks, st);
-      return;
-    }
-  }
   if ((init ? t.init_threads : t.threads) == 768)
     init ? launch_nt<S, 768, true, PUSH>(p, nblocks, st) : launch_nt<S, 768, false, PUSH>(p, nblocks, st);
   else

@@ -64,7 +64,6 @@ void leapfrog_tb_prepare(bool push) {
   prepare_nt<2, 1024, true>();
   prepare_nt<3, 1024, true>();
   prepare_nt<4, 1024, true>();
-  prepare_nt<4, 960, false>();  // (the store-wave variant)
 }
 
 size_t leapfrog_tb_lds_bytes(int stages) {

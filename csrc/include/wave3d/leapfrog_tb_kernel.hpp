@@ -441,7 +441,8 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         for (int r = 0; r < QR; ++r)
           if (wbase_r + r * NT < G::NR) Rg[r][rs] = u1_at(x, lrid[r], grof[r] & kLd);
       } else {
-        const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;  // always an allocated plane
+        // always an allocated plane (bulk iterations load planes inside the allocation by construction: no clamp)
+        const int xs = decltype(bkc)::value ? x : x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
         const gdouble* base = plane_ptr(bkc, p.cur, 6, xs);
 #pragma unroll
         for (int q = 0; q < Q; ++q)
@@ -457,7 +458,7 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         for (int q = 0; q < Q; ++q)
           if (wsm[q]) Lm[q][slot] = phi_at(x, lid[q]);
       } else {
-        const int xs = x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
+        const int xs = decltype(bkc)::value ? x : x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
         const gdouble* base = plane_ptr(bkc, p.prev, 4, xs);
 #pragma unroll
         for (int q = 0; q < Q; ++q)
@@ -628,7 +629,14 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         else
           o = L[k - 2][q][s0];
         const int g = gof[q];
+#ifdef W3D_EXPERIMENT_SELV
+        // (experiment: the update computed for every lane and selected, no exec-masked branch around it)
+        double lf = leapfrog(c, o, lap, tau2);
+        asm volatile("" : "+v"(lf));
+        const double v = (xreal && (gof[q] & kReal)) ? lf : 0.0;
+#else
         const double v = (xreal && (gof[q] & kReal)) ? leapfrog(c, o, lap, tau2) : 0.0;
+#endif
         if constexpr (k < S) {
           L[k][q][s0] = v;
           dst[tid + q * NT] = v;

@@ -629,14 +629,18 @@ __global__ __launch_bounds__(NT) void k_leapfrog_tb(const TbParams p) {
         else
           o = L[k - 2][q][s0];
         const int g = gof[q];
-#ifdef W3D_EXPERIMENT_SELV
-        // (experiment: the update computed for every lane and selected, no exec-masked branch around it)
-        double lf = leapfrog(c, o, lap, tau2);
-        asm volatile("" : "+v"(lf));
-        const double v = (xreal && (gof[q] & kReal)) ? lf : 0.0;
-#else
-        const double v = (xreal && (gof[q] & kReal)) ? leapfrog(c, o, lap, tau2) : 0.0;
-#endif
+        // analytic-start pass: the update is computed for every lane and selected (the opaque register keeps the
+        // compiler from wrapping it, and the neighbour reads feeding it, in an exec-masked branch): 712 vs 740 µs,
+        // s_waitcnt per iteration 76 -> 55. The 4-step pass keeps the branch (1091 vs 1058 µs with the select;
+        // profiles/r4/lds_read2.md)
+        double v;
+        if constexpr (INIT) {
+          double lf = leapfrog(c, o, lap, tau2);
+          asm volatile("" : "+v"(lf));
+          v = (xreal && (gof[q] & kReal)) ? lf : 0.0;
+        } else {
+          v = (xreal && (gof[q] & kReal)) ? leapfrog(c, o, lap, tau2) : 0.0;
+        }
         if constexpr (k < S) {
           L[k][q][s0] = v;
           dst[tid + q * NT] = v;

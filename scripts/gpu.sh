@@ -181,6 +181,21 @@ run_fakesweep() {
       done
     done
   done
+  # (round 4) the same ranks WITH their copy-engine traffic, mean of 20 solves after 8 warmups ("sdma" schedules: a
+  # second, pessimistic curve — one GPU's engines carry what a node's links would)
+  local v tag
+  for P in 2 4 8; do
+    for spec in "slab:--transport sdma:slab-sdma" "slab:--transport sdma --no-overlap:slab-sdma-seq" \
+                "block:--transport sdma --no-overlap:block-sdma-seq"; do
+      IFS=: read -r dec v tag <<< "$spec"
+      [ "$dec" = block ] && [ "$P" -lt 4 ] && continue
+      for r in 0 1; do
+        timeout -k 5 120 ./bin/wave3d 512 0.001 20 1 --fake-rank "$r/$P" --decomp "$dec" $v --repeat 20 \
+          --warmup 8 --quiet --json /tmp/fs.json > /dev/null || return 1
+        python3 -c "import json,sys;d=json.load(open('/tmp/fs.json'));print(json.dumps({'P':$P,'decomp':'x'.join(map(str,d['dims'])),'schedule':'$tag','rank':$r,'solve_s':d['mean_s'],'best_s':d['solve_s']}))" >> "$out" || return 1
+      done
+    done
+  done
   cat "$out"
 }
 

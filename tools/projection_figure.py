@@ -8,7 +8,10 @@ Input: the JSON lines of ``scripts/gpu.sh fakesweep`` — the 1-GPU solve, and o
 A point's time is the max over the sampled ranks; each P keeps its fastest schedule.
 
 This prices the compute side of a multi-GPU solve only: the halo traffic over xGMI (and the overlap that hides part of
-it) is not in it, so the numbers are an upper bound on what an 8-GPU node can reach, not a measurement of one. The
+it) is not in it, so the numbers are an upper bound on what an 8-GPU node can reach, not a measurement of one.
+Schedules whose name contains "sdma" (round 4) are fake ranks WITH their copy-engine traffic (mean of the timed
+solves): every message of the rank goes through this one GPU's SDMA engines, where a node gives each neighbour link
+its own — a pessimistic bracket. They form a second curve and never enter the compute-only one. The
 measured curve comes from the driver's SCALE records (tools/scaling_report.py). The panels mirror the reference's
 speedup / efficiency figure (readme.md:102-108, iamge1.png).
 """
@@ -34,13 +37,18 @@ def load(path):
     return pts
 
 
-def table(pts):
-    t1 = min(pts[1].values())
+def table(pts, traffic: bool = False):
+    """Fastest schedule per P among the compute-only ones (traffic=False) or the copy-engine ones (True; P = 1 is the
+    one-GPU solve either way)."""
+    t1 = min(v for k, v in pts[1].items() if "sdma" not in k)
     rows = []
     for P in sorted(pts):
-        sched, t = min(pts[P].items(), key=lambda kv: kv[1])
+        cand = {k: v for k, v in pts[P].items() if P == 1 or (("sdma" in k) == traffic)}
+        if not cand:
+            continue
+        sched, t = min(cand.items(), key=lambda kv: kv[1])
         rows.append({"P": P, "schedule": sched, "t": t, "gcell": CELLS / t / 1e9, "speedup": t1 / t,
-                     "eff": t1 / t / P, "all": dict(sorted(pts[P].items()))})
+                     "eff": t1 / t / P, "all": dict(sorted(cand.items()))})
     return rows
 
 
@@ -49,15 +57,21 @@ def main(argv=None) -> int:
     ap.add_argument("path")
     ap.add_argument("--plot", default="")
     a = ap.parse_args(argv)
-    rows = table(load(a.path))
-    print("| GPUs | fastest schedule | per-rank compute ms | GCell/s (compute only) | speedup | efficiency | "
-          "schedules (ms) | P100 reference |")
-    print("|---|---|---|---|---|---|---|---|")
-    for r in rows:
-        alls = ", ".join(f"{k} {v * 1e3:.3f}" for k, v in r["all"].items())
-        ref = f"{REF_S[r['P']]} s" if r["P"] in REF_S else "—"
-        print(f"| {r['P']} | {r['schedule']} | {r['t'] * 1e3:.3f} | {r['gcell']:.0f} | {r['speedup']:.2f} | "
-              f"{r['eff']:.2f} | {alls} | {ref} |")
+    pts = load(a.path)
+    rows = table(pts)
+    trows = table(pts, traffic=True)
+    trows = trows if len(trows) > 1 else []
+    for title, rr in (("compute only", rows), ("with copy-engine traffic on one GPU's engines", trows)):
+        if not rr:
+            continue
+        print(f"\n{title}\n")
+        print("| GPUs | fastest schedule | per-rank ms | GCell/s | speedup | efficiency | schedules (ms) | P100 reference |")
+        print("|---|---|---|---|---|---|---|---|")
+        for r in rr:
+            alls = ", ".join(f"{k} {v * 1e3:.3f}" for k, v in r["all"].items())
+            ref = f"{REF_S[r['P']]} s" if r["P"] in REF_S else "—"
+            print(f"| {r['P']} | {r['schedule']} | {r['t'] * 1e3:.3f} | {r['gcell']:.0f} | {r['speedup']:.2f} | "
+                  f"{r['eff']:.2f} | {alls} | {ref} |")
     if a.plot:
         import matplotlib
 
@@ -67,13 +81,18 @@ def main(argv=None) -> int:
         ps = [r["P"] for r in rows]
         fig, (a1, a2) = plt.subplots(1, 2, figsize=(11, 4.2))
         a1.plot(ps, [r["speedup"] for r in rows], "o-", label="MI355X, per-rank compute (fake rank, no traffic)")
+        if trows:
+            a1.plot([r["P"] for r in trows], [r["speedup"] for r in trows], "^-",
+                    label="MI355X, fake rank + its copy-engine traffic (one GPU's engines)")
         a1.plot([1, ps[-1]], [1, ps[-1]], ":", color="gray", label="ideal")
         a1.plot(list(REF_S), [REF_S[1] / REF_S[p] for p in REF_S], "s--", label="P100 reference (readme.md:99-100)")
         a1.set_xlabel("GPUs")
         a1.set_ylabel("speedup vs 1 GPU")
-        a1.set_title("512³ K=20 fp64: compute-only projection")
+        a1.set_title("512³ K=20 fp64: one-GPU projection")
         a1.legend(fontsize=8)
         a2.plot(ps, [r["eff"] for r in rows], "o-", label="MI355X, per-rank compute")
+        if trows:
+            a2.plot([r["P"] for r in trows], [r["eff"] for r in trows], "^-", label="MI355X, + copy-engine traffic")
         a2.plot(list(REF_S), [REF_S[1] / REF_S[p] / p for p in REF_S], "s--", label="P100 reference")
         a2.set_xlabel("GPUs")
         a2.set_ylabel("efficiency")

@@ -2,6 +2,8 @@
 // reference's output lines, the JSON helpers of the summary, and the CPU programs' runners.
 #pragma once
 
+#include <functional>
+#include <istream>
 #include <string>
 #include <vector>
 
@@ -60,6 +62,14 @@ struct Args {
 
 // argv → Args (positional N tau K [L], long options; argv[0] picks the reference program's personality)
 Args parse(int argc, char** argv);
+
+// --serve: print `greeting` (one JSON line), then answer one command per stdin line with one JSON line on stdout —
+// handle(cmd, rest of the line) returns the reply; "quit" ends the loop (exit 0), an unknown command or a thrown error
+// is reported as {"error": ...} (a thrown error also ends the loop, exit 1: the rank's state may be inconsistent).
+// The Python side is mpi_cuda_amd/parallel/native_proc.py.
+int serve_loop(const std::string& greeting, const std::function<std::string(const std::string&, std::istream&)>& handle);
+std::string jexact(double v);  // every digit (%.17g): logs and byte counts compared exactly on the Python side
+std::string steps_exact(const std::vector<int>& st, const std::vector<double>& mx, const std::vector<double>& rms);
 [[noreturn]] void usage(const char* msg = nullptr);
 // the reference's per-step line (report.pdf p.15-16 §4.3): "Step %d, t = %f, Max Error = %e, L2 Error = %e"
 void print_errors(const std::vector<int>& steps, const std::vector<double>& mx, const std::vector<double>& rms,

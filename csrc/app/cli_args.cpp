@@ -3,6 +3,8 @@
 #include <cctype>
 #include <cstdio>
 #include <cstdlib>
+#include <iostream>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -221,6 +223,46 @@ std::string steps_json(const std::vector<int>& st, const std::vector<double>& mx
   for (size_t i = 0; i < st.size(); ++i)
     o += (i ? ", [" : "[") + std::to_string(st[i]) + ", " + jnum(mx[i]) + ", " + jnum(rms[i]) + "]";
   return o + "]";
+}
+
+std::string jexact(double v) {
+  char b[40];
+  std::snprintf(b, sizeof b, "%.17g", v);
+  return b;
+}
+std::string steps_exact(const std::vector<int>& st, const std::vector<double>& mx, const std::vector<double>& rms) {
+  std::string o = "[";
+  for (size_t i = 0; i < st.size(); ++i)
+    o += (i ? ", [" : "[") + std::to_string(st[i]) + ", " + jexact(mx[i]) + ", " + jexact(rms[i]) + "]";
+  return o + "]";
+}
+
+int serve_loop(const std::string& greeting,
+               const std::function<std::string(const std::string&, std::istream&)>& handle) {
+  auto reply = [](const std::string& line) {
+    std::fputs(line.c_str(), stdout);
+    std::fputc('\n', stdout);
+    std::fflush(stdout);
+  };
+  reply(greeting);
+  std::string line;
+  while (std::getline(std::cin, line)) {
+    std::istringstream in(line);
+    std::string cmd;
+    in >> cmd;
+    if (cmd.empty()) continue;
+    if (cmd == "quit") {
+      reply("{\"bye\": true}");
+      return 0;
+    }
+    try {
+      reply(handle(cmd, in));
+    } catch (const std::exception& e) {
+      reply("{\"error\": " + jstr(json_escape(e.what())) + "}");
+      return 1;  // (a failed collective leaves the peers to their own timeouts: this rank is gone)
+    }
+  }
+  return 0;  // (stdin closed: the parent is gone)
 }
 
 SolverOptions options_from(const Args& a, bool fake) {

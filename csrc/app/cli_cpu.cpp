@@ -18,6 +18,25 @@ int run_cpu(const Args& a) {
     const int n0 = load_checkpoint(a.resume, a.prob, prev, cur);
     s.set_state(prev.data(), cur.data(), n0);
   }
+  if (a.serve) {  // (the rank-process protocol on the CPU solver: run / dump / quit — cli.hpp serve_loop)
+    const std::string greeting = "{\"ready\": true, \"backend\": \"cpu\", \"rank\": 0, \"world\": 1, \"dims\": [1, 1, 1], "
+                                 "\"schedule\": \"cpu-openmp\", \"mode\": \"cpu\", \"transport\": \"none\"}";
+    return serve_loop(greeting, [&](const std::string& cmd, std::istream& in) -> std::string {
+      if (cmd == "run") {
+        const CpuResult r = s.run();
+        return "{\"solve_s\": " + jexact(r.solve_s) + ", \"local_s\": " + jexact(r.solve_s) +
+               ", \"graph\": false, \"overlap\": false, \"finite\": " + (r.finite ? "true" : "false") +
+               ", \"steps\": " + steps_exact(r.steps, r.max_err, r.rms_err) + "}";
+      }
+      if (cmd == "dump") {
+        std::string prefix;
+        in >> prefix;
+        write_dump(prefix, a.prob, s.layout(), s.field(0), 0, 1, Dims{1, 1, 1});
+        return "{\"dump\": " + jstr(prefix) + "}";
+      }
+      return "{\"error\": " + jstr("unknown command: " + cmd) + "}";
+    });
+  }
   CpuResult r;
   double best = 1e30, sum = 0;
   for (int i = 0; i < a.warmup + a.repeat; ++i) {

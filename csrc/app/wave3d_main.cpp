@@ -60,77 +60,49 @@ void combine_logs(RunResult& r, const HostColl& hc) {
   }
 }
 
-// --serve: the rank's solver stays up and takes one command per stdin line, answering each with one JSON line on
-// stdout — the native rank process behind the Python Solver(runtime="process") (mpi_cuda_amd/parallel/native_proc.py):
-// a torch process cannot capture the multi-rank schedules (HIP 7.0 runtime, see multistream_capture_safe), this
-// process's ROCm 7.2 runtime can. Every rank must receive the same command sequence (run and quit are collective).
+// --serve (GPU): the rank's solver stays up and answers one command per stdin line (cli.hpp serve_loop) — the native
+// rank process behind the Python Solver(runtime="process") (mpi_cuda_amd/parallel/native_proc.py): a torch process
+// cannot capture the multi-rank schedules (HIP 7.0 runtime, see multistream_capture_safe), this process's ROCm 7.2
+// runtime can. Every rank must receive the same command sequence (run and quit are collective).
 //   run            one solve (barrier first): {"solve_s" (max over ranks), "local_s", "graph", "finite", "steps"}
 //   hash W         field_hash of u^K (W = 0) / u^{K−1} (W = 1) over this rank's owned nodes
 //   traffic        GpuSolver::traffic of the last solve's schedule
 //   dump PREFIX    write u^K of this rank (wave3d-dump-v1)
 //   quit           leave the loop (exit status 0)
 int serve(const Args& a, GpuSolver& s, const HostColl& hc, bool file_coll, const std::string& sched) {
-  auto jx = [](double v) {  // (every digit: the Python side compares logs and byte counts exactly)
-    char b[40];
-    std::snprintf(b, sizeof b, "%.17g", v);
-    return std::string(b);
-  };
-  auto reply = [](const std::string& line) {
-    std::fputs(line.c_str(), stdout);
-    std::fputc('\n', stdout);
-    std::fflush(stdout);
-  };
   const Dims d = s.dims();
-  {
+  std::ostringstream g;
+  g << "{\"ready\": true, \"backend\": \"hip\", \"rank\": " << s.rank() << ", \"world\": " << s.world()
+    << ", \"dims\": [" << d.px << ", " << d.py << ", " << d.pz << "], \"schedule\": " << jstr(sched)
+    << ", \"mode\": " << jstr(s.mode()) << ", \"transport\": " << jstr(s.transport()) << "}";
+  return serve_loop(g.str(), [&](const std::string& cmd, std::istream& in) -> std::string {
     std::ostringstream o;
-    o << "{\"ready\": true, \"rank\": " << s.rank() << ", \"world\": " << s.world() << ", \"dims\": [" << d.px
-      << ", " << d.py << ", " << d.pz << "], \"schedule\": " << jstr(sched) << ", \"mode\": " << jstr(s.mode())
-      << ", \"transport\": " << jstr(s.transport()) << "}";
-    reply(o.str());
-  }
-  std::string line;
-  while (std::getline(std::cin, line)) {
-    std::istringstream in(line);
-    std::string cmd;
-    in >> cmd;
-    std::ostringstream o;
-    try {
-      if (cmd == "run") {
-        hc.barrier();
-        RunResult r = s.run();
-        const double t = hc.max(r.solve_s);
-        if (file_coll) combine_logs(r, hc);
-        o << "{\"solve_s\": " << jx(t) << ", \"local_s\": " << jx(r.solve_s) << ", \"graph\": "
-          << (s.options().graph ? "true" : "false") << ", \"overlap\": " << (s.overlapped() ? "true" : "false")
-          << ", \"finite\": " << (r.finite ? "true" : "false") << ", \"steps\": [";
-        for (size_t i = 0; i < r.steps.size(); ++i)
-          o << (i ? ", " : "") << "[" << r.steps[i] << ", " << jx(r.max_err[i]) << ", " << jx(r.rms_err[i]) << "]";
-        o << "]}";
-      } else if (cmd == "hash") {
-        int w = 0;
-        in >> w;
-        o << "{\"hash\": \"" << std::to_string(s.field_hash(w)) << "\"}";
-      } else if (cmd == "traffic") {
-        const GpuSolver::Traffic tr = s.traffic();
-        o << "{\"field_bytes\": " << jx(tr.field_bytes) << ", \"halo_bytes\": " << jx(tr.halo_bytes) << "}";
-      } else if (cmd == "dump") {
-        std::string prefix;
-        in >> prefix;
-        write_dump(prefix, a.prob, s.layout(), s.download(0), s.rank(), s.world(), d);
-        o << "{\"dump\": " << jstr(prefix) << "}";
-      } else if (cmd == "quit") {
-        reply("{\"bye\": true}");
-        return 0;
-      } else {
-        o << "{\"error\": " << jstr("unknown command: " + cmd) << "}";
-      }
-    } catch (const std::exception& e) {
-      reply("{\"error\": " + jstr(json_escape(e.what())) + "}");
-      return 1;  // (a failed collective leaves the peers to their own timeouts: this rank is gone)
+    if (cmd == "run") {
+      hc.barrier();
+      RunResult r = s.run();
+      const double t = hc.max(r.solve_s);
+      if (file_coll) combine_logs(r, hc);
+      o << "{\"solve_s\": " << jexact(t) << ", \"local_s\": " << jexact(r.solve_s) << ", \"graph\": "
+        << (s.options().graph ? "true" : "false") << ", \"overlap\": " << (s.overlapped() ? "true" : "false")
+        << ", \"finite\": " << (r.finite ? "true" : "false") << ", \"steps\": " << steps_exact(r.steps, r.max_err, r.rms_err)
+        << "}";
+    } else if (cmd == "hash") {
+      int w = 0;
+      in >> w;
+      o << "{\"hash\": \"" << std::to_string(s.field_hash(w)) << "\"}";
+    } else if (cmd == "traffic") {
+      const GpuSolver::Traffic tr = s.traffic();
+      o << "{\"field_bytes\": " << jexact(tr.field_bytes) << ", \"halo_bytes\": " << jexact(tr.halo_bytes) << "}";
+    } else if (cmd == "dump") {
+      std::string prefix;
+      in >> prefix;
+      write_dump(prefix, a.prob, s.layout(), s.download(0), s.rank(), s.world(), d);
+      o << "{\"dump\": " << jstr(prefix) << "}";
+    } else {
+      o << "{\"error\": " << jstr("unknown command: " + cmd) << "}";
     }
-    reply(o.str());
-  }
-  return 0;  // (stdin closed: the parent is gone)
+    return o.str();
+  });
 }
 
 int run_group(const Args& a, const SolverOptions& o, const hipDeviceProp_t& prop) {

@@ -6,7 +6,7 @@ A torch process cannot graph-capture the multi-rank schedules: the HIP 7.0 runti
 system ROCm 7.2 runtime and captures them (one graph per solve, or per parity for the copy-engine transport). This
 module therefore runs each rank's solver in a ``bin/wave3d --serve`` child — the same runtime ``bench.py`` starts per
 rank — and talks to it one JSON line per command (``run``, ``hash W``, ``traffic``, ``dump P``, ``quit``; protocol in
-``csrc/app/wave3d_main.cpp`` ``serve``). The solver, its buffers, communicator and captured graphs stay up between
+``csrc/app/cli.hpp`` ``serve_loop``, handlers in ``wave3d_main.cpp`` ``serve`` and ``cli_cpu.cpp``). The solver, its buffers, communicator and captured graphs stay up between
 ``run()`` calls, so repeated solves time the replayed graph exactly as the CLI does.
 
 Rendezvous: rank 0 draws a nonce, broadcast over the torch.distributed group (gloo or RCCL), which names the file the
@@ -101,8 +101,12 @@ class NativeRankProcess:
                                    f"{self._stderr_tail()}")
 
     def command(self, line: str) -> dict:
-        self._p.stdin.write(line + "\n")
-        self._p.stdin.flush()
+        try:
+            self._p.stdin.write(line + "\n")
+            self._p.stdin.flush()
+        except (BrokenPipeError, OSError):
+            rc = self._p.wait()
+            raise RuntimeError(f"native rank process {self.rank} exited (rc={rc}):\n{self._stderr_tail()}") from None
         return self._read()
 
     def run(self) -> dict:
@@ -132,6 +136,11 @@ class NativeRankProcess:
             except Exception:
                 self._p.kill()
                 self._p.wait()
+        for f in (self._p.stdin, self._p.stdout):
+            try:
+                f.close()
+            except Exception:
+                pass
         self._log.close()
         if os.path.exists(self._log.name):
             os.remove(self._log.name)

@@ -199,3 +199,40 @@ def test_cli_cpu_checkpoint_resume_bitexact(tmp_path):
     assert steps(resumed) == [l for l in steps(direct) if int(l.split()[1].rstrip(",")) > 10]
     meta = json.loads((tmp_path / "c10.prev.json").read_text())
     assert meta["step"] == 9 and json.loads((tmp_path / "c10.cur.json").read_text())["step"] == 10
+
+
+def test_native_rank_process_protocol_cpu(tmp_path):
+    """The rank-process protocol behind Solver(runtime="process") (bin/wave3d --serve, parallel/native_proc.py), on
+    the CPU solver: greeting, repeated solves with the exact log, dump, error replies, clean quit, and a child that
+    dies mid-session turning into a Python error instead of a hang."""
+    from mpi_cuda_amd import ProblemSpec
+    from mpi_cuda_amd.parallel.native_proc import NativeRankProcess
+    from mpi_cuda_amd.solver import Solver
+    from mpi_cuda_amd.utils.dump import load
+
+    spec = ProblemSpec(N=32, tau=1e-3, K=10, check_every=1)
+    ref = Solver(spec, backend="cpu")
+    r = ref.run()
+    p = NativeRankProcess(spec, 0, 1, 0, extra_args=("--cpu", "--threads", "2"), timeout_s=60)
+    try:
+        assert p.info["ready"] and p.info["backend"] == "cpu" and p.info["dims"] == [1, 1, 1]
+        for _ in range(2):
+            a = p.run()
+            assert a["steps"] == r.steps and a["max_err"] == r.max_err and a["rms_err"] == r.rms_err
+            assert a["finite"] is True and a["graph"] is False and a["solve_s"] > 0
+        prefix = str(tmp_path / "d")
+        p.dump(prefix)
+        field, meta = load(prefix)
+        assert np.array_equal(field, ref.owned_field(0).numpy())
+        with pytest.raises(RuntimeError, match="unknown command"):
+            p.command("bogus")
+        assert p.run()["max_err"] == r.max_err  # (still serving after an error reply)
+    finally:
+        p.close()
+    assert p._p.returncode == 0
+    q = NativeRankProcess(spec, 0, 1, 0, extra_args=("--cpu",), timeout_s=60)
+    q._p.kill()
+    q._p.wait()
+    with pytest.raises(RuntimeError, match="exited"):
+        q.run()
+    q.close()

@@ -1,5 +1,7 @@
 // wave3d CLI: command line, reference program personalities, output helpers. See cli.hpp; reference CLI: report.pdf
 // p.12-15 §4.2, p.20-26 §5.
+#include <fcntl.h>
+#include <unistd.h>
 #include <cctype>
 #include <cstdio>
 #include <cstdlib>
@@ -239,30 +241,53 @@ std::string steps_exact(const std::vector<int>& st, const std::vector<double>& m
 
 int serve_loop(const std::string& greeting,
                const std::function<std::string(const std::string&, std::istream&)>& handle) {
-  auto reply = [](const std::string& line) {
-    std::fputs(line.c_str(), stdout);
-    std::fputc('\n', stdout);
-    std::fflush(stdout);
+  // Private descriptors for the protocol: the commands keep arriving on what was fd 0 and the replies leave on what
+  // was fd 1, while fd 0 becomes /dev/null and fd 1 the stderr stream. Measured: a process with RCCL communicators lost
+  // the commands queued in its stdin during a graph capture (rccl-self group), and RCCL prints its banner to stdout.
+  std::fflush(stdout);
+  const int in_fd = dup(0), out_fd = dup(1);
+  W3D_REQUIRE(in_fd >= 0 && out_fd >= 0, "serve: cannot duplicate stdin / stdout");
+  const int nul = open("/dev/null", O_RDONLY);
+  if (nul >= 0) {
+    dup2(nul, 0);
+    close(nul);
+  }
+  dup2(2, 1);
+  FILE* cmd_in = fdopen(in_fd, "r");
+  FILE* rep_out = fdopen(out_fd, "w");
+  W3D_REQUIRE(cmd_in && rep_out, "serve: cannot open the protocol streams");
+  auto reply = [&](const std::string& line) {
+    std::fputs(line.c_str(), rep_out);
+    std::fputc('\n', rep_out);
+    std::fflush(rep_out);
   };
   reply(greeting);
-  std::string line;
-  while (std::getline(std::cin, line)) {
-    std::istringstream in(line);
+  char* buf = nullptr;
+  size_t cap = 0;
+  int rc = 0;
+  for (;;) {
+    const ssize_t n = getline(&buf, &cap, cmd_in);
+    if (n < 0) break;  // (stdin closed: the parent is gone)
+    std::istringstream in(std::string(buf, static_cast<size_t>(n)));
     std::string cmd;
     in >> cmd;
     if (cmd.empty()) continue;
     if (cmd == "quit") {
       reply("{\"bye\": true}");
-      return 0;
+      break;
     }
     try {
       reply(handle(cmd, in));
     } catch (const std::exception& e) {
       reply("{\"error\": " + jstr(json_escape(e.what())) + "}");
-      return 1;  // (a failed collective leaves the peers to their own timeouts: this rank is gone)
+      rc = 1;  // (a failed collective leaves the peers to their own timeouts: this rank is gone)
+      break;
     }
   }
-  return 0;  // (stdin closed: the parent is gone)
+  std::free(buf);
+  std::fclose(cmd_in);
+  std::fclose(rep_out);
+  return rc;
 }
 
 SolverOptions options_from(const Args& a, bool fake) {

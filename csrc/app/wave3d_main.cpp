@@ -112,6 +112,47 @@ int run_group(const Args& a, const SolverOptions& o, const hipDeviceProp_t& prop
     const int n0 = load_checkpoint(a.resume, a.prob, prev, cur);
     g.set_state(prev.data(), cur.data(), n0);
   }
+  if (a.serve) {
+    // --group P --serve: all P ranks in this process (the Python Solver(world=P, runtime="process") of ONE Python
+    // process); run / hash (summed over the ranks) / traffic (summed) / dump (one file per rank) / quit
+    const Dims d0 = g.rank(0).dims();
+    std::ostringstream gr;
+    gr << "{\"ready\": true, \"backend\": \"hip\", \"rank\": 0, \"world\": " << g.world() << ", \"dims\": [" << d0.px
+       << ", " << d0.py << ", " << d0.pz << "], \"schedule\": " << jstr(g.rank(0).mode()) << ", \"mode\": "
+       << jstr(g.rank(0).mode()) << ", \"transport\": " << jstr(g.transport()) << "}";
+    return serve_loop(gr.str(), [&](const std::string& cmd, std::istream& in) -> std::string {
+      std::ostringstream out;
+      if (cmd == "run") {
+        const RunResult r = g.run();
+        out << "{\"solve_s\": " << jexact(r.solve_s) << ", \"local_s\": " << jexact(r.solve_s) << ", \"graph\": "
+            << (g.graph_enabled() ? "true" : "false") << ", \"overlap\": false, \"finite\": "
+            << (r.finite ? "true" : "false") << ", \"steps\": " << steps_exact(r.steps, r.max_err, r.rms_err) << "}";
+      } else if (cmd == "hash") {
+        int w = 0;
+        in >> w;
+        unsigned long long h = 0;
+        for (int q = 0; q < g.world(); ++q) h += g.rank(q).field_hash(w);
+        out << "{\"hash\": \"" << std::to_string(h) << "\"}";
+      } else if (cmd == "traffic") {
+        double fb = 0, hb = 0;
+        for (int q = 0; q < g.world(); ++q) {
+          const GpuSolver::Traffic t = g.rank(q).traffic();
+          fb += t.field_bytes;
+          hb += t.halo_bytes;
+        }
+        out << "{\"field_bytes\": " << jexact(fb) << ", \"halo_bytes\": " << jexact(hb) << "}";
+      } else if (cmd == "dump") {
+        std::string prefix;
+        in >> prefix;
+        for (int q = 0; q < g.world(); ++q)
+          write_dump(prefix, a.prob, g.rank(q).layout(), g.rank(q).download(0), q, g.world(), d0);
+        out << "{\"dump\": " << jstr(prefix) << "}";
+      } else {
+        out << "{\"error\": " << jstr("unknown command: " + cmd) << "}";
+      }
+      return out.str();
+    });
+  }
   RunResult r;
   double best = 1e30, sum = 0;
   for (int i = 0; i < a.warmup + a.repeat; ++i) {

@@ -35,12 +35,15 @@ class NativeRankProcess:
 
     def __init__(self, spec, rank: int, world: int, device: int, transport: str = "rccl", decomp: str = "slab",
                  temporal: int = 4, overlap: bool = True, graph: bool = True, rccl: bool = True,
-                 autotune: bool = False, group=None, timeout_s: float = 300.0, nonce: str | None = None,
+                 autotune: bool = False, group=None, timeout_s: float | None = None, nonce: str | None = None,
                  extra_args: tuple = ()):
         if transport not in _TRANSPORT_FLAGS:
             raise ValueError(f"runtime='process' runs transports {sorted(_TRANSPORT_FLAGS)}, not {transport!r}")
         if not os.path.exists(CLI):
             raise RuntimeError(f"native runtime {CLI} is missing (python tools/build.py)")
+        # bound of every reply (the greeting includes the solver's setup): W3D_PROC_TIMEOUT_S, default 300 s
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("W3D_PROC_TIMEOUT_S", "300"))
         self.rank, self.world, self.timeout_s = rank, world, timeout_s
         if nonce is None:
             nonce = uuid.uuid4().hex
@@ -69,6 +72,9 @@ class NativeRankProcess:
                                                 delete=False)
         self._p = subprocess.Popen(cmd, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=self._log,
                                    text=True, bufsize=1)
+        # replies are split into lines here, from raw reads: a buffered readline() after select() could leave the
+        # greeting in Python's buffer behind a library's banner lines and then wait on an empty pipe
+        self._buf = b""
         self.info = self._read()
         if not self.info.get("ready"):
             raise RuntimeError(f"native rank process {rank}: unexpected greeting {self.info}")
@@ -78,27 +84,40 @@ class NativeRankProcess:
         with open(self._log.name) as f:
             return f.read()[-2000:]
 
+    def _line(self, deadline: float) -> bytes | None:
+        """Next complete stdout line (without its newline), or None when none has arrived by ``deadline``."""
+        fd = self._p.stdout.fileno()
+        while b"\n" not in self._buf:
+            left = deadline - time.monotonic()
+            if left <= 0:
+                return None
+            ready, _, _ = select.select([fd], [], [], min(left, 1.0))
+            if ready:
+                chunk = os.read(fd, 1 << 16)
+                if not chunk:
+                    rc = self._p.wait()
+                    raise RuntimeError(f"native rank process {self.rank} exited (rc={rc}):\n{self._stderr_tail()}")
+                self._buf += chunk
+            elif self._p.poll() is not None:
+                raise RuntimeError(f"native rank process {self.rank} exited (rc={self._p.returncode}):\n"
+                                   f"{self._stderr_tail()}")
+        line, self._buf = self._buf.split(b"\n", 1)
+        return line
+
     def _read(self) -> dict:
         deadline = time.monotonic() + self.timeout_s
         while True:
-            left = deadline - time.monotonic()
-            if left <= 0:
+            line = self._line(deadline)
+            if line is None:
                 self._p.kill()
                 raise TimeoutError(f"native rank process {self.rank}: no reply in {self.timeout_s:.0f} s\n"
                                    f"{self._stderr_tail()}")
-            ready, _, _ = select.select([self._p.stdout], [], [], min(left, 1.0))
-            if ready:
-                line = self._p.stdout.readline()
-                if not line:
-                    rc = self._p.wait()
-                    raise RuntimeError(f"native rank process {self.rank} exited (rc={rc}):\n{self._stderr_tail()}")
-                msg = json.loads(line)
-                if "error" in msg:
-                    raise RuntimeError(f"native rank process {self.rank}: {msg['error']}")
-                return msg
-            if self._p.poll() is not None:
-                raise RuntimeError(f"native rank process {self.rank} exited (rc={self._p.returncode}):\n"
-                                   f"{self._stderr_tail()}")
+            if not line.lstrip().startswith(b"{"):
+                continue  # (a library's own stdout line, e.g. RCCL's banner: not a reply)
+            msg = json.loads(line)
+            if "error" in msg:
+                raise RuntimeError(f"native rank process {self.rank}: {msg['error']}")
+            return msg
 
     def command(self, line: str) -> dict:
         try:

@@ -197,20 +197,61 @@ class Solver:
         """runtime="process": this rank's production solver in a ``bin/wave3d --serve`` child (graph-captured under
         the system ROCm runtime, which a torch process cannot do for multi-rank schedules; parallel/native_proc.py).
         Transports: rccl, sdma / sdma-ipc (copy engines), push / push-ipc; one process per rank (torchrun)."""
+        import torch.distributed as dist
+
         from .parallel.native_proc import NativeRankProcess
 
         if self.backend != "hip":
             raise ValueError("runtime='process' runs the native HIP backend")
-        self.transport = {"sdma": "sdma-ipc", "push": "push-ipc"}.get(self.transport, self.transport)
         if device is None:
             device = self.rank % max(1, torch.cuda.device_count())  # (device_count does not initialise the GPU)
         self.device = torch.device("cuda", device)
         self.comm = None
-        self._impl = NativeRankProcess(self.spec, self.rank, self.world, device, self.transport, decomp, temporal,
-                                       overlap, graph, rccl, autotune, group)
+        # one Python process driving all ranks (no torch.distributed job): the whole in-process group lives in ONE
+        # rank process (bin/wave3d --group P --group-transport T --serve), graph-captured under its ROCm 7.2 runtime
+        self._group_proc = self.world > 1 and not dist.is_initialized() and self.transport in (
+            "loopback", "rccl-self", "push", "sdma", "multi-device")
+        if self._group_proc:
+            if autotune:
+                raise ValueError("runtime='process' with an in-process group has no autotune")
+            self._impl = NativeRankProcess(self.spec, 0, 1, device, "rccl", decomp, temporal, overlap, graph, True,
+                                           False, None, extra_args=("--group", str(self.world), "--group-transport",
+                                                                    self.transport))
+        else:
+            self.transport = {"sdma": "sdma-ipc", "push": "push-ipc"}.get(self.transport, self.transport)
+            self._impl = NativeRankProcess(self.spec, self.rank, self.world, device, self.transport, decomp,
+                                           temporal, overlap, graph, rccl, autotune, group)
         self.dims = tuple(self._impl.info["dims"])
         self.schedule = self._impl.info["schedule"]
         self.autotune_times, self.autotune_rejected = {}, {}
+
+    def _process_fields(self, which: int, assemble: bool) -> torch.Tensor:
+        """runtime="process": u^K through the rank process's wave3d-dump-v1 files — this rank's owned nodes, or (assemble)
+        the global (N+1)³ field from every rank of an in-process group / of a single rank."""
+        import json
+        import tempfile
+
+        import numpy as np
+
+        if which != 0:
+            raise ValueError("runtime='process' downloads u^K (which=0) only")
+        if assemble and self.world > 1 and not self._group_proc:
+            raise RuntimeError("global_field of a process-per-rank job: gather the ranks' owned_field instead")
+        with tempfile.TemporaryDirectory() as d:
+            prefix = os.path.join(d, "f")
+            self._impl.dump(prefix)
+            ranks = range(self.world) if (assemble or self._group_proc) else [self.rank]
+            n = self.spec.N + 1
+            out = np.zeros((n, n, n)) if assemble else None
+            for r in ranks:
+                tag = f".rank{r}" if self.world > 1 else ""
+                meta = json.loads(open(prefix + tag + ".json").read())
+                a = np.fromfile(prefix + tag + ".bin", dtype=np.float64).reshape(meta["shape"])
+                if not assemble:
+                    return torch.from_numpy(a)
+                x0, y0, z0 = meta["offset"]
+                out[x0:x0 + a.shape[0], y0:y0 + a.shape[1], z0:z0 + a.shape[2]] = a
+        return torch.from_numpy(out)
 
     def close(self) -> None:
         """Stop the native rank process (runtime="process"); a no-op otherwise."""
@@ -303,6 +344,8 @@ class Solver:
         """The whole (N+1)³ field u^K (which=0) / u^{K-1} (which=1) on the CPU (single rank or loopback group)."""
         from .ops.stencil import grid_view
 
+        if self.runtime == "process":  # the rank process dumps u^K (all its ranks for a group): assemble the dumps
+            return self._process_fields(which, assemble=True)
         if self.transport not in ("loopback", "rccl-self", "push", "sdma", "multi-device"):
             if self.world != 1:
                 raise RuntimeError("global_field needs world == 1 or the loopback transport")
@@ -321,20 +364,7 @@ class Solver:
         from .ops.stencil import grid_view
 
         if self.runtime == "process":  # through a wave3d-dump-v1 file of the rank process (u^K only)
-            import json
-            import tempfile
-
-            import numpy as np
-
-            if which != 0:
-                raise ValueError("runtime='process' downloads u^K (which=0) only")
-            with tempfile.TemporaryDirectory() as d:
-                prefix = os.path.join(d, "f")
-                self._impl.dump(prefix)
-                tag = f".rank{self.rank}" if self.world > 1 else ""
-                meta = json.loads(open(prefix + tag + ".json").read())
-                a = np.fromfile(prefix + tag + ".bin", dtype=np.float64).reshape(meta["shape"])
-            return torch.from_numpy(a)
+            return self._process_fields(which, assemble=False)
         if self.transport == "torch":
             return self._impl.owned_field(which)
         if self.backend == "hip":

@@ -236,3 +236,35 @@ def test_native_rank_process_protocol_cpu(tmp_path):
     with pytest.raises(RuntimeError, match="exited"):
         q.run()
     q.close()
+
+
+def test_native_rank_process_banner_in_one_chunk(tmp_path, monkeypatch):
+    """A library banner written to the child's stdout in the same pipe chunk as the greeting (RCCL prints one while an
+    rccl-self group initialises, before the serve loop takes stdout over): the client skips the banner lines and
+    still finds the greeting and every reply, and a silent child times out instead of hanging."""
+    from mpi_cuda_amd import ProblemSpec
+    from mpi_cuda_amd.parallel import native_proc
+
+    fake = tmp_path / "wave3d"
+    fake.write_text("#!/bin/sh\n"
+                    "printf 'RCCL version : x\\nHIP version : y\\n{\"ready\": true, \"dims\": [2, 1, 1]}\\n'\n"
+                    "while read l; do case \"$l\" in\n"
+                    "  run) printf 'noise\\n{\"steps\": [[2, 0.5, 0.25]], \"solve_s\": 0.1}\\n';;\n"
+                    "  hang) sleep 30;;\n"
+                    "  quit) echo '{\"bye\": true}'; exit 0;;\n"
+                    "esac; done\n")
+    fake.chmod(0o755)
+    monkeypatch.setattr(native_proc, "CLI", str(fake))
+    spec = ProblemSpec(N=16, tau=1e-3, K=2)
+    p = native_proc.NativeRankProcess(spec, 0, 1, 0, timeout_s=5)
+    try:
+        assert p.info == {"ready": True, "dims": [2, 1, 1]}
+        r = p.run()
+        assert r["steps"] == [2] and r["max_err"] == [0.5] and r["rms_err"] == [0.25]
+    finally:
+        p.close()
+    assert p._p.returncode == 0
+    q = native_proc.NativeRankProcess(spec, 0, 1, 0, timeout_s=1)
+    with pytest.raises(TimeoutError, match="no reply"):
+        q.command("hang")
+    q.close()

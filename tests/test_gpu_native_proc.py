@@ -20,6 +20,12 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+@pytest.fixture(autouse=True)
+def _short_replies(monkeypatch):
+    # (a rank process that stops answering fails the test in a minute instead of hanging the suite)
+    monkeypatch.setenv("W3D_PROC_TIMEOUT_S", "60")
+
+
 def test_process_runtime_one_rank_matches_inproc(gpu):
     spec = ProblemSpec(N=96, tau=1e-3, K=20)
     ref = Solver(spec, backend="hip", device=0)
@@ -88,3 +94,31 @@ def test_process_runtime_two_ranks_sdma_graph(gpu, tmp_path):
             assert me == pytest.approx(r1.max_err, rel=1e-12) and re_ == pytest.approx(r1.rms_err, rel=1e-9)
         hashes += m["hash"]
     assert hashes % (1 << 64) == ref.field_hash(0)
+
+
+@pytest.mark.parametrize("transport,decomp,graph", [("rccl-self", "slab", True), ("loopback", "2x2x1", True),
+                                                   ("sdma", "slab", False), ("sdma", "2x2x1", False)])
+def test_process_runtime_group_graph(gpu, transport, decomp, graph):
+    """Solver(..., world=P) from ONE Python process with runtime="process": the whole in-process group runs in one
+    native rank process (bin/wave3d --group P --serve). Its ROCm 7.2 runtime captures the RCCL (rccl-self) and
+    loopback groups, which the torch process's runtime cannot (graph=True); copy-engine groups enqueue eagerly by design
+    (one rank's flag waits are released by other ranks' streams, GpuGroup), their graph-captured form being one process
+    per rank (test_process_runtime_two_ranks_sdma_graph). Every solve: the single-GPU log and field bit for bit."""
+    spec = ProblemSpec(N=96, tau=1e-3, K=20)
+    ref = Solver(spec, backend="hip", device=0)
+    r1 = ref.run()
+    world = 4 if decomp == "2x2x1" else 2
+    s = Solver(spec, backend="hip", transport=transport, world=world, rank=0, decomp=decomp, device=0,
+               runtime="process")
+    try:
+        assert s.transport == transport and s.dims[0] == 2
+        for _ in range(3):
+            r = s.run()
+            assert r.extra["graph"] is graph
+            assert r.steps == r1.steps and r.max_err == r1.max_err
+            for a, b in zip(r.rms_err, r1.rms_err):
+                assert a == pytest.approx(b, rel=1e-12)
+        assert torch.equal(s.global_field(0), ref.global_field(0))
+        assert s.field_hash(0) == ref.field_hash(0)
+    finally:
+        s.close()

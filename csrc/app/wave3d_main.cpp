@@ -307,10 +307,22 @@ int run_gpu(const Args& a) {
     W3D_HIP(hipDeviceSynchronize());
     hc.barrier();
     const double t0 = wall_s();
-    for (int i = 0; i < a.bench_steps; ++i) r = s->run();
+    const RunResult warm = r;
+    // (W3D_BENCH_SYNC_EACH=1: one host round trip per solve, as before run_batch — A/B runs)
+    std::vector<RunResult> rs;
+    if (std::getenv("W3D_BENCH_SYNC_EACH"))
+      for (int i = 0; i < a.bench_steps; ++i) rs.push_back(s->run());
+    else
+      rs = s->run_batch(a.bench_steps);
     W3D_HIP(hipDeviceSynchronize());
     hc.barrier();
     bench_s = hc.max(wall_s() - t0);
+    // every timed solve's own log equals the warmup solve's (exact; a fake rank's ghosts are never filled: skipped)
+    for (size_t i = 0; i < rs.size() && a.fake_rank < 0; ++i)
+      if (rs[i].max_err != warm.max_err || rs[i].rms_err != warm.rms_err || !rs[i].finite)
+        fail("bench: timed solve " + std::to_string(i) + " of rank " + std::to_string(rank) +
+             " produced a different error log than the warmup solve");
+    r = rs.back();
   }
   // per-phase breakdown of the schedule that was timed: one more solve with the same kernels, traced with events
   PhaseTimes ph;

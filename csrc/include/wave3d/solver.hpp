@@ -151,6 +151,13 @@ class GpuSolver {
 
   // One full solve: u⁰, u¹ → K−1 leapfrog steps with error checks → global error log on the host.
   RunResult run();
+  // n solves back to back (bench.py's timed block): a one-rank solver with a captured graph enqueues all n replays,
+  // each followed by the copy of its own error log into its slot of a pinned host buffer, and synchronises once at
+  // the end; the CLI then checks every timed solve's log against the warmup solve's. Every solve runs in full. (The
+  // host round trip it removes between solves measured within noise of 0 at 512³: profiles/r4/vmcnt/README.md.)
+  // Other solvers (several ranks, copy engines, push, timers, resume, no graph) call run() n times. solve_s of each
+  // result = the batch's wall time / n.
+  std::vector<RunResult> run_batch(int n);
   // Per-phase event timers for the following run() calls (those launch eagerly; the captured graph is kept for when
   // the timers are switched off again): a phase breakdown of exactly the schedule the graph replays.
   void set_timers(bool on) { opt_.timers = on; }
@@ -226,6 +233,7 @@ class GpuSolver {
   void pack_halo(hipStream_t st);   // faces (single steps) / S-deep regions (block passes) → send_buf_
   void unpack_halo(hipStream_t st); // recv_buf_ → ghost layers
   void gather_errors(RunResult& r);
+  void decode_log(const Partial* host, int nsrc, RunResult& r) const;  // per-rank partials → r's log (rank order)
   // Schedule: a solve is phase_init() followed by units; a unit advances one step (in place over u^{n−1}) or 2..4
   // (a fused pass into the two free buffers). Multi-rank units run shell -> exchange -> interior.
   enum class Mode { kSingleStep, kFusedSingle, kDeep, kDeepTb };
@@ -310,6 +318,8 @@ class GpuSolver {
   int n_partials_ = 0;
   Partial* errlog_ = nullptr;    // [K+1]
   Partial* errall_ = nullptr;    // [world][K+1]
+  Partial* hbatch_ = nullptr;    // pinned [batch][K+1] (run_batch)
+  int hbatch_n_ = 0;
   std::vector<double> ct_;       // cos(a_t n τ)
   hipStream_t s0_ = nullptr, s1_ = nullptr;
   bool own_s0_ = true;  // false: a GpuGroup "push" rank on the group's shared compute stream

@@ -519,6 +519,20 @@ PYBIND11_MODULE(_C, m) {
              }
              return result_dict(r);
            })
+      .def("run_batch",
+           [](GpuSolver& s, int n) {
+             std::vector<RunResult> rs;
+             {
+               py::gil_scoped_release nogil;
+               rs = s.run_batch(n);
+             }
+             py::list out;
+             for (const RunResult& r : rs) out.append(result_dict(r));
+             return out;
+           },
+           py::arg("n"),
+           "n solves back to back; a one-rank graph-captured solver enqueues them all and synchronises once (each "
+           "solve's own log copied out)")
       .def("download",
            [](const GpuSolver& s, int which) {
              auto v = s.download(which);

@@ -432,6 +432,7 @@ GpuSolver::~GpuSolver() {
     }
   if (stg_) (void)hipFree(stg_);
   if (push_host_) (void)hipHostFree(push_host_);
+  if (hbatch_) (void)hipHostFree(hbatch_);
   if (push_dev_) (void)hipFree(push_dev_);
   if (flags_) (void)hipFree(flags_);
   if (s0_ && own_s0_) (void)hipStreamDestroy(s0_);
@@ -1128,7 +1129,11 @@ void GpuSolver::gather_errors(RunResult& r) {
   });
   wait_stream(s0_, comm_.get(), gpu_timeout_s());
   push_check();
-  const int nsrc = static_cast<int>(host.size() / per);
+  decode_log(host.data(), static_cast<int>(host.size() / per), r);
+}
+
+void GpuSolver::decode_log(const Partial* host, int nsrc, RunResult& r) const {
+  const size_t per = static_cast<size_t>(prob_.K + 1);
   // copy-engine transport: a flag wait that timed out marked word 0 of that rank's log (step 0 is never checked)
   for (int q = 0; q < nsrc && sdma_; ++q)
     W3D_REQUIRE(host[static_cast<size_t>(q) * per].x == 0.0,
@@ -1202,6 +1207,44 @@ RunResult GpuSolver::run() {
   collect_phases(r);
   ++runs_;
   return r;
+}
+
+std::vector<RunResult> GpuSolver::run_batch(int n) {
+  std::vector<RunResult> out;
+  if (n <= 0) return out;
+  const bool pipelined = world_ == 1 && !sdma_ && !push_ && opt_.graph && graph_exec_ && !opt_.timers &&
+                         resume_n_ == 0;
+  if (!pipelined) {
+    for (int i = 0; i < n; ++i) out.push_back(run());
+    return out;
+  }
+  const size_t per = static_cast<size_t>(prob_.K + 1);
+  if (hbatch_n_ < n) {
+    if (hbatch_) W3D_HIP(hipHostFree(hbatch_));
+    hbatch_ = nullptr;
+    W3D_HIP(hipHostMalloc(reinterpret_cast<void**>(&hbatch_), static_cast<size_t>(n) * per * sizeof(Partial),
+                          hipHostMallocDefault));
+    hbatch_n_ = n;
+  }
+  cur_unit_ = -1;
+  const double t0 = now_s();
+  for (int i = 0; i < n; ++i) {
+    W3D_HIP(hipGraphLaunch(graph_exec_, s0_));
+    // (stream order: this solve's log is copied out before the next replay's init overwrites it)
+    W3D_HIP(hipMemcpyAsync(hbatch_ + static_cast<size_t>(i) * per, errlog_, per * sizeof(Partial),
+                           hipMemcpyDeviceToHost, s0_));
+  }
+  wait_stream(s0_, nullptr, gpu_timeout_s());
+  const double dt = (now_s() - t0) / n;
+  xsolves_ += static_cast<unsigned>(n);
+  runs_ += n;
+  for (int i = 0; i < n; ++i) {
+    RunResult r;
+    decode_log(hbatch_ + static_cast<size_t>(i) * per, 1, r);
+    r.solve_s = dt;
+    out.push_back(std::move(r));
+  }
+  return out;
 }
 
 // ------------------------------------------------------------------------------------------------------------------

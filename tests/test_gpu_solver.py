@@ -131,3 +131,20 @@ def test_traffic_accounting(gpu):
     t = s.traffic()
     assert t["field_bytes"] == (2 + 4 * 4) * 63 ** 3 * 8
     assert t["halo_bytes"] == 0
+
+
+def test_run_batch_pipelined_logs(gpu):
+    """GpuSolver::run_batch (bench.py's timed block): n graph replays enqueued back to back, each solve's log copied
+    into its own pinned slot, one sync — every solve returns the same log as a synchronised run(), and the field after
+    the batch is the single run()'s field bit for bit (also for a batch larger than the previous pinned buffer)."""
+    spec = ProblemSpec(N=96, tau=1e-3, K=20)
+    s = Solver(spec, backend="hip", device=0)
+    r1 = s.run()  # (captures the graph)
+    h1 = s.field_hash(0)
+    for n in (3, 7):
+        rs = s._impl.run_batch(n)
+        assert len(rs) == n
+        for r in rs:
+            assert list(r["steps"]) == r1.steps and list(r["max_err"]) == r1.max_err
+            assert list(r["rms_err"]) == r1.rms_err and r["solve_s"] > 0
+        assert s.field_hash(0) == h1

@@ -297,6 +297,18 @@ class Solver:
                            {k: v for k, v in r.items() if k not in ("steps", "max_err", "rms_err", "solve_s",
                                                                     "finite")})
 
+    def run_batch(self, n: int) -> list:
+        """n solves back to back, each with its own error log. A one-rank in-process HIP solver enqueues the n graph
+        replays and synchronises once (``GpuSolver::run_batch``, the bench's timed block; solve_s = batch time / n);
+        every other backend runs run() n times."""
+        if self.backend == "hip" and self.runtime == "inproc" and hasattr(self._impl, "run_batch"):
+            return [SolveResult(self.spec, self.backend, self.transport, self.world, tuple(self.dims), list(r["steps"]),
+                                list(r["max_err"]), list(r["rms_err"]), float(r["solve_s"]), bool(r["finite"]),
+                                {k: v for k, v in r.items() if k not in ("steps", "max_err", "rms_err", "solve_s",
+                                                                         "finite")})
+                    for r in self._impl.run_batch(int(n))]
+        return [self.run() for _ in range(int(n))]
+
     def set_state(self, prev, cur, step: int) -> None:
         """Loaded-field start (resume): every following run() starts at ``step`` from u^{step-1} = prev and
         u^{step} = cur (GLOBAL (N+1)³ float64 arrays or tensors, e.g. utils.dump.load of a checkpoint) and continues to

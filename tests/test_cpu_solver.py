@@ -48,3 +48,16 @@ def test_cfl_guard_and_blowup_detection():
         Solver(ProblemSpec(N=64, tau=0.02, K=30), backend="cpu")
     r = solve(ProblemSpec(N=64, tau=0.02, K=400, check_every=100), backend="cpu", force=True)
     assert not r.finite or r.max_err[-1] > 1e3
+
+
+def test_run_batch_falls_back_to_run_on_cpu():
+    """Solver.run_batch(n) on a backend without a batched native path: n ordinary solves, each the run() log."""
+    from mpi_cuda_amd import ProblemSpec
+    from mpi_cuda_amd.solver import Solver
+
+    s = Solver(ProblemSpec(N=24, tau=1e-3, K=6, check_every=1), backend="cpu")
+    r1 = s.run()
+    rs = s.run_batch(3)
+    assert len(rs) == 3
+    for r in rs:
+        assert r.steps == r1.steps and r.max_err == r1.max_err and r.rms_err == r1.rms_err

@@ -142,9 +142,9 @@ def test_run_batch_pipelined_logs(gpu):
     r1 = s.run()  # (captures the graph)
     h1 = s.field_hash(0)
     for n in (3, 7):
-        rs = s._impl.run_batch(n)
+        rs = s.run_batch(n)
         assert len(rs) == n
         for r in rs:
-            assert list(r["steps"]) == r1.steps and list(r["max_err"]) == r1.max_err
-            assert list(r["rms_err"]) == r1.rms_err and r["solve_s"] > 0
+            assert r.steps == r1.steps and r.max_err == r1.max_err
+            assert r.rms_err == r1.rms_err and r.solve_s > 0 and r.finite
         assert s.field_hash(0) == h1

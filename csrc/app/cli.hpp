@@ -26,7 +26,7 @@ struct Args {
   bool timers = false;
   bool debug_sync = false;
   bool poison = false;
-  int temporal = 4;
+  int temporal = 5;
   bool tb = true;
   int tb_threads = 0;
   int tb_init_threads = 0;

@@ -77,7 +77,7 @@ void launch_leapfrog2(const Layout& l, const Coeffs& c, const double* prev, cons
 // the kernel (init_first's formulas, bit-identical), prev/cur are not read: it writes u^S, u^{S+1} with no HBM reads.
 constexpr int kTbTile = 32;  // (y, z) tile edge of the LDS S-step passes (leapfrog_tb_kernel.hpp tbk::kTile)
 struct LeapfrogTbTiling {
-  int stages = 4;         // 2, 3 or 4 steps per pass
+  int stages = 4;         // steps per pass: 2..4 (k_leapfrog_tb), 2..5 (k_leapfrog_p2)
   int threads = 1024;     // workgroup size (768 or 1024)
   int init_threads = 768; // ... of the analytic-start pass (measured at 512³, S = 3: 768 → 932 µs, 1024 → 1027 µs;
                           // the S = 4 passes go the other way: 768 → 1123 µs, 1024 → 1076 µs)
@@ -85,6 +85,7 @@ struct LeapfrogTbTiling {
   bool xcd_blocks = false; // with xcd_remap: each XCD owns a square-ish tile block, not two-row strips (measured: no gain)
   int target_blocks = 256; // fewer (y,z) tiles than this: split x into chunks (one workgroup per CU at 1 WG/CU)
   int min_chunk = 16;      // ... of at least this many planes (each chunk recomputes S−1 planes on both sides)
+  bool p2 = true;          // the pair-tiled pass (k_leapfrog_p2, S ≤ 5) wherever it applies (leapfrog_p2_supported)
 };
 // Slab peer-push transport of an LDS pass (x faces only; every slab rank has the same plane geometry, so a plane's
 // in-plane offsets are the same on both sides). The pass
@@ -149,6 +150,17 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
                         const LBox& real = tb_default_real(), bool analytic_start = false, int level_stride = 0,
                         int grid_blocks = 0, const TbPush* push = nullptr, const TbPush* push_dev = nullptr,
                         const TbPack* pack = nullptr, const TbPack* pack_dev = nullptr);
+
+// The pair-tiled S-step pass (kernels_leapfrog_p2.hip): the same contract as launch_leapfrog_tb for boxes that span
+// the rank's whole y/z interior (one rank, x slabs) and S = 2..5 (analytic start: 2..4); no push / fused pack.
+// launch_leapfrog_tb dispatches to it when tiling.p2 is set and it applies.
+bool leapfrog_p2_supported(const Layout& l, const LBox& box, int stages);
+int leapfrog_p2_partials(const Layout& l, const LBox& box, const LeapfrogTbTiling& t);
+void leapfrog_p2_prepare();
+void launch_leapfrog_p2(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
+                        double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
+                        Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, const LBox& real,
+                        bool analytic_start, int level_stride = 0, int grid_blocks = 0);
 
 // Error of a stored field vs φ·ct over `box` (step 1 / standalone check). Writes leapfrog-compatible partials and
 // returns how many.

@@ -69,7 +69,7 @@ int load_checkpoint(const std::string& prefix, const Problem& p, std::vector<dou
 // simplicity; a later candidate must beat every earlier one by more than the tie margin to be chosen.
 struct Candidate {
   std::string name, decomp, transport;  // transport: rccl | sdma | push
-  int temporal = 4;
+  int temporal = 5;
   bool overlap = true;
   int sdma_streams = 0;            // copy streams (0: the solver's default)
   bool shells_concurrent = false;  // overlap: shells beside the interior instead of before it

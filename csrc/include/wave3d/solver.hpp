@@ -40,11 +40,12 @@ struct SolverOptions {
   bool poison_ghosts = false;   // NaN-fill ghost layers before each exchange (a missed halo poisons the errors)
   bool fake_comm = false;       // perf study only: run rank `rank` of `world` alone, exchanges replaced by no-ops
   LeapfrogTiling tiling;
-  // Temporal blocking: up to `temporal` (2..4) steps per HBM pass wherever no halo exchange intervenes. One rank:
-  // k_leapfrog_tb passes (all levels in LDS, error checks at any level), the steps split into passes by measured
-  // per-step cost; slab ranks: the same LDS passes with `temporal`-deep x halos (one exchange per pass; tb = false:
-  // two-step k_leapfrog2 passes with 2-deep halos). 1 = one step per pass everywhere.
-  int temporal = 4;
+  // Temporal blocking: up to `temporal` (2..5) steps per HBM pass wherever no halo exchange intervenes. One rank:
+  // k_leapfrog_p2 passes (pair-tiled, S ≤ 5; all levels in LDS, error checks at any level), the steps split into
+  // passes by measured per-step cost; slab ranks: k_leapfrog_tb passes with `temporal`-deep x halos, S ≤ 4 (5 is
+  // taken as 4; one exchange per pass; tb = false: two-step k_leapfrog2 passes with 2-deep halos). 1 = one step
+  // per pass everywhere.
+  int temporal = 5;
   bool tb = true;  // one rank: LDS kernel (false: k_leapfrog2 pairs, only where the intermediate step has no check)
   Leapfrog2Tiling tiling2;
   LeapfrogTbTiling tiling_tb;
@@ -332,6 +333,7 @@ class GpuSolver {
   // one batched launch when the regions wrap and at the end of the solve (one launch instead of one per checked step)
   static constexpr int kTbRegions = 8;
   static constexpr int kTbSlots = 8;  // launches with partials per level and unit (shell boxes + interior)
+  static constexpr int kTbLevels = 5; // levels per pass (5-step passes: k_leapfrog_p2)
   Partial* tb_partials_ = nullptr;
   int tb_region_ = 0;
   std::vector<ReduceJob> pending_;

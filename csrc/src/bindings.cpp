@@ -397,7 +397,9 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("xcd_remap", &LeapfrogTbTiling::xcd_remap)
       .def_readwrite("xcd_blocks", &LeapfrogTbTiling::xcd_blocks)
       .def_readwrite("target_blocks", &LeapfrogTbTiling::target_blocks)
-      .def_readwrite("min_chunk", &LeapfrogTbTiling::min_chunk);
+      .def_readwrite("min_chunk", &LeapfrogTbTiling::min_chunk)
+      .def_readwrite("p2", &LeapfrogTbTiling::p2);
+  m.def("gpu_leapfrog_p2_supported", &leapfrog_p2_supported);
   m.def("gpu_leapfrog_tb_lds_bytes", &leapfrog_tb_lds_bytes);
   m.def("gpu_leapfrog_tb_partials", &leapfrog_tb_partials);
   m.def("gpu_leapfrog_tb",
@@ -405,7 +407,7 @@ PYBIND11_MODULE(_C, m) {
            std::uintptr_t out2, const LBox& box, std::uintptr_t s, std::vector<double> ct, int check_mask,
            std::uintptr_t partials, const LeapfrogTbTiling& t, std::uintptr_t stream, const LBox& real,
            bool analytic_start) {
-          ct.resize(4, 0.0);
+          ct.resize(5, 0.0);
           launch_leapfrog_tb(l, c, dptr<const double>(prev), dptr<const double>(cur), dptr<double>(out1),
                              dptr<double>(out2), box, dptr<const double>(s) + 1, ct.data(), check_mask,
                              dptr<Partial>(partials), t, sptr(stream), real, analytic_start);

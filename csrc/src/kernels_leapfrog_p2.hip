@@ -1,0 +1,181 @@
+// Pair-tiled deep temporal blocking (k_leapfrog_p2, leapfrog_p2_kernel.hpp): S = 2..5 leapfrog steps per HBM pass.
+//
+// Why a second LDS S-step kernel. The 4-step pass of k_leapfrog_tb (one node per thread and position set) ran at
+// 1.0–1.06 ms against ≈0.8 ms for its bytes, and its compute alone took 684 µs (profiles/r4/lds_read2.md): per bulk
+// iteration a wave issued ≈570 instructions for 8 node-stages — 240 of them scalar (exec-mask branches per stage and
+// position set, 64-bit plane pointers), 13 LDS reads + a write per node-stage, and 9 of 16 waves carried a second,
+// partly empty position set that the others waited for at every barrier. S = 5 (one HBM pass fewer per 20-step
+// solve) did not fit its registers. This kernel is laid out for CDNA4 from the instruction stream up:
+//   * TWO z-adjacent nodes per thread (a 16-byte pair): the y neighbours of both are one ds_read_b128 each, the z
+//     neighbours one ds_read_b64 each, the new values one ds_write_b128 — 5 LDS instructions per pair-stage instead of
+//     10 — and the loads and stores of a pair are one buffer dwordx4 each;
+//   * the tile's own 32 × 32 nodes are exactly waves 0–7 (the lane groups of ds_read_b128 each hold one tile row, so
+//     every y-neighbour read is conflict-free); the halo pairs follow in "onion" order, so a wave computes only the
+//     stages its deepest pair needs (stage k's region shrinks by one node per side), and the halo waves are dealt to
+//     the four SIMDs by stage work (leapfrog_p2_kernel.hpp make_tab): per plane ≈54 pair-stage wave-instructions
+//     where position sets × stages would be 62.5, spread within one stage over the SIMDs;
+//   * stores and the check run only in waves 0–7 (wave-uniform), Dirichlet zeros are selects on SGPR lane masks
+//     (all-true in interior tiles), the x tests of the general planes are scalar: the bulk iteration has no exec-mask
+//     branches at all;
+//   * planes are addressed through buffer resources (a 32-bit per-thread offset, the plane base in SGPRs; an offset
+//     past the plane returns 0 / drops a store), and every wave issues the same vector-memory sequence, so the
+//     in-order vmcnt wait of the u^n commit covers exactly its load, not the previous stores;
+//   * S = 5 at 128 VGPRs: u^{n−1} and u^n are loaded late (after stages 1 and 2, into registers those stages free),
+//     three per-thread LDS bases replace per-plane address registers, and the loop-invariant address folding that
+//     LLVM would otherwise hoist is blocked per iteration.
+// One pass is bit-identical to S single steps (stencil.hpp formulas and operation order), the analytic-start pass to
+// k_init_first + S steps. Tests: tests/test_gpu_kernels.py (test_leapfrog_p2_*).
+#include "wave3d/leapfrog_p2_launch.hpp"
+
+namespace wave3d {
+
+using namespace p2k;
+
+namespace {
+
+struct P2Plan {
+  P2Params prm{};
+  int nblocks = 0;
+};
+
+// LDS budget of a pass: the largest x chunk whose sin table still fits next to the planes
+int p2_max_xlen(int S, bool init) {
+  const size_t cap = 160 * 1024 - 2 * 16 * sizeof(double) - 256;  // minus the reduction arrays (+ alignment slack)
+  size_t base = 0;
+  switch (S) {
+    case 2: base = init ? p2_lds_bytes<true, 2>(0) : p2_lds_bytes<false, 2>(0); break;
+    case 3: base = init ? p2_lds_bytes<true, 3>(0) : p2_lds_bytes<false, 3>(0); break;
+    case 4: base = init ? p2_lds_bytes<true, 4>(0) : p2_lds_bytes<false, 4>(0); break;
+    default: base = p2_lds_bytes<false, 5>(0); break;
+  }
+  if (base >= cap) return 0;
+  return static_cast<int>((cap - base) / sizeof(double)) - (2 * S + 4);
+}
+
+P2Plan make_plan_p2(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, LBox real, bool init) {
+  const int S = t.stages;
+  W3D_REQUIRE(S >= 2 && S <= 5, "leapfrog_p2: stages must be 2..5");
+  W3D_REQUIRE(!init || S <= 4, "leapfrog_p2: the analytic-start pass takes at most 4 steps");
+  W3D_REQUIRE(leapfrog_p2_supported(l, b, S), "leapfrog_p2: the box must span the rank's whole y/z interior");
+  const LBox full = compute_box(l);
+  if (real.x0 > real.x1) {
+    real.x0 = full.x0;
+    real.x1 = full.x1;
+  }
+  // x: u^{n+k} (k < S) is read up to S−k planes beyond the box (real there, or beyond the global boundary); u^n is
+  // read S planes beyond, within the allocation unless beyond the global boundary
+  const bool lo_ok = real.x0 <= b.x0 - (S - 1) || l.gx0 + real.x0 <= 1;
+  const bool hi_ok = real.x1 >= b.x1 + (S - 1) || l.gx0 + real.x1 >= l.N;
+  W3D_REQUIRE(lo_ok && hi_ok, "leapfrog_p2: stage-1 range does not cover the box halo in x");
+  W3D_REQUIRE(l.gx0 + b.x0 - S <= 0 || b.x0 - S >= -l.xg, "leapfrog_p2: halo deeper than the ghosts in x");
+  W3D_REQUIRE(l.gx0 + b.x1 + S - 1 >= l.N || b.x1 + S - 1 < l.nx + l.xg, "leapfrog_p2: halo deeper than the ghosts in x");
+  W3D_REQUIRE(real.x0 >= -l.xg && real.x1 <= l.nx + l.xg, "leapfrog_p2: real range outside the allocation in x");
+  W3D_REQUIRE(l.plane < (i64{1} << 27), "leapfrog_p2: plane too large for 32-bit buffer offsets");
+  P2Plan pl;
+  P2Params& p = pl.prm;
+  p.plane = l.plane;
+  p.pitch = static_cast<int>(l.pitch);
+  p.ya = static_cast<int>(l.yg);
+  p.za = static_cast<int>(l.zg + l.zs);
+  p.ay0 = static_cast<int>(-l.yg);
+  p.ay1 = static_cast<int>(l.ny + l.yg);
+  p.x0 = static_cast<int>(b.x0);
+  p.x1 = static_cast<int>(b.x1);
+  p.xlen = static_cast<int>(imax(1, b.x1 - b.x0));
+  p.nxc = 1;
+  p.sx0 = static_cast<int>(real.x0);
+  p.sx1 = static_cast<int>(real.x1);
+  p.ax0 = static_cast<int>(-l.xg);
+  p.ax1 = static_cast<int>(l.nx + l.xg);
+  p.N = static_cast<int>(l.N);
+  p.gx0 = static_cast<int>(l.gx0);
+  p.gy0 = static_cast<int>(l.gy0);
+  p.gz0 = static_cast<int>(l.gz0);
+  p.y0 = static_cast<int>(b.y0);
+  p.z0 = static_cast<int>(b.z0);
+  p.y1 = static_cast<int>(b.y1);
+  p.z1 = static_cast<int>(b.z1);
+  if (b.x1 <= b.x0 || b.y1 <= b.y0 || b.z1 <= b.z0) return pl;
+  p.nty = static_cast<int>(ceil_div(b.y1 - b.y0, kT));
+  p.ntz = static_cast<int>(ceil_div(b.z1 - b.z0, kT));
+  const int tiles = p.nty * p.ntz;
+  const i64 nxb = b.x1 - b.x0;
+  i64 want = 1;
+  // x chunks when the tile grid alone leaves CUs idle (at least min_chunk planes each), or when the x sin table of
+  // the whole range would not fit the LDS
+  if (t.target_blocks > tiles) want = imin(ceil_div(t.target_blocks, tiles), imax(1, nxb / imax(1, t.min_chunk)));
+  const int maxlen = p2_max_xlen(S, init);
+  W3D_REQUIRE(maxlen >= 1, "leapfrog_p2: the tile does not fit in LDS");
+  want = imax(want, ceil_div(nxb, maxlen));
+  p.xlen = static_cast<int>(ceil_div(nxb, want));
+  p.nxc = static_cast<int>(ceil_div(nxb, p.xlen));
+  const int blocks = tiles * p.nxc;
+  pl.nblocks = t.xcd_remap ? static_cast<int>(round_up(blocks, 8)) : blocks;
+  p.nblocks = pl.nblocks;
+  p.xcd_remap = t.xcd_remap ? 1 : 0;
+  p.xper = pl.nblocks / 8;
+  return pl;
+}
+
+}  // namespace
+
+bool leapfrog_p2_supported(const Layout& l, const LBox& box, int stages) {
+  // the pass's tiles span the rank's whole y/z compute range (one rank, or x slabs), pairs start on 16-byte nodes
+  const LBox full = compute_box(l);
+  return stages >= 2 && stages <= 5 && box.y0 == full.y0 && box.y1 == full.y1 && box.z0 == full.z0 &&
+         box.z1 == full.z1 && l.gy0 == 0 && l.gz0 == 0 && l.ny == l.N + 1 && l.nz == l.N + 1 && l.yg >= 1 &&
+         l.zg >= 1 && (box.z0 + l.zg + l.zs) % 2 == 0;
+}
+
+int leapfrog_p2_partials(const Layout& l, const LBox& box, const LeapfrogTbTiling& t) {
+  LeapfrogTbTiling t1 = t;
+  t1.stages = 2;  // (block count: the tiling and the x chunks; S = 2 keeps the ghost-depth checks satisfiable)
+  const LBox real{-l.xg, l.nx + l.xg, 1, 0, 1, 0};
+  return make_plan_p2(l, box, t1, real, false).nblocks;
+}
+
+void leapfrog_p2_prepare() {
+  prepare_p2_s2();
+  prepare_p2_s3();
+  prepare_p2_s4();
+  prepare_p2_s5();
+}
+
+void launch_leapfrog_p2(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
+                        double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
+                        Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, const LBox& real,
+                        bool analytic_start, int level_stride, int grid_blocks) {
+  W3D_REQUIRE(out1 != out2 && (analytic_start || (prev != out1 && prev != out2 && cur != out1 && cur != out2)),
+              "leapfrog_p2 needs four distinct buffers");
+  P2Plan pl = make_plan_p2(l, box, t, real, analytic_start);
+  if (pl.nblocks == 0) return;
+  P2Params& p = pl.prm;
+  if (grid_blocks > 0) {
+    W3D_REQUIRE(grid_blocks >= pl.nblocks && (!t.xcd_remap || grid_blocks % 8 == 0), "leapfrog_p2: bad grid_blocks");
+    pl.nblocks = p.nblocks = grid_blocks;
+    p.xper = pl.nblocks / 8;
+  }
+  const i64 kb = (l.xg - 1) * l.plane;  // x base only: in-plane offsets are plane-relative
+  p.prev = analytic_start ? out1 + kb : prev + kb;  // (the analytic start reads neither: any valid buffer)
+  p.cur = analytic_start ? out2 + kb : cur + kb;
+  p.out1 = out1 + kb;
+  p.out2 = out2 + kb;
+  p.s = d_s;
+  p.tau2 = c.lam;
+  p.half_tau2 = c.half_lam;
+  p.check_mask = partials != nullptr ? (check_mask & ((1 << t.stages) - 1)) : 0;
+  p.partials = p.check_mask != 0 ? partials : nullptr;
+  W3D_REQUIRE(level_stride == 0 || level_stride >= pl.nblocks, "leapfrog_p2: level stride below the block count");
+  p.lstride = level_stride > 0 ? level_stride : pl.nblocks;
+  for (int k = 0; k < 5; ++k) p.ct[k] = (ct != nullptr && k < t.stages) ? ct[k] : 0.0;
+  switch (t.stages) {
+    case 2: launch_p2_s2(p, pl.nblocks, analytic_start, stream); break;
+    case 3: launch_p2_s3(p, pl.nblocks, analytic_start, stream); break;
+    case 4: launch_p2_s4(p, pl.nblocks, analytic_start, stream); break;
+    default: launch_p2_s5(p, pl.nblocks, analytic_start, stream); break;
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) fail(std::string("leapfrog_p2 launch: ") + hipGetErrorString(e));
+}
+
+}  // namespace wave3d

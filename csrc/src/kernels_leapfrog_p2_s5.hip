@@ -1,0 +1,15 @@
+// k_leapfrog_p2 instantiations for S = 5 (normal passes only: an analytic-start pass with its φ slots would not fit
+// the 160 KiB of LDS at S = 5). Design: kernels_leapfrog_p2.hip.
+#include "wave3d/leapfrog_p2_launch.hpp"
+
+namespace wave3d {
+namespace p2k {
+
+void launch_p2_s5(const P2Params& p, int nblocks, bool init, hipStream_t st) {
+  W3D_REQUIRE(!init, "leapfrog_p2: the analytic-start pass takes at most 4 steps");
+  launch_cm<5, false>(p, nblocks, st);
+}
+void prepare_p2_s5() { prepare_all<5, false>(); }
+
+}  // namespace p2k
+}  // namespace wave3d

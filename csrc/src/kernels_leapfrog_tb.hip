@@ -30,6 +30,8 @@
 // passes, deeper prefetch, half tiles, branch-free selects, a conflict-free position order) are documented with their
 // numbers in profiles/r1_tb_queue_experiments.md. The pass
 // semantics (which plane of which level each stage reads) are mirrored by tools/tb_emulate.py (CPU tests).
+#include <algorithm>
+
 #include "wave3d/leapfrog_tb_kernel.hpp"
 
 namespace wave3d {
@@ -51,6 +53,7 @@ void l2_flush_all(hipStream_t stream) {
 }
 
 void leapfrog_tb_prepare(bool push) {
+  leapfrog_p2_prepare();
   if (push) prepare_push();
   prepare_nt<2, 768, false>();
   prepare_nt<3, 768, false>();
@@ -76,7 +79,9 @@ int leapfrog_tb_partials(const Layout& l, const LBox& box, const LeapfrogTbTilin
   const LBox real{-l.xg, l.nx + l.xg, -l.yg, l.ny + l.yg, -l.zg, l.nz + l.zg};
   LeapfrogTbTiling t1 = t;
   t1.stages = 2;  // (block count independent of S; S = 2 keeps the ghost-depth checks satisfiable)
-  return make_plan_tb(l, box, t1, real).nblocks;
+  const int n = make_plan_tb(l, box, t1, real).nblocks;
+  // (the pair-tiled pass may split x differently: a slot holds either kernel's partials)
+  return t.p2 && leapfrog_p2_supported(l, box, 2) ? std::max(n, leapfrog_p2_partials(l, box, t)) : n;
 }
 
 void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
@@ -86,6 +91,13 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
                         const TbPush* push_dev, const TbPack* pack, const TbPack* pack_dev) {
   W3D_REQUIRE(out1 != out2 && (analytic_start || (prev != out1 && prev != out2 && cur != out1 && cur != out2)),
               "leapfrog_tb needs four distinct buffers");
+  if (t.p2 && (push == nullptr || !push->on) && pack == nullptr && leapfrog_p2_supported(l, box, t.stages) &&
+      (!analytic_start || t.stages <= 4)) {
+    launch_leapfrog_p2(l, c, prev, cur, out1, out2, box, d_s, ct, check_mask, partials, t, stream, real,
+                       analytic_start, level_stride, grid_blocks);
+    return;
+  }
+  W3D_REQUIRE(t.stages <= 4, "leapfrog_tb: 5-step passes need the pair-tiled kernel (tiling.p2)");
   TbPlan pl = make_plan_tb(l, box, t, real);
   if (pl.nblocks == 0) return;
   TbParams& p = pl.prm;

@@ -162,7 +162,9 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   // schedule mode: temporal blocking on one rank, or on a 1-D slab decomposition with `temporal`-deep x halos (LDS
   // passes) or 2-deep ones (two-step passes). Decided from the SMALLEST rank box so every rank picks the same mode.
   mode_ = Mode::kSingleStep;
-  W3D_REQUIRE(opt_.temporal >= 1 && opt_.temporal <= 4, "temporal must be 1..4");
+  W3D_REQUIRE(opt_.temporal >= 1 && opt_.temporal <= 5, "temporal must be 1..5");
+  // 5-step passes: the pair-tiled kernel on one rank only (multi-rank passes keep k_leapfrog_tb's S ≤ 4)
+  if (opt_.temporal == 5 && (world > 1 || !opt_.tb || !opt_.tiling_tb.p2)) opt_.temporal = 4;
   if (opt_.temporal >= 2 && world == 1) mode_ = Mode::kFusedSingle;
   const bool slab = dims_.py == 1 && dims_.pz == 1;
   if (opt_.temporal >= 2 && world > 1) {
@@ -387,7 +389,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   // the LDS passes' partials live apart: their reductions are deferred, so the immediate users of partials_ (init,
   // single steps between passes) must not overwrite them
   if (n_tb_ > 0)
-    W3D_HIP(hipMalloc(&tb_partials_, static_cast<size_t>(kTbRegions) * 4 * kTbSlots * n_tb_ * sizeof(Partial)));
+    W3D_HIP(hipMalloc(&tb_partials_, static_cast<size_t>(kTbRegions) * kTbLevels * kTbSlots * n_tb_ * sizeof(Partial)));
   W3D_HIP(hipMalloc(&errlog_, static_cast<size_t>(prob_.K + 1) * sizeof(Partial)));
   W3D_HIP(hipMalloc(&errall_, static_cast<size_t>(world_) * (prob_.K + 1) * sizeof(Partial)));
   ct_.resize(static_cast<size_t>(prob_.K + 1));
@@ -444,7 +446,7 @@ size_t GpuSolver::device_bytes() const {
          static_cast<size_t>(imax(plan_.packed_doubles, deep_max_) + imax(plan_.packed_doubles, send_total_)) *
              sizeof(double) +
          static_cast<size_t>(n_partials_) * sizeof(Partial) + static_cast<size_t>(prob_.N + 3) * sizeof(double) +
-         static_cast<size_t>(kTbRegions) * 4 * kTbSlots * static_cast<size_t>(n_tb_) * sizeof(Partial);
+         static_cast<size_t>(kTbRegions) * kTbLevels * kTbSlots * static_cast<size_t>(n_tb_) * sizeof(Partial);
 }
 
 void GpuSolver::set_state(const double* prev, const double* cur, int n0) {
@@ -554,9 +556,15 @@ void GpuSolver::build_units() {
     // pass of s steps with every 2nd level checked, measured at 512³ (tools/tune_leapfrog.py --tb); the analytic
     // first pass reads nothing but computes u⁰, u¹ (compute-bound). Slab ranks (deep-tb) take passes of ≥ 2 steps
     // only: every pass writes the two levels the next one reads, so each exchange is one message pair per face.
-    static const double kStepCost[5] = {0.0, 610.0, 437.0, 302.0, 258.0};
+    static const double kStepCostTb[6] = {0.0, 610.0, 437.0, 302.0, 258.0, 1e9};
     // (analytic: φ-stage start, re-measured)
-    static const double kAnalyticCost[5] = {0.0, 1e9, 346.0, 300.0, 318.0};
+    static const double kAnalyticCostTb[6] = {0.0, 1e9, 346.0, 300.0, 318.0, 1e9};
+    // the pair-tiled passes (k_leapfrog_p2, one rank): µs per step at 512³ (profiles/r5/)
+    static const double kStepCostP2[6] = {0.0, 610.0, 430.0, 290.0, 225.0, 180.0};
+    static const double kAnalyticCostP2[6] = {0.0, 1e9, 300.0, 200.0, 135.0, 1e9};
+    const bool p2 = opt_.tiling_tb.p2 && world_ == 1 && leapfrog_p2_supported(lay_, full_, 2);
+    const double* kStepCost = p2 ? kStepCostP2 : kStepCostTb;
+    const double* kAnalyticCost = p2 ? kAnalyticCostP2 : kAnalyticCostTb;
     const int rem = K - n, smax = opt_.temporal, smin = mode_ == Mode::kDeepTb ? 2 : 1;
     std::vector<double> best(static_cast<size_t>(rem + 1), 1e300);
     std::vector<int> take(static_cast<size_t>(rem + 1), 1);
@@ -831,7 +839,7 @@ void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase, hipStream_t s
   if (st == nullptr) st = s0_;
   LeapfrogTbTiling t = opt_.tiling_tb;
   t.stages = u.steps;
-  double cts[4] = {0, 0, 0, 0};
+  double cts[5] = {0, 0, 0, 0, 0};
   int mask = 0;
   for (int k = 1; k <= u.steps; ++k) {
     cts[k - 1] = ct_[static_cast<size_t>(u.n + k)];
@@ -839,7 +847,7 @@ void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase, hipStream_t s
   }
   const int slots = mode_ == Mode::kDeepTb ? kTbSlots : 1;
   W3D_REQUIRE(tb_slots_ < slots, "leapfrog_tb: too many launches in one unit");
-  Partial* part = mask ? tb_partials_ + tb_region_ * (4 * slots * n_tb_) + tb_slots_ * n_tb_ : nullptr;
+  Partial* part = mask ? tb_partials_ + tb_region_ * (kTbLevels * slots * n_tb_) + tb_slots_ * n_tb_ : nullptr;
   const LBox real = mode_ == Mode::kDeepTb ? sreal_ : tb_default_real();
   // push transport: this pass's parameters (make_push) from the table phase_init uploaded; the command-processor
   // waits (push_cp_wait) are stream operations issued here, before the launch
@@ -964,7 +972,7 @@ void GpuSolver::unit_interior(int i) {
     }
     const int slots = mode_ == Mode::kDeepTb ? kTbSlots : 1;
     if (tb_slots_ > 0) {
-      Partial* region = tb_partials_ + tb_region_ * (4 * slots * n_tb_);
+      Partial* region = tb_partials_ + tb_region_ * (kTbLevels * slots * n_tb_);
       for (int k = 1; k <= u.steps; ++k)
         if (is_check_[static_cast<size_t>(u.n + k)])
           pending_.push_back(ReduceJob{region + (k - 1) * slots * n_tb_, tb_slots_ * n_tb_, errlog_ + u.n + k});

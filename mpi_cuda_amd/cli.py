@@ -40,7 +40,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-temporal", action="store_true")
-    ap.add_argument("--temporal", type=int, default=4, help="at most this many steps per HBM pass (2..4)")
+    ap.add_argument("--temporal", type=int, default=5, help="at most this many steps per HBM pass (2..5)")
     ap.add_argument("--no-tb", action="store_true", help="two-step register-queue passes instead of the LDS kernel")
     ap.add_argument("--timers", action="store_true")
     ap.add_argument("--json", default="")

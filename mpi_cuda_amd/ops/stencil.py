@@ -112,8 +112,10 @@ def leapfrog2(layout, coeffs, prev: torch.Tensor, cur: torch.Tensor, out1: torch
 
 def leapfrog_tb(layout, coeffs, prev: torch.Tensor, cur: torch.Tensor, out1: torch.Tensor, out2: torch.Tensor, box,
                 s_ext: torch.Tensor, stages: int = 4, ct=None, check_mask: int = 0, threads: int = 1024,
-                analytic_start: bool = False):
+                analytic_start: bool = False, p2: bool = True, target_blocks: int | None = None):
     """``stages`` fused leapfrog steps held in LDS (HIP only): out1 = u^{n+S-1}, out2 = u^{n+S}.
+
+    ``p2`` selects the pair-tiled kernel (S <= 5) wherever it applies, else k_leapfrog_tb (S <= 4).
 
     ``ct[k-1]`` is the time factor of u^{n+k}; for every bit k-1 set in ``check_mask`` the (L∞, Σe²) error of u^{n+k}
     is returned in a dict {k: (max, sumsq)}. ``analytic_start``: n = 1, u⁰ and u¹ are computed in the kernel
@@ -124,6 +126,9 @@ def leapfrog_tb(layout, coeffs, prev: torch.Tensor, cur: torch.Tensor, out1: tor
     t = C.LeapfrogTbTiling()
     t.stages = stages
     t.threads = threads
+    t.p2 = p2  # the pair-tiled kernel (k_leapfrog_p2) where it applies; False: k_leapfrog_tb
+    if target_blocks is not None:
+        t.target_blocks = target_blocks
     nb = C.gpu_leapfrog_tb_partials(layout, box, t)
     ct = list(ct) if ct is not None else [0.0] * stages
     part = torch.empty((stages * max(nb, 1), 2), dtype=torch.float64, device=out1.device) if check_mask else None

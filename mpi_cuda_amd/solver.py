@@ -93,7 +93,7 @@ class Solver:
     def __init__(self, spec: ProblemSpec, backend: str = "auto", transport: str = "auto", decomp: str = "slab",
                  rank: int | None = None, world: int | None = None, device: int | None = None,
                  overlap: bool = True, graph: bool = True, threads: int = 0, tiling: dict | None = None,
-                 comm=None, group=None, stage_via_host: bool = False, force: bool = False, temporal: int = 4,
+                 comm=None, group=None, stage_via_host: bool = False, force: bool = False, temporal: int = 5,
                  tiling2: dict | None = None, init2: bool = True, timers: bool = False, tb: bool = True,
                  tiling_tb: dict | None = None,
                  debug_sync: bool = False, poison_ghosts: bool = False, deep_min_planes: int | None = None,
@@ -259,7 +259,7 @@ class Solver:
             self._impl.close()
 
     @staticmethod
-    def _options(C, decomp, spec, overlap, graph, tiling, temporal=4, tiling2=None, init2=True, tb=True,
+    def _options(C, decomp, spec, overlap, graph, tiling, temporal=5, tiling2=None, init2=True, tb=True,
                  tiling_tb=None):
         opts = C.SolverOptions()
         opts.temporal = temporal

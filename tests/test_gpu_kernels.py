@@ -187,7 +187,7 @@ def test_leapfrog_tb_equals_single_steps(gpu, stages, N, threads):
     o1 = torch.zeros(int(lay.total), dtype=torch.float64, device="cuda")
     o2 = torch.zeros_like(o1)
     mask = (1 << stages) - 1
-    e_gpu = ops.leapfrog_tb(lay, co, prev.cuda(), cur.cuda(), o1, o2, box, s.cuda(), stages, ct, mask, threads)
+    e_gpu = ops.leapfrog_tb(lay, co, prev.cuda(), cur.cuda(), o1, o2, box, s.cuda(), stages, ct, mask, threads, p2=False)
     torch.cuda.synchronize()
     assert torch.equal(ops.to_grid(lay, o1.cpu()), ops.to_grid(lay, a))
     assert torch.equal(ops.to_grid(lay, o2.cpu()), ops.to_grid(lay, b))
@@ -215,7 +215,7 @@ def test_leapfrog_tb_analytic_start(gpu, stages, N):
     o1 = torch.zeros(int(lay.total), dtype=torch.float64, device="cuda")
     o2 = torch.zeros_like(o1)
     e_gpu = ops.leapfrog_tb(lay, co, None, None, o1, o2, box, s.cuda(), stages, ct, (1 << stages) - 1,
-                            analytic_start=True)
+                            analytic_start=True, p2=False)
     torch.cuda.synchronize()
     inner = (slice(1, -1),) * 3  # u⁰ = φ also fills the ghosts of the CPU buffers; the pass writes the interior only
     assert torch.equal(ops.to_grid(lay, o1.cpu())[inner], ops.to_grid(lay, a)[inner])
@@ -223,6 +223,106 @@ def test_leapfrog_tb_analytic_start(gpu, stages, N):
     for k in range(1, stages + 1):
         assert e_gpu[k][0] == e_cpu[k][0]
         assert math.isclose(e_gpu[k][1], e_cpu[k][1], rel_tol=1e-12)
+
+
+def _rand_interior(C, lay, seed):
+    torch.manual_seed(seed)
+    g = torch.zeros((int(lay.nx) + 2, int(lay.ny) + 2, int(lay.nz) + 2), dtype=torch.float64)
+    g[2:-2, 2:-2, 2:-2] = torch.randn(int(lay.nx) - 2, int(lay.ny) - 2, int(lay.nz) - 2, dtype=torch.float64)
+    return ops.from_grid(lay, g)
+
+
+P2_MASKS = {"all": lambda S: (1 << S) - 1, "odd": lambda S: 0b10101 & ((1 << S) - 1),
+            "even": lambda S: 0b01010 & ((1 << S) - 1), "none": lambda S: 0}
+
+
+@pytest.mark.parametrize("stages", [2, 3, 4, 5])
+@pytest.mark.parametrize("N", [40, 77, 130])
+@pytest.mark.parametrize("chunked", [False, True])
+@pytest.mark.parametrize("mask", ["all", "odd", "even"])
+def test_leapfrog_p2_equals_single_steps(gpu, stages, N, chunked, mask):
+    """Pair-tiled pass (k_leapfrog_p2): one pass of S steps == S CPU steps, bit for bit, fields and checked levels.
+    chunked: x split into chunks (the CH instantiations); N = 130 has interior tiles (no Dirichlet select needed)."""
+    C = gpu
+    prob, co, lay, _ = _setup(C, N)
+    box = C.compute_box(lay)
+    assert C.gpu_leapfrog_p2_supported(lay, box, stages)
+    prev, cur = _rand_interior(C, lay, N * 13 + stages), _rand_interior(C, lay, N * 17 + stages)
+    s = ops.sin_table_ext(prob)
+    ct = [math.cos(prob.a_t * (5 + k) * prob.tau) for k in range(1, stages + 1)]
+    a, b = prev.clone(), cur.clone()
+    e_cpu = {}
+    for k in range(1, stages + 1):
+        e_cpu[k] = ops.leapfrog(lay, co, b, a, [box], s, ct[k - 1], check=True)
+        a, b = b, a
+    o1 = torch.zeros(int(lay.total), dtype=torch.float64, device="cuda")
+    o2 = torch.zeros_like(o1)
+    m = P2_MASKS[mask](stages)
+    e_gpu = ops.leapfrog_tb(lay, co, prev.cuda(), cur.cuda(), o1, o2, box, s.cuda(), stages, ct, m,
+                            p2=True, target_blocks=256 if chunked else 1)
+    torch.cuda.synchronize()
+    assert torch.equal(ops.to_grid(lay, o1.cpu()), ops.to_grid(lay, a))
+    assert torch.equal(ops.to_grid(lay, o2.cpu()), ops.to_grid(lay, b))
+    assert sorted(e_gpu) == [k for k in range(1, stages + 1) if m >> (k - 1) & 1]
+    for k in e_gpu:
+        assert e_gpu[k][0] == e_cpu[k][0]
+        assert math.isclose(e_gpu[k][1], e_cpu[k][1], rel_tol=1e-12)
+    # PyTorch fp64 reference of the last level (S plain leapfrog steps of the same op)
+    pa, pb = ops.to_grid(lay, prev), ops.to_grid(lay, cur)
+    for _ in range(stages):
+        pa, pb = pb, ops.ref_leapfrog_grid(pb, pa, co.ihx2, co.ihy2, co.ihz2, co.tau2, box)
+    torch.testing.assert_close(ops.to_grid(lay, o2.cpu()), pb, rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("stages", [2, 3, 4])
+@pytest.mark.parametrize("N", [40, 77, 130])
+@pytest.mark.parametrize("chunked", [False, True])
+def test_leapfrog_p2_analytic_start(gpu, stages, N, chunked):
+    """Pair-tiled analytic-start pass == init_first + S CPU steps on the interior, bit for bit."""
+    C = gpu
+    prob, co, lay, _ = _setup(C, N)
+    box = C.compute_box(lay)
+    s = ops.sin_table_ext(prob)
+    u0, u1 = ops.alloc_field(lay), ops.alloc_field(lay)
+    ops.init_first(lay, co, s, u0, u1)
+    ct = [math.cos(prob.a_t * (1 + k) * prob.tau) for k in range(1, stages + 1)]
+    a, b = u0.clone(), u1.clone()
+    e_cpu = {}
+    for k in range(1, stages + 1):
+        e_cpu[k] = ops.leapfrog(lay, co, b, a, [box], s, ct[k - 1], check=True)
+        a, b = b, a
+    o1 = torch.zeros(int(lay.total), dtype=torch.float64, device="cuda")
+    o2 = torch.zeros_like(o1)
+    e_gpu = ops.leapfrog_tb(lay, co, None, None, o1, o2, box, s.cuda(), stages, ct, (1 << stages) - 1,
+                            analytic_start=True, p2=True, target_blocks=256 if chunked else 1)
+    torch.cuda.synchronize()
+    inner = (slice(1, -1),) * 3
+    assert torch.equal(ops.to_grid(lay, o1.cpu())[inner], ops.to_grid(lay, a)[inner])
+    assert torch.equal(ops.to_grid(lay, o2.cpu())[inner], ops.to_grid(lay, b)[inner])
+    for k in range(1, stages + 1):
+        assert e_gpu[k][0] == e_cpu[k][0]
+        assert math.isclose(e_gpu[k][1], e_cpu[k][1], rel_tol=1e-12)
+
+
+def test_leapfrog_p2_equals_tb(gpu):
+    """The two LDS kernels agree bit for bit on a 4-step pass (same formulas and operation order)."""
+    C = gpu
+    prob, co, lay, _ = _setup(C, 96)
+    box = C.compute_box(lay)
+    prev, cur = _rand_interior(C, lay, 5), _rand_interior(C, lay, 6)
+    s = ops.sin_table_ext(prob).cuda()
+    ct = [0.5, 0.4, 0.3, 0.2]
+    outs = []
+    for p2 in (False, True):
+        o1 = torch.zeros(int(lay.total), dtype=torch.float64, device="cuda")
+        o2 = torch.zeros_like(o1)
+        e = ops.leapfrog_tb(lay, co, prev.cuda(), cur.cuda(), o1, o2, box, s, 4, ct, 0b1111, p2=p2)
+        outs.append((o1.cpu(), o2.cpu(), e))
+    assert torch.equal(ops.to_grid(lay, outs[0][0]), ops.to_grid(lay, outs[1][0]))
+    assert torch.equal(ops.to_grid(lay, outs[0][1]), ops.to_grid(lay, outs[1][1]))
+    for k in range(1, 5):
+        assert outs[0][2][k][0] == outs[1][2][k][0]
+        assert math.isclose(outs[0][2][k][1], outs[1][2][k][1], rel_tol=1e-12)
 
 
 @pytest.mark.parametrize("N,world,rank,decomp", [(36, 1, 0, "slab"), (53, 1, 0, "slab"), (40, 2, 1, "slab"),

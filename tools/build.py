@@ -49,6 +49,11 @@ LIB_SOURCES = [
     ("src/kernels_init2.hip", "hip"),
     ("src/kernels_leapfrog_tb.hip", "hip"),
     ("src/kernels_leapfrog_tb_push.hip", "hip"),
+    ("src/kernels_leapfrog_p2.hip", "hip"),
+    ("src/kernels_leapfrog_p2_s2.hip", "hip"),
+    ("src/kernels_leapfrog_p2_s3.hip", "hip"),
+    ("src/kernels_leapfrog_p2_s4.hip", "hip"),
+    ("src/kernels_leapfrog_p2_s5.hip", "hip"),
     ("src/solver_gpu.cpp", "hip"),
     ("src/transport_sdma.cpp", "hip"),
     ("src/runtime_launch.cpp", "hip"),

@@ -25,9 +25,12 @@ step is one solve); ``vs_baseline`` = value ÷ the reference's published total-t
 best number, the 2-GPU 5.316 — ``vs_baseline_basis`` says which). The problem size is fixed as GPUs are added:
 ``scaling`` is "strong". ``rccl_nranks`` is the communicator size RCCL itself reports (ncclCommCount).
 
-If the native runtime fails on any rank, every rank stops with a non-zero exit and no JSON line. ``--allow-fallback``
-instead re-runs the solve in-process over the torch.distributed transport (the Python single-step loop) and marks the
-line ``"degraded": true`` with the error text. ``--python`` runs the in-process Python ``Solver`` path directly.
+On several ranks the copy-engine (SDMA) schedules join the autotune only after a cross-device qualification child (a
+64³ solve whose log must equal a one-rank solve's) passes. If the main native run fails on any rank, every rank starts
+ONE fresh child with the conservative schedule (RCCL slabs, 4-step passes, no overlap, no autotune) and the line says
+so (``fallback_schedule``, ``first_failure``); if that fails too, every rank stops with a non-zero exit and no JSON
+line. ``--allow-fallback`` then re-runs the solve in-process over the torch.distributed transport (the Python
+single-step loop) and marks the line ``"degraded": true`` with the error text. ``--python`` runs the in-process Python ``Solver`` path directly.
 ``--cpu`` drives the same orchestration with the native CPU ranks (the contract test without a GPU).
 """
 from __future__ import annotations
@@ -83,6 +86,8 @@ def _args(argv=None):
                     help="native ranks without an RCCL communicator (push / sdma only; host collectives through files)")
     ap.add_argument("--autotune-sdma", action="store_true",
                     help="several ranks: include the copy-engine candidates in the autotune (opt-in across GPUs)")
+    ap.add_argument("--no-qualify", action="store_true",
+                    help="several ranks: skip the cross-device copy-engine qualification before the autotune")
     ap.add_argument("--timeout", type=float, default=420.0,
                     help="seconds before a native rank is killed (below the driver's 600 s bench limit)")
     ap.add_argument("--out", default="", help="also append the JSON line to this file")
@@ -149,31 +154,127 @@ def _correct(a, finite, steps) -> tuple[bool, str]:
 # ------------------------------------------------------------------------------------------------------------------
 # native runtime (default)
 # ------------------------------------------------------------------------------------------------------------------
-def run_native(a, rank: int, world: int, local: int) -> int:
+def _agree(ok: int, world: int) -> int:
+    if world == 1:
+        return ok
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([ok], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return int(t.item())
+
+
+def _child(a, rank: int, world: int, local: int, args: list[str], tag: str, ranks: int | None = None) -> dict:
+    """One native child per rank (``bin/wave3d`` with ``args``) in a fresh rendezvous; every rank learns whether all
+    succeeded. ``ranks`` = 1: rank 0 runs a one-rank job alone (the others wait). Returns {ok, res (rank 0), tail,
+    rc, why}."""
     import torch.distributed as dist
 
     from mpi_cuda_amd.parallel.rccl import broadcast_bytes
 
-    if not os.path.exists(CLI):
-        raise SystemExit(f"bench: native runtime {CLI} is missing (python tools/build.py)")
     nonce = uuid.uuid4().hex.encode() if rank == 0 else None
     if world > 1:
         nonce = broadcast_bytes(nonce, 0)
     nonce = nonce.decode()
+    jw = world if ranks is None else ranks
+    runs = rank < jw
     tmp = tempfile.gettempdir()
     rdzv = os.path.join(tmp, f"wave3d-bench-{nonce}.uid")
     abort_flag = os.path.join(tmp, f"wave3d-bench-{nonce}.abort")
     out_json = os.path.join(tmp, f"wave3d-bench-{nonce}.rank{rank}.json")
     log_path = os.path.join(tmp, f"wave3d-bench-{nonce}.rank{rank}.log")
+    rc, why, tail = 0, "", ""
+    if runs:
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(jw), LOCAL_RANK=str(local), W3D_RDZV_FILE=rdzv,
+                   W3D_JOB_ID=f"bench{nonce}", W3D_TIMEOUT_S=os.environ.get("W3D_TIMEOUT_S", "180"))
+        if a.share_gpus:
+            env["W3D_SHARE_GPUS"] = "1"
+            if jw > 1 and _distinct_gpus(jw) < jw and a.native_transport == "push":
+                env["W3D_CU_SPLIT"] = "auto"  # concurrent ranks on one GPU: disjoint CU ranges (in-kernel push waits)
+        # fault injection (tests): the main run; W3D_BENCH_FAIL_FALLBACK=1 also the conservative retry
+        fail_rank = os.environ.get("W3D_BENCH_FAIL_SETUP_RANK")
+        if fail_rank is not None and (tag == "main" or (tag == "fallback" and os.environ.get("W3D_BENCH_FAIL_FALLBACK"))):
+            env["W3D_FAULT_RANK"] = fail_rank
+        t0 = time.perf_counter()
+        with open(log_path, "w") as log:
+            p = subprocess.Popen([CLI, *args, "--json", out_json], env=env, stdout=log, stderr=subprocess.STDOUT)
+            rc = None
+            while rc is None:
+                try:
+                    rc = p.wait(timeout=0.2)
+                except subprocess.TimeoutExpired:
+                    if os.path.exists(abort_flag):
+                        why = "a peer rank failed"
+                    elif time.perf_counter() - t0 > a.timeout:
+                        why = f"timed out after {a.timeout:.0f} s"
+                    else:
+                        continue
+                    p.kill()
+                    rc = p.wait()
+        if rc != 0:
+            open(abort_flag, "w").close()  # peers stop their children instead of waiting in a collective
+        with open(log_path) as f:
+            tail = f.read()[-2000:]
+    ok = _agree(1 if rc == 0 else 0, world)
+    res = None
+    if ok and rank == 0:
+        with open(out_json) as f:
+            res = json.load(f)
+    for path in (out_json, log_path):
+        if os.path.exists(path):
+            os.remove(path)
+    if world > 1:
+        dist.barrier()
+        if rank == 0 and os.path.exists(abort_flag):
+            os.remove(abort_flag)
+    err = (tail.strip().splitlines()[-1] if tail.strip() else f"exit {rc}") if rc != 0 else ""
+    return {"ok": bool(ok), "res": res, "tail": tail, "rc": rc, "why": why, "err": err}
+
+
+def _qualify_sdma(a, rank: int, world: int, local: int) -> tuple[bool, str]:
+    """Cross-device copy-engine qualification before the autotune may time the SDMA schedules: a short 64³ solve over
+    all ranks with the copy-engine transport, whose error log must equal a one-rank solve's (L∞ exactly, Σe² within
+    1e-12: the max is order-free, the sum's grouping follows the decomposition). Both run in fresh children."""
+    small = ["64", "0.001", "20", "1", "--quiet", "--warmup", "1", "--repeat", "1"]
+    ref = _child(a, rank, world, local, small, "qualify-ref", ranks=1)
+    got = _child(a, rank, world, local, small + ["--transport", "sdma", "--no-autotune", "--decomp", "slab",
+                                                  "--temporal", "4"], "qualify")
+    verdict = b"0"
+    why = ""
+    if rank == 0:
+        if not ref["ok"] or not got["ok"]:
+            why = f"qualification child failed: {(got if ref['ok'] else ref)['err']}"
+        else:
+            r, g = ref["res"]["steps"], got["res"]["steps"]
+            same = len(r) == len(g) and all(x[0] == y[0] and x[1] == y[1] and abs(x[2] - y[2]) <= 1e-12 * abs(x[2])
+                                            for x, y in zip(r, g))
+            why = "copy-engine 64^3 log equals the one-rank log" if same else "copy-engine 64^3 log differs"
+            verdict = b"1" if same else b"0"
+    if world > 1:
+        from mpi_cuda_amd.parallel.rccl import broadcast_bytes
+
+        verdict = broadcast_bytes(verdict, 0)
+        why = broadcast_bytes(why.encode(), 0).decode()
+    return verdict == b"1", why
+
+
+def run_native(a, rank: int, world: int, local: int) -> int:
+    if not os.path.exists(CLI):
+        raise SystemExit(f"bench: native runtime {CLI} is missing (python tools/build.py)")
     multi = world > 1
     warm = max(a.warmup, 2 if multi else 1)
-    if a.native_transport == "sdma" or a.autotune_sdma:
+    temporal = 1 if a.no_temporal else a.temporal
+    sdma_ok, sdma_why = False, ""
+    if multi and not a.cpu and not a.no_rccl and not a.no_autotune and not a.no_qualify:
+        sdma_ok, sdma_why = _qualify_sdma(a, rank, world, local)
+    autotune_sdma = a.autotune_sdma or sdma_ok
+    if a.native_transport == "sdma" or autotune_sdma:
         # copy-engine runs: one 9-12 ms solve among the first 2-7 of every run, never later (profiles/r4/sdma_streams.md)
         warm = max(warm, 8)
-    temporal = 1 if a.no_temporal else a.temporal
-    cmd = [CLI, str(a.N), repr(a.tau), str(a.K), repr(a.L), "--quiet", "--json", out_json,
-           "--warmup", str(warm - 1), "--repeat", "1", "--bench-steps", str(a.steps),
-           "--decomp", a.decomp, "--temporal", str(temporal)]
+    base = [str(a.N), repr(a.tau), str(a.K), repr(a.L), "--quiet", "--warmup", str(warm - 1), "--repeat", "1",
+            "--bench-steps", str(a.steps)]
+    cmd = base + ["--decomp", a.decomp, "--temporal", str(temporal)]
     if a.cpu:
         cmd.append("--cpu")
     else:
@@ -183,7 +284,7 @@ def run_native(a, rank: int, world: int, local: int) -> int:
             cmd.append("--no-rccl")
         if (multi or a.autotune) and not a.no_autotune and not a.no_rccl:
             cmd.append("--autotune")
-            if a.autotune_sdma:
+            if autotune_sdma:
                 cmd.append("--autotune-sdma")
         if not a.no_phases:
             cmd.append("--phases")
@@ -191,61 +292,40 @@ def run_native(a, rank: int, world: int, local: int) -> int:
             cmd.append("--no-overlap")
         if a.no_graph:
             cmd.append("--no-graph")
-    env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(local), W3D_RDZV_FILE=rdzv,
-               W3D_JOB_ID=f"bench{nonce}", W3D_TIMEOUT_S=os.environ.get("W3D_TIMEOUT_S", "180"))
-    if a.share_gpus:
-        env["W3D_SHARE_GPUS"] = "1"
-        if multi and _distinct_gpus(world) < world and a.native_transport == "push":
-            env["W3D_CU_SPLIT"] = "auto"  # concurrent ranks on one GPU: disjoint CU ranges (in-kernel push waits)
-    fail_rank = os.environ.get("W3D_BENCH_FAIL_SETUP_RANK")  # fault injection (tests)
-    if fail_rank is not None:
-        env["W3D_FAULT_RANK"] = fail_rank
     t0 = time.perf_counter()
-    with open(log_path, "w") as log:
-        p = subprocess.Popen(cmd, env=env, stdout=log, stderr=subprocess.STDOUT)
-        rc, why = None, ""
-        while rc is None:
-            try:
-                rc = p.wait(timeout=0.2)
-            except subprocess.TimeoutExpired:
-                if os.path.exists(abort_flag):
-                    why = "a peer rank failed"
-                elif time.perf_counter() - t0 > a.timeout:
-                    why = f"timed out after {a.timeout:.0f} s"
-                else:
-                    continue
-                p.kill()
-                rc = p.wait()
-    wall = time.perf_counter() - t0
-    if rc != 0:
-        open(abort_flag, "w").close()  # peers stop their children instead of waiting in a collective
-    with open(log_path) as f:
-        tail = f.read()[-2000:]
-    ok = 1 if rc == 0 else 0
-    if multi:
-        import torch
+    run = _child(a, rank, world, local, cmd, "main")
+    fallback = None
+    if not run["ok"] and multi and not a.no_rccl:
+        # one fresh child with the conservative native schedule (no autotune, RCCL slabs, sequential exchange), so a
+        # first contact with a node that breaks an autotune candidate still yields a labelled scaling point
+        # the failing rank's own message (the others report only that a peer failed)
+        errs = [run["err"]]
+        if world > 1:
+            import torch.distributed as dist
 
-        t = torch.tensor([ok], dtype=torch.int64)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        ok = int(t.item())
-    res = None
-    if ok and rank == 0:
-        with open(out_json) as f:
-            res = json.load(f)
-    for path in (out_json, log_path):
-        if os.path.exists(path):
-            os.remove(path)
-    if not ok:
-        err = tail.strip().splitlines()[-1] if tail.strip() else f"exit {rc}"
-        if rc != 0:
-            print(f"[bench rank {rank}] native runtime failed (rc={rc}{', ' + why if why else ''}): {err}\n{tail}",
+            errs = [None] * world
+            dist.all_gather_object(errs, run["err"])
+        own = [e for e in errs if e and "another rank" not in e and "peer" not in e]
+        first = (own or [e for e in errs if e] or ["unknown failure"])[0]
+        if rank == 0:
+            print(f"[bench] native run failed ({first}); retrying once with the conservative schedule",
                   file=sys.stderr, flush=True)
-        if multi:
-            dist.barrier()
-            if rank == 0 and os.path.exists(abort_flag):
-                os.remove(abort_flag)
+        safe = base + ["--decomp", "slab", "--temporal", "4", "--no-overlap"]
+        if a.cpu:
+            safe.append("--cpu")
+        elif not a.no_phases:
+            safe.append("--phases")
+        run = _child(a, rank, world, local, safe, "fallback")
+        fallback = {"schedule": "slab-S4-seq, no autotune" + ("" if a.cpu else ", rccl"), "first_failure": first}
+    wall = time.perf_counter() - t0
+    res, tail = run["res"], run["tail"]
+    if not run["ok"]:
+        if run["rc"] != 0:
+            why = run["why"]
+            print(f"[bench rank {rank}] native runtime failed (rc={run['rc']}{', ' + why if why else ''}): "
+                  f"{run['err']}\n{tail}", file=sys.stderr, flush=True)
         if a.allow_fallback and not a.cpu:
-            return run_python(a, rank, world, local, degraded=f"native runtime failed: {err}")
+            return run_python(a, rank, world, local, degraded=f"native runtime failed: {run['err']}")
         return 1
     if rank == 0:
         bench_s = float(res["bench_s"])
@@ -277,7 +357,10 @@ def run_native(a, rank: int, world: int, local: int) -> int:
         }
         extra = {
             "wall_clock_s": round(ms / 1e3, 6),
-            "best_solve_s": round(float(res.get("solve_s", 0.0)), 6),
+            # the timed block: K solves enqueued back to back (one graph replay each), one sync at the end
+            "batched_ms": round(ms, 4),
+            # the fastest warmup / repeat solve timed on its own (host round trip per solve): a different measurement
+            "sync_each_best_ms": round(float(res.get("solve_s", 0.0)) * 1e3, 4),
             "baseline_wall_clock_s": {1: 0.752, 2: 0.505}.get(world),
             "final_max_err": final_linf,
             "final_rms_err": final_rms,
@@ -292,6 +375,12 @@ def run_native(a, rank: int, world: int, local: int) -> int:
             "phases_ms": res.get("phases_ms"),
             "distinct_gpus": None if a.cpu else _distinct_gpus(world),
         }
+        if fallback is not None:
+            extra["fallback_schedule"] = fallback["schedule"]
+            extra["first_failure"] = fallback["first_failure"]
+        if multi and not a.cpu:
+            extra["sdma_qualified"] = sdma_ok
+            extra["sdma_qualification"] = sdma_why or ("skipped" if a.no_qualify or a.no_autotune else None)
         if not a.cpu and multi and extra["distinct_gpus"] < world:
             extra["rehearsal"] = f"{world} ranks sharing {extra['distinct_gpus']} GPU(s): not a scaling point"
         _emit(a, _line(a, world, value, ms, cfg, extra))

@@ -153,7 +153,7 @@ def test_bench_setup_failure_stops_every_rank(gpu, tmp_path):
     import time
 
     out = tmp_path / "b.jsonl"
-    env = dict(os.environ, W3D_TIMEOUT_S="60", W3D_BENCH_FAIL_SETUP_RANK="1")
+    env = dict(os.environ, W3D_TIMEOUT_S="60", W3D_BENCH_FAIL_SETUP_RANK="1", W3D_BENCH_FAIL_FALLBACK="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
            "--master-port", str(29300 + os.getpid() % 200), os.path.join(ROOT, "bench.py"), "--gpus", "2",
            "--share-gpus", "--no-rccl", "--native-transport", "push", "--steps", "3", "--warmup", "2",

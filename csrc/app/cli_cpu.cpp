@@ -37,11 +37,12 @@ int run_cpu(const Args& a) {
       return "{\"error\": " + jstr("unknown command: " + cmd) + "}";
     });
   }
-  CpuResult r;
+  CpuResult r, rb;  // rb: the best solve (its phases are printed)
   double best = 1e30, sum = 0;
   for (int i = 0; i < a.warmup + a.repeat; ++i) {
     r = s.run();
     if (i >= a.warmup) {
+      if (r.solve_s < best) rb = r;
       best = std::min(best, r.solve_s);
       sum += r.solve_s;
     }
@@ -54,16 +55,23 @@ int run_cpu(const Args& a) {
   }
   if (!a.quiet) print_errors(r.steps, r.max_err, r.rms_err, a.prob.tau);
   const double gcell = a.prob.cell_updates() / best / 1e9;
-  std::printf("Total time: %.6f s (init %.6f s, compute %.6f s), threads %d, %.3f GCell/s\n", best, r.init_s,
-              r.compute_s, cpu_max_threads(), gcell);
+  std::printf("Total time: %.6f s (init %.6f s, compute %.6f s), threads %d, %.3f GCell/s\n", best, rb.init_s,
+              rb.compute_s, cpu_max_threads(), gcell);
+  // the reference's CPU phase columns (report.pdf p.16): one process has no halo (Dirichlet zeros are structural)
+  std::printf("Phases (s): init %.6f | compute %.6f | boundary %.6f | exchange %.6f\n", rb.init_s, rb.compute_s,
+              rb.boundary_s, rb.exchange_s);
   if (!a.json.empty()) {
     std::ofstream j(a.json);
     j << "{\"backend\": \"cpu\", \"N\": " << a.prob.N << ", \"tau\": " << jnum(a.prob.tau) << ", \"K\": "
       << a.prob.K << ", \"L\": " << jnum(a.prob.L) << ", \"ranks\": 1, \"dims\": [1, 1, 1], \"threads\": "
       << cpu_max_threads() << ", \"solve_s\": " << jnum(best) << ", \"mean_s\": " << jnum(sum / a.repeat)
       << ", \"gcell_per_s\": " << jnum(gcell) << ", \"schedule\": \"cpu-openmp\", \"bench_steps\": " << a.bench_steps
-      << ", \"bench_s\": " << jnum(bench_s) << ", \"finite\": " << (r.finite ? "true" : "false") << ", \"steps\": "
-      << steps_json(r.steps, r.max_err, r.rms_err) << "}\n";
+      << ", \"bench_s\": " << jnum(bench_s) << ", \"finite\": " << (r.finite ? "true" : "false")
+      << ", \"phases_s\": {\"init\": " << jnum(rb.init_s) << ", \"compute\": " << jnum(rb.compute_s)
+      << ", \"boundary\": " << jnum(rb.boundary_s) << ", \"exchange\": " << jnum(rb.exchange_s) << "}"
+      << ", \"phases_slowest_rank_s\": {\"init\": " << jnum(rb.init_s) << ", \"compute\": " << jnum(rb.compute_s)
+      << ", \"boundary\": 0, \"exchange\": 0}"
+      << ", \"steps\": " << steps_json(r.steps, r.max_err, r.rms_err) << "}\n";
   }
   if (!a.dump.empty()) write_dump(a.dump, a.prob, s.layout(), s.field(0), 0, 1, Dims{1, 1, 1});
   if (!a.checkpoint.empty())
@@ -78,16 +86,17 @@ int run_cpu_rank(const Args& a, ShmGroup& g, int rank) {
     CpuRankSolver s(a.prob, g, rank, a.check_every, a.threads);
     // fault injection: W3D_FAULT_RANK=r makes rank r fail before its first exchange
     if (const char* fr = std::getenv("W3D_FAULT_RANK"); fr && std::atoi(fr) == rank) fail("injected fault");
-    CpuResult r;
-    double best = 1e30, sum = 0, exch = 0;
+    CpuResult r, rb;  // rb: the best solve (its phases, each the max over ranks, are printed)
+    double best = 1e30, sum = 0;
     for (int i = 0; i < a.warmup + a.repeat; ++i) {
       r = s.run();
       if (i >= a.warmup) {
-        if (r.solve_s < best) exch = s.exchange_s();
+        if (r.solve_s < best) rb = r;
         best = std::min(best, r.solve_s);
         sum += r.solve_s;
       }
     }
+    const double exch = rb.exchange_s;
     double bench_s = 0.0;  // the end barrier waits for the slowest rank: rank 0's interval is the max over ranks
     if (a.bench_steps > 0) {
       g.barrier();
@@ -102,6 +111,10 @@ int run_cpu_rank(const Args& a, ShmGroup& g, int rank) {
       const double gcell = a.prob.cell_updates() / best / 1e9;
       std::printf("Total time: %.6f s (max over %d ranks, decomp %dx%dx%d; exchange %.6f s), threads %d per rank, "
                   "%.3f GCell/s\n", best, g.world(), d.px, d.py, d.pz, exch, cpu_max_threads(), gcell);
+      std::printf("Phases (s, max over ranks): init %.6f | compute %.6f | boundary %.6f | exchange %.6f\n", rb.init_s,
+                  rb.compute_s, rb.boundary_s, rb.exchange_s);
+      std::printf("Phases (s, slowest rank): init %.6f | compute %.6f | boundary %.6f | exchange %.6f\n",
+                  rb.slow_phases[0], rb.slow_phases[1], rb.slow_phases[2], rb.slow_phases[3]);
       if (!a.json.empty()) {
         std::ofstream j(a.json);
         j << "{\"backend\": \"cpu\", \"ranks\": " << g.world() << ", \"dims\": [" << d.px << ", " << d.py << ", "
@@ -111,8 +124,13 @@ int run_cpu_rank(const Args& a, ShmGroup& g, int rank) {
           << ", \"final_max_err\": " << (r.max_err.empty() ? 0.0 : r.max_err.back())
           << ", \"final_rms_err\": " << (r.rms_err.empty() ? 0.0 : r.rms_err.back())
           << ", \"schedule\": \"cpu-openmp-ranks\", \"bench_steps\": " << a.bench_steps << ", \"bench_s\": "
-          << jnum(bench_s) << ", \"finite\": " << (r.finite ? "true" : "false") << ", \"steps\": "
-          << steps_json(r.steps, r.max_err, r.rms_err) << "}\n";
+          << jnum(bench_s) << ", \"finite\": " << (r.finite ? "true" : "false")
+          << ", \"phases_s\": {\"init\": " << jnum(rb.init_s) << ", \"compute\": " << jnum(rb.compute_s)
+          << ", \"boundary\": " << jnum(rb.boundary_s) << ", \"exchange\": " << jnum(rb.exchange_s) << "}"
+          << ", \"phases_slowest_rank_s\": {\"init\": " << jnum(rb.slow_phases[0]) << ", \"compute\": "
+          << jnum(rb.slow_phases[1]) << ", \"boundary\": " << jnum(rb.slow_phases[2]) << ", \"exchange\": "
+          << jnum(rb.slow_phases[3]) << "}"
+          << ", \"steps\": " << steps_json(r.steps, r.max_err, r.rms_err) << "}\n";
       }
     }
     if (!a.dump.empty()) write_dump(a.dump, a.prob, s.layout(), s.field(0), rank, g.world(), d);

@@ -92,6 +92,12 @@ struct CpuResult {
   std::vector<int> steps;
   std::vector<double> max_err, rms_err;
   double solve_s = 0.0, init_s = 0.0, compute_s = 0.0, check_s = 0.0;
+  // the reference's CPU phase columns (report.pdf p.16): boundary = halo faces packed / unpacked,
+  // exchange = waiting for the neighbours (and the final error reduction); ranks: each the max over ranks
+  double boundary_s = 0.0, exchange_s = 0.0;
+  // the slowest rank's own init / compute / boundary / exchange (they add up to its solve time; the per-phase maxima
+  // above come from different ranks and overlap in time)
+  double slow_phases[4] = {0.0, 0.0, 0.0, 0.0};
   bool finite = true;
 };
 

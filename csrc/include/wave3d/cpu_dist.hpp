@@ -85,7 +85,7 @@ class CpuRankSolver {
   std::vector<double> u_[2];
   std::vector<double> s_;
   int final_ = 1;
-  double exchange_s_ = 0.0;
+  double exchange_s_ = 0.0, boundary_s_ = 0.0;
 };
 
 }  // namespace wave3d

@@ -185,12 +185,18 @@ std::vector<int> CpuRankSolver::check_steps() const {
 // again before the outboxes may be overwritten (the MPI_Sendrecv of the reference's exchange, report.pdf p.16).
 void CpuRankSolver::exchange(double* u) {
   if (!plan_.any()) return;
+  const double t0 = now_s();
   for (size_t f = 0; f < plan_.faces.size(); ++f)
     cpu_pack_face(lay_, plan_.faces[f], u, g_.outbox(rank_, static_cast<int>(f)));
+  const double t1 = now_s();
   g_.barrier();
+  const double t2 = now_s();
   for (size_t f = 0; f < plan_.faces.size(); ++f)
     cpu_unpack_face(lay_, plan_.faces[f], g_.outbox(plan_.faces[f].peer, peer_face_[f]), u);
+  const double t3 = now_s();
   g_.barrier();
+  boundary_s_ += (t1 - t0) + (t3 - t2);  // face packing ("boundary processing")
+  exchange_s_ += (t2 - t1) + (now_s() - t3);  // waiting for the neighbours
 }
 
 CpuResult CpuRankSolver::run() {
@@ -203,7 +209,7 @@ CpuResult CpuRankSolver::run() {
   for (int n : check_steps()) is_check[static_cast<size_t>(n)] = 1;
   double* mine = g_.slot(rank_);
   for (size_t q = 0; q < 2 * static_cast<size_t>(K + 1); ++q) mine[q] = 0.0;
-  exchange_s_ = 0.0;
+  exchange_s_ = boundary_s_ = 0.0;
   g_.barrier();
   const double t0 = now_s();
   cpu_init_first(lay_, c, s, u_[0].data(), u_[1].data());  // ghosts analytic: no exchange before step 2
@@ -220,11 +226,7 @@ CpuResult CpuRankSolver::run() {
   }
   int cur = 1, old = 0;
   for (int n = 1; n <= K - 1; ++n) {
-    if (n > 1) {
-      const double te = now_s();
-      exchange(u_[cur].data());
-      exchange_s_ += now_s() - te;
-    }
+    if (n > 1) exchange(u_[cur].data());
     const double tc = now_s();
     if (is_check[static_cast<size_t>(n + 1)]) {
       ErrAcc a;
@@ -240,6 +242,9 @@ CpuResult CpuRankSolver::run() {
   const size_t tslot = 2 * static_cast<size_t>(K + 1);
   mine[tslot] = now_s() - t0;
   mine[tslot + 1] = exchange_s_;
+  mine[tslot + 2] = boundary_s_;
+  mine[tslot + 3] = r.init_s;
+  mine[tslot + 4] = r.compute_s;
   g_.barrier();  // every rank's partials and timers are in its slot
   const double n_int = static_cast<double>(prob_.N - 1);
   const double denom = n_int * n_int * n_int;
@@ -256,10 +261,22 @@ CpuResult CpuRankSolver::run() {
     if (!std::isfinite(m) || !std::isfinite(sum)) r.finite = false;
   }
   r.solve_s = 0.0;
-  for (int q = 0; q < g_.world(); ++q) {  // the reference reports the slowest rank (max over ranks)
-    r.solve_s = std::max(r.solve_s, g_.slot(q)[tslot]);
-    exchange_s_ = std::max(exchange_s_, g_.slot(q)[tslot + 1]);
+  for (int q = 0; q < g_.world(); ++q) {  // the reference reports the slowest rank (max over ranks), per phase too
+    const double* v = g_.slot(q);
+    if (v[tslot] >= r.solve_s) {
+      r.slow_phases[0] = v[tslot + 3];
+      r.slow_phases[1] = v[tslot + 4];
+      r.slow_phases[2] = v[tslot + 2];
+      r.slow_phases[3] = v[tslot + 1];
+    }
+    r.solve_s = std::max(r.solve_s, v[tslot]);
+    exchange_s_ = std::max(exchange_s_, v[tslot + 1]);
+    boundary_s_ = std::max(boundary_s_, v[tslot + 2]);
+    r.init_s = std::max(r.init_s, v[tslot + 3]);
+    r.compute_s = std::max(r.compute_s, v[tslot + 4]);
   }
+  r.exchange_s = exchange_s_;
+  r.boundary_s = boundary_s_;
   g_.barrier();  // the slots may be reused by the next run
   return r;
 }

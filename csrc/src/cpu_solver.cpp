@@ -104,6 +104,8 @@ CpuResult CpuSolver::run() {
   }
   final_ = cur;
   r.solve_s = now_s() - t0;
+  r.slow_phases[0] = r.init_s;
+  r.slow_phases[1] = r.compute_s;
   return r;
 }
 

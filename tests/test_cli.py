@@ -88,6 +88,29 @@ def test_cpu_multiprocess_bitexact(tmp_path, np_, decomp):
     assert np.array_equal(got, full)
 
 
+@pytest.mark.parametrize("np_", [1, 2, 4])
+def test_cpu_phase_columns(tmp_path, np_):
+    """The reference's CPU phase columns (report.pdf p.16): init / compute / boundary / exchange, each
+    the max over ranks, printed and in --json, plus the slowest rank's own four, which account for its solve (sum
+    within 5 % of the total; maxima of different ranks overlap in time, so their sum may exceed it)."""
+    j = tmp_path / "p.json"
+    args = [64, 0.001, 10, "--cpu", "--threads", 1, "--repeat", 3, "--json", j]
+    if np_ > 1:
+        args += ["--np", np_, "--decomp", "slab"]
+    out = run(*args).stdout
+    assert any(l.startswith("Phases (s") and "boundary" in l and "exchange" in l for l in out.splitlines())
+    rec = json.loads(j.read_text())
+    ph, sl = rec["phases_s"], rec["phases_slowest_rank_s"]
+    assert set(ph) == set(sl) == {"init", "compute", "boundary", "exchange"}
+    assert all(ph[k] >= sl[k] for k in ph)
+    total = sum(sl.values())
+    assert abs(total - rec["solve_s"]) <= 0.05 * rec["solve_s"], (sl, rec["solve_s"])
+    if np_ == 1:
+        assert ph["boundary"] == 0.0 and ph["exchange"] == 0.0
+    else:
+        assert ph["boundary"] > 0.0 and ph["exchange"] > 0.0
+
+
 def test_cpu_multiprocess_rank_failure_is_an_error():
     """Fault injection: one rank fails before its first exchange; the others leave their barriers with an error at
     once (shared failure flag) instead of waiting for the barrier timeout, and the run exits non-zero."""

@@ -78,7 +78,10 @@ int serve(const Args& a, GpuSolver& s, const HostColl& hc, bool file_coll, const
   return serve_loop(g.str(), [&](const std::string& cmd, std::istream& in) -> std::string {
     std::ostringstream o;
     if (cmd == "run") {
-      hc.barrier();
+      if (hc.idle_barrier)
+        hc.idle_barrier();
+      else
+        hc.barrier();
       RunResult r = s.run();
       const double t = hc.max(r.solve_s);
       if (file_coll) combine_logs(r, hc);

@@ -30,7 +30,10 @@ std::string job_segment_name();
 std::string rdzv_path();
 std::string exchange_unique_id(int rank);
 // Every rank's bytes (equal sizes) through files next to the rendezvous file, in rank order.
-std::vector<std::string> file_allgather(int rank, int world, const std::string& mine, const std::string& tag);
+// timeout_s: 0 = W3D_FILE_TIMEOUT_S (default 120 s), < 0 = as long as the parent process lives
+std::vector<std::string> file_allgather(int rank, int world, const std::string& mine, const std::string& tag,
+                                        double timeout_s = 0.0);
+double proc_timeout_s();
 // Fork P ranks before anything touches the GPU (RANK / LOCAL_RANK / WORLD_SIZE / W3D_RDZV_FILE in their env). Returns
 // -1 in a child (continue as that rank), the first non-zero exit status of the children in the parent.
 int spawn_ranks(int np);
@@ -43,6 +46,7 @@ struct HostColl {
   std::function<bool(bool)> agree;
   std::function<double(double)> max;
   std::function<void()> barrier;
+  std::function<void()> idle_barrier;  // (optional) a barrier between requests of the serve loop: no fixed bound
   std::function<std::vector<std::string>(const std::string&)> allgather;
   std::function<void()> cleanup;  // files of a file-based collective (the last one stays: a peer may still read it)
   static HostColl single(int rank = 0);                         // one rank (or a fake rank): identity collectives

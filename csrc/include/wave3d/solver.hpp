@@ -111,6 +111,7 @@ struct RunResult {
   PhaseTimes phases;              // only with SolverOptions::timers
   std::vector<UnitTrace> trace;   // per unit, only with SolverOptions::timers
   bool finite = true;
+  bool batched = false;           // run_batch's pipelined path: solve_s is the batch's wall time / n
 };
 
 // Thin owner of an RCCL communicator.
@@ -156,8 +157,8 @@ class GpuSolver {
   // each followed by the copy of its own error log into its slot of a pinned host buffer, and synchronises once at
   // the end; the CLI then checks every timed solve's log against the warmup solve's. Every solve runs in full. (The
   // host round trip it removes between solves measured within noise of 0 at 512³: profiles/r4/vmcnt/README.md.)
-  // Other solvers (several ranks, copy engines, push, timers, resume, no graph) call run() n times. solve_s of each
-  // result = the batch's wall time / n.
+  // Other solvers (several ranks, copy engines, push, timers, resume, no graph) call run() n times. solve_s: on the
+  // pipelined path the batch's wall time / n (RunResult::batched = true), otherwise each run()'s own time.
   std::vector<RunResult> run_batch(int n);
   // Per-phase event timers for the following run() calls (those launch eagerly; the captured graph is kept for when
   // the timers are switched off again): a phase breakdown of exactly the schedule the graph replays.

@@ -43,6 +43,7 @@ py::dict result_dict(const RunResult& r) {
   d["max_err"] = r.max_err;
   d["rms_err"] = r.rms_err;
   d["solve_s"] = r.solve_s;
+  d["batched"] = r.batched;
   d["finite"] = r.finite;
   py::dict ph;
   ph["init_ms"] = r.phases.init_ms;

@@ -108,11 +108,20 @@ std::string exchange_unique_id(int rank) {
   }
 }
 
-std::vector<std::string> file_allgather(int rank, int world, const std::string& mine, const std::string& tag) {
+double proc_timeout_s() {
+  const char* v = std::getenv("W3D_FILE_TIMEOUT_S");
+  const double t = v ? std::atof(v) : 0.0;
+  return t > 0.0 ? t : 120.0;
+}
+
+std::vector<std::string> file_allgather(int rank, int world, const std::string& mine, const std::string& tag,
+                                        double timeout_s) {
   auto path = [&](int r) { return rdzv_path() + "." + tag + std::to_string(r); };
   publish(path(rank), mine);
   std::vector<std::string> all(static_cast<size_t>(world));
   const double t0 = wall_s();
+  const double bound = timeout_s == 0.0 ? proc_timeout_s() : timeout_s;  // (< 0: while the parent lives)
+  const pid_t parent = getppid();
   for (int r = 0; r < world; ++r) {
     for (;;) {
       if (fresh_file(path(r))) {
@@ -123,7 +132,8 @@ std::vector<std::string> file_allgather(int rank, int world, const std::string& 
         }
       }
       const double waited = wall_s() - t0;
-      if (waited > 120.0) fail("timed out waiting for " + path(r));  // (a peer that died)
+      if (bound > 0.0 && waited > bound) fail("timed out waiting for " + path(r));  // (a peer that died)
+      if (bound < 0.0 && getppid() != parent) fail("the parent process exited while waiting for " + path(r));
       // poll fast first: this is also the per-solve barrier of ranks without a communicator, and a rank leaving it
       // 20 ms after its peer made the peer's solve wait that long for its flags (solve-time mean 3x the best, measured
       // on 2 processes sharing one GPU: profiles/r4/proc_parity.md); back off once a peer is clearly slow
@@ -226,11 +236,12 @@ HostColl HostColl::files(int rank, int world) {
     std::vector<std::string> mine;
   };
   auto st = std::make_shared<State>();
-  auto gather = [st, rank, world](const std::string& b) {
+  auto gather_t = [st, rank, world](const std::string& b, double timeout_s) {
     const std::string tag = "c" + std::to_string(st->n++) + "r";
     st->mine.push_back(rdzv_path() + "." + tag + std::to_string(rank));
-    return file_allgather(rank, world, b, tag);
+    return file_allgather(rank, world, b, tag, timeout_s);
   };
+  auto gather = [gather_t](const std::string& b) { return gather_t(b, 0.0); };
   HostColl h;
   h.rank = rank;
   h.world = world;
@@ -250,6 +261,13 @@ HostColl HostColl::files(int rank, int world) {
     return m;
   };
   h.barrier = [gather] { (void)gather("b"); };
+  // the serve loop's barrier before a solve: the peer ranks' Python callers may spend any time between run()
+  // calls, so it waits as long as this rank's parent lives — or W3D_PROC_TIMEOUT_S if set, the bound the
+  // Python side (NativeRankProcess) puts on every reply (the other file collectives: W3D_FILE_TIMEOUT_S, 120 s)
+  h.idle_barrier = [gather_t] {
+    const char* v = std::getenv("W3D_PROC_TIMEOUT_S");
+    (void)gather_t("b", v && std::atof(v) > 0.0 ? std::atof(v) : -1.0);
+  };
   h.cleanup = [st] {
     for (size_t i = 0; i + 1 < st->mine.size(); ++i) std::remove(st->mine[i].c_str());
   };

@@ -1196,7 +1196,10 @@ RunResult GpuSolver::run() {
     if (ok) ok = hipGraphInstantiate(&gx, g, nullptr, nullptr, 0) == hipSuccess;
     // (upload now rather than at the first replay; the copy-engine runs still show one 9-12 ms solve among their first
     // 2-7 — never later — with or without it: profiles/r4/sdma_streams.md. bench.py warms copy-engine runs up longer)
-    if (ok) ok = hipGraphUpload(gx, s0_) == hipSuccess;
+    if (ok && hipGraphUpload(gx, s0_) != hipSuccess) {
+      (void)hipGraphExecDestroy(gx);  // (instantiated but not uploadable: release it, run eagerly)
+      ok = false;
+    }
     if (g) (void)hipGraphDestroy(g);
     (void)hipGetLastError();
     if (!ok) {
@@ -1242,7 +1245,8 @@ std::vector<RunResult> GpuSolver::run_batch(int n) {
     W3D_HIP(hipMemcpyAsync(hbatch_ + static_cast<size_t>(i) * per, errlog_, per * sizeof(Partial),
                            hipMemcpyDeviceToHost, s0_));
   }
-  wait_stream(s0_, nullptr, gpu_timeout_s());
+  // (the per-solve bound, per replay: a long timed block is not a hang)
+  wait_stream(s0_, nullptr, gpu_timeout_s() * n);
   const double dt = (now_s() - t0) / n;
   xsolves_ += static_cast<unsigned>(n);
   runs_ += n;
@@ -1250,6 +1254,7 @@ std::vector<RunResult> GpuSolver::run_batch(int n) {
     RunResult r;
     decode_log(hbatch_ + static_cast<size_t>(i) * per, 1, r);
     r.solve_s = dt;
+    r.batched = true;
     out.push_back(std::move(r));
   }
   return out;
@@ -1739,7 +1744,11 @@ RunResult GpuGroup::run() {
     if (ok) {
       const hipError_t e = hipGraphInstantiate(&exec_, g, nullptr, nullptr, 0);
       if (dbg) std::fprintf(stderr, "[group] instantiate: %s\n", hipGetErrorString(e));
-      ok = e == hipSuccess && hipGraphUpload(exec_, gs_) == hipSuccess;  // (see GpuSolver::run)
+      ok = e == hipSuccess;
+      if (ok && hipGraphUpload(exec_, gs_) != hipSuccess) {  // (see GpuSolver::run)
+        (void)hipGraphExecDestroy(exec_);
+        ok = false;
+      }
     }
     if (g) (void)hipGraphDestroy(g);
     (void)hipGetLastError();

@@ -118,7 +118,30 @@ class Solver:
             raise ValueError("runtime is 'inproc' (this process) or 'process' (a native bin/wave3d rank process)")
         self.runtime = runtime
         if runtime == "process":
-            self._init_process(device, decomp, temporal, overlap, graph, rccl, autotune, group)
+            # every option the rank process honours becomes its CLI flag; the others raise (none is
+            # dropped silently)
+            flags = []
+            if tiling is not None or tiling2 is not None:
+                raise ValueError("runtime='process' takes no tiling / tiling2 overrides (the rank process uses its "
+                                 "defaults; run in-process to sweep tilings)")
+            tt = dict(tiling_tb or {})
+            for k, flag in (("threads", "--tb-threads"), ("init_threads", "--tb-init-threads")):
+                if k in tt:
+                    flags += [flag, str(int(tt.pop(k)))]
+            if tt:
+                raise ValueError(f"runtime='process' cannot honour tiling_tb keys {sorted(tt)}")
+            if copy_engines and self.transport not in ("sdma", "sdma-ipc"):
+                raise ValueError("runtime='process': copy engines are the 'sdma' transport (transport='sdma')")
+            for on, flag in ((timers, "--timers"), (debug_sync, "--debug-sync"), (poison_ghosts, "--poison-ghosts"),
+                             (not tb, "--no-tb"), (not init2, "--no-init2"), (not fused_pack, "--no-fused-pack")):
+                if on:
+                    flags.append(flag)
+            for val, flag in ((tb_min_planes, "--tb-min-planes"), (deep_min_planes, "--deep-min-planes")):
+                if val is not None:
+                    flags += [flag, str(int(val))]
+            if autotune_rounds != 5:
+                flags += ["--autotune-rounds", str(int(autotune_rounds))]
+            self._init_process(device, decomp, temporal, overlap, graph, rccl, autotune, group, tuple(flags))
             return
         C = load()
         if self.backend == "hip":
@@ -193,7 +216,7 @@ class Solver:
         else:
             self.dims = (1, 1, 1)
 
-    def _init_process(self, device, decomp, temporal, overlap, graph, rccl, autotune, group) -> None:
+    def _init_process(self, device, decomp, temporal, overlap, graph, rccl, autotune, group, flags=()) -> None:
         """runtime="process": this rank's production solver in a ``bin/wave3d --serve`` child (graph-captured under
         the system ROCm runtime, which a torch process cannot do for multi-rank schedules; parallel/native_proc.py).
         Transports: rccl, sdma / sdma-ipc (copy engines), push / push-ipc; one process per rank (torchrun)."""
@@ -216,11 +239,11 @@ class Solver:
                 raise ValueError("runtime='process' with an in-process group has no autotune")
             self._impl = NativeRankProcess(self.spec, 0, 1, device, "rccl", decomp, temporal, overlap, graph, True,
                                            False, None, extra_args=("--group", str(self.world), "--group-transport",
-                                                                    self.transport))
+                                                                    self.transport, *flags))
         else:
             self.transport = {"sdma": "sdma-ipc", "push": "push-ipc"}.get(self.transport, self.transport)
             self._impl = NativeRankProcess(self.spec, self.rank, self.world, device, self.transport, decomp,
-                                           temporal, overlap, graph, rccl, autotune, group)
+                                           temporal, overlap, graph, rccl, autotune, group, extra_args=flags)
         self.dims = tuple(self._impl.info["dims"])
         self.schedule = self._impl.info["schedule"]
         self.autotune_times, self.autotune_rejected = {}, {}

@@ -62,3 +62,18 @@ def test_multirank_dump_assembles(tmp_path):
 
     _, ref, _ = torch_reference_solve(ProblemSpec(N=26, tau=1e-3, K=5), return_fields=True)
     assert np.array_equal(u, ref.numpy())
+
+
+def test_process_runtime_rejects_options_it_cannot_honour():
+    """Solver(runtime='process') forwards the options its rank process honours as CLI flags and raises for
+    the others instead of dropping them silently (checked before any process or GPU is touched)."""
+    import pytest
+
+    from mpi_cuda_amd import ProblemSpec
+    from mpi_cuda_amd.solver import Solver
+
+    spec = ProblemSpec(N=16, tau=1e-3, K=4)
+    for kw in (dict(tiling={"rows": 4}), dict(tiling2={"rows": 2}), dict(tiling_tb={"xcd_blocks": True}),
+               dict(copy_engines=True)):
+        with pytest.raises(ValueError):
+            Solver(spec, backend="hip", transport="rccl", runtime="process", **kw)

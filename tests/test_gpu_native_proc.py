@@ -51,7 +51,12 @@ from mpi_cuda_amd.solver import Solver
 dist.init_process_group("gloo")
 spec = ProblemSpec(N=int(os.environ["N"]), tau=1e-3, K=20)
 s = Solver(spec, backend="hip", transport="sdma", decomp="slab", device=0, rccl=False, runtime="process")
-rs = [s.run() for _ in range(int(os.environ["REPS"]))]
+rs = []
+for i in range(int(os.environ["REPS"])):
+    if i == 1 and dist.get_rank() == 1:  # (a slow caller between run() calls)
+        import time
+        time.sleep(float(os.environ.get("SLEEP", "0")))
+    rs.append(s.run())
 f = s.owned_field(0)
 torch.save({"f": f, "rank": dist.get_rank()}, os.environ["OUT"] + f".{dist.get_rank()}.pt")
 out = {"graph": [r.extra["graph"] for r in rs], "solve_s": [r.solve_s for r in rs], "local_s": [r.extra["local_s"] for r in rs],
@@ -94,6 +99,25 @@ def test_process_runtime_two_ranks_sdma_graph(gpu, tmp_path):
             assert me == pytest.approx(r1.max_err, rel=1e-12) and re_ == pytest.approx(r1.rms_err, rel=1e-9)
         hashes += m["hash"]
     assert hashes % (1 << 64) == ref.field_hash(0)
+
+
+def test_process_runtime_serve_barrier_waits_for_a_slow_caller(gpu, tmp_path):
+    """the serve loop's barrier before a solve (file collectives, no RCCL) waits as long as the rank's parent
+    lives, not a fixed bound: with the file collectives bounded at 2 s (W3D_FILE_TIMEOUT_S), rank 1's caller sleeps
+    5 s between run() calls and both ranks still finish."""
+    script = tmp_path / "w.py"
+    script.write_text(_WORKER)
+    env = dict(os.environ, ROOT=ROOT, OUT=str(tmp_path / "res"), N="48", REPS="3", W3D_TIMEOUT_S="30",
+               W3D_FILE_TIMEOUT_S="2", SLEEP="5")
+    env.pop("W3D_RDZV_FILE", None)
+    env.pop("W3D_PROC_TIMEOUT_S", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(29450 + os.getpid() % 150), str(script)]
+    p = subprocess.run(cmd, env=env, timeout=240, capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr[-3000:]
+    for rank in range(2):
+        m = json.loads((tmp_path / f"res.{rank}.json").read_text())
+        assert len(m["max_err"]) == 3
 
 
 @pytest.mark.parametrize("transport,decomp,graph", [("rccl-self", "slab", True), ("loopback", "2x2x1", True),

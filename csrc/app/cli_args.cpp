@@ -61,6 +61,8 @@ constexpr Personality kPersonalities[] = {
                "  --debug-sync       synchronize after every step (race triage)\n"
                "  --poison-ghosts    NaN-fill ghost layers before every exchange (missed-halo detector)\n"
                "  --fake-rank R/P    perf study: time rank R of a P-rank decomposition alone on one GPU, no transport\n"
+               "  --fake-traffic     with --fake-rank: every exchange sends and receives the rank's exact messages to\n"
+               "                     itself over a one-rank RCCL communicator (real RCCL kernels and bytes; values wrong)\n"
                "  --group P          all P ranks of the decomposition in this process on one GPU (rehearsal of the\n"
                "                     multi-rank path; --group-transport rccl-self (default: RCCL send/recv, each rank\n"
                "                     over a one-rank communicator), loopback (device copies) or push)\n"
@@ -148,6 +150,7 @@ Args parse(int argc, char** argv) {
       a.fake_rank = std::stoi(v.substr(0, v.find('/')));
       a.fake_world = std::stoi(v.substr(v.find('/') + 1));
     }
+    else if (s == "--fake-traffic") a.fake_traffic = true;
     else if (s == "--group") a.group = std::stoi(next());
     else if (s == "--bench-steps") a.bench_steps = std::stoi(next());
     else if (s == "--autotune") a.autotune = true;
@@ -306,6 +309,7 @@ SolverOptions options_from(const Args& a, bool fake) {
   if (a.tb_init_threads > 0) o.tiling_tb.init_threads = a.tb_init_threads;
   o.init2 = a.init2;
   o.fake_comm = fake;
+  o.fake_traffic = fake && a.fake_traffic;
   W3D_REQUIRE(a.transport == "rccl" || a.transport == "push" || a.transport == "sdma",
               "--transport must be rccl, push or sdma, not " + a.transport);
   o.push = a.transport == "push";

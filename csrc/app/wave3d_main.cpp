@@ -215,7 +215,9 @@ int run_gpu(const Args& a) {
 
   std::shared_ptr<Comm> comm;
   const double t_comm0 = wall_s();
-  if (world > 1 && !fake && !a.no_rccl) {
+  if (fake && a.fake_traffic) {  // a one-rank communicator for the fake rank's self traffic (--fake-traffic)
+    comm = std::make_shared<Comm>(0, 1, Comm::make_unique_id());
+  } else if (world > 1 && !fake && !a.no_rccl) {
     W3D_REQUIRE(local < ndev || std::getenv("W3D_SHARE_GPUS"),
                 "rank " + std::to_string(rank) + " has local rank " + std::to_string(local) + " but only " +
                     std::to_string(ndev) + " GPU(s) are visible (RCCL needs one GPU per rank)");
@@ -232,7 +234,9 @@ int run_gpu(const Args& a) {
   // host collectives: RCCL; files for ranks without a communicator (--no-rccl rehearsal, outside timed regions); none
   // for one rank or a fake rank
   const bool file_coll = !comm && world > 1 && !fake;
-  const HostColl hc = comm ? HostColl::rccl(comm) : file_coll ? HostColl::files(rank, world) : HostColl::single(rank);
+  const HostColl hc = comm && !fake ? HostColl::rccl(comm)
+                      : file_coll       ? HostColl::files(rank, world)
+                                        : HostColl::single(rank);
   W3D_REQUIRE(!a.no_rccl || world == 1 || fake || ((a.transport == "push" || a.transport == "sdma") && !a.autotune),
               "--no-rccl: ranks without a communicator can only run the push or sdma transport (no autotune)");
   std::unique_ptr<GpuSolver> s;

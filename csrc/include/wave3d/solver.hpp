@@ -39,6 +39,8 @@ struct SolverOptions {
   bool debug_sync = false;      // hipDeviceSynchronize after every step (race triage; disables the graph)
   bool poison_ghosts = false;   // NaN-fill ghost layers before each exchange (a missed halo poisons the errors)
   bool fake_comm = false;       // perf study only: run rank `rank` of `world` alone, exchanges replaced by no-ops
+  bool fake_traffic = false;    // ... unless set: the exact message set goes to itself over a one-rank communicator
+                                // (RCCL copy kernels and bytes next to the passes; the received values are its own)
   LeapfrogTiling tiling;
   // Temporal blocking: up to `temporal` (2..5) steps per HBM pass wherever no halo exchange intervenes. One rank:
   // k_leapfrog_p2 passes (pair-tiled, S ≤ 5; all levels in LDS, error checks at any level), the steps split into

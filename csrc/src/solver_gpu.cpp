@@ -472,7 +472,7 @@ std::string GpuSolver::transport() const {
   if (world_ == 1) return "none";
   if (sdma_) return "sdma";
   if (push_) return "push";
-  if (opt_.fake_comm) return "fake";
+  if (opt_.fake_comm) return opt_.fake_traffic && comm_ ? "fake-rccl-self" : "fake";
   if (loopback_) return comm_ ? "rccl-self" : "loopback";
   return "rccl";
 }
@@ -804,7 +804,17 @@ void GpuSolver::unpack_halo(hipStream_t st) {
 void GpuSolver::exchange(hipStream_t st, const std::vector<GpuSolver*>* pull) {
   const bool packed = packs();
   if (packed && !pull) pack_halo(st);  // (group: each rank packed its own faces)
-  if (!opt_.fake_comm) {  // fake_comm (perf study): one rank's schedule timed alone, ghosts keep stale values
+  if (opt_.fake_comm && opt_.fake_traffic && comm_) {
+    // perf study: the rank's real message set, sent to and received from itself over a
+    // one-rank communicator — RCCL's copy kernels, CU and LDS use and bytes as in the real exchange
+    ncclComm_t c = static_cast<ncclComm_t>(comm_->raw());
+    W3D_NCCL(ncclGroupStart());
+    for (const Msg& m : msgs_) {
+      W3D_NCCL(ncclSend(m.send, static_cast<size_t>(m.count), ncclFloat64, 0, c, st));
+      W3D_NCCL(ncclRecv(m.recv, static_cast<size_t>(m.count), ncclFloat64, 0, c, st));
+    }
+    W3D_NCCL(ncclGroupEnd());
+  } else if (!opt_.fake_comm) {  // fake_comm (perf study): one rank's schedule timed alone, ghosts keep stale values
     ncclComm_t c = static_cast<ncclComm_t>(comm_->raw());
     W3D_NCCL(ncclGroupStart());
     for (const Msg& m : msgs_) {
@@ -1127,7 +1137,7 @@ void GpuSolver::gather_errors(RunResult& r) {
   std::vector<Partial> host(per * static_cast<size_t>(world_));
   cur_unit_ = -1;
   timed(kPhaseGather, s0_, [&] {
-    if (world_ > 1 && comm_) {
+    if (world_ > 1 && comm_ && !opt_.fake_comm) {  // (a fake rank's communicator is its own one-rank one)
       W3D_NCCL(ncclAllGather(errlog_, errall_, 2 * per, ncclFloat64, static_cast<ncclComm_t>(comm_->raw()), s0_));
       W3D_HIP(hipMemcpyAsync(host.data(), errall_, host.size() * sizeof(Partial), hipMemcpyDeviceToHost, s0_));
     } else {

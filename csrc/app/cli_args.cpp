@@ -63,6 +63,7 @@ constexpr Personality kPersonalities[] = {
                "  --fake-rank R/P    perf study: time rank R of a P-rank decomposition alone on one GPU, no transport\n"
                "  --fake-traffic     with --fake-rank: every exchange sends and receives the rank's exact messages to\n"
                "                     itself over a one-rank RCCL communicator (real RCCL kernels and bytes; values wrong)\n"
+               "  --reserve-cus N    keep N CUs (a multiple of 8: N/8 per XCD) off the passes for RCCL's copy kernels\n"
                "  --group P          all P ranks of the decomposition in this process on one GPU (rehearsal of the\n"
                "                     multi-rank path; --group-transport rccl-self (default: RCCL send/recv, each rank\n"
                "                     over a one-rank communicator), loopback (device copies) or push)\n"
@@ -151,6 +152,7 @@ Args parse(int argc, char** argv) {
       a.fake_world = std::stoi(v.substr(v.find('/') + 1));
     }
     else if (s == "--fake-traffic") a.fake_traffic = true;
+    else if (s == "--reserve-cus") a.reserve_cus = std::stoi(next());
     else if (s == "--group") a.group = std::stoi(next());
     else if (s == "--bench-steps") a.bench_steps = std::stoi(next());
     else if (s == "--autotune") a.autotune = true;
@@ -310,6 +312,7 @@ SolverOptions options_from(const Args& a, bool fake) {
   o.init2 = a.init2;
   o.fake_comm = fake;
   o.fake_traffic = fake && a.fake_traffic;
+  o.reserve_cus = a.reserve_cus;
   W3D_REQUIRE(a.transport == "rccl" || a.transport == "push" || a.transport == "sdma",
               "--transport must be rccl, push or sdma, not " + a.transport);
   o.push = a.transport == "push";

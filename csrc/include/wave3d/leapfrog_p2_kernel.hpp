@@ -293,6 +293,14 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
   // plane i+2 after stage 2 (plane i−1's slot is dead by then): 8 VGPRs fewer at the stage peak, and the vector-memory
   // sequence of an iteration is loads, loads, stores — the next commit waits for its load, never for a store
   constexpr bool kLate = !INIT && S >= 4;
+  // deep prefetch (experiment, off: -DP2_DEEP=1): the same two load points, each one plane further ahead — u^{n−1}
+  // plane i+2 into the slot stage 1 just consumed (two u^{n−1} slots), u^n plane i+3 into plane i−1's slot (dead after
+  // stage 2); twice the bytes in flight per CU. Measured 2.7 % slower per solve (head-loop spills; the loads were not
+  // what held the pass back: profiles/r5/p2_attribution.md)
+#ifndef P2_DEEP
+#define P2_DEEP 0
+#endif
+  constexpr bool kDeep = kLate && S == 5 && P2_DEEP;
   extern __shared__ double lds[];
   const int tid = static_cast<int>(threadIdx.x);
   int blk = static_cast<int>(blockIdx.x);
@@ -386,7 +394,11 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
                                                static_cast<int>(P * 8), 0x00020000);
     };
     auto load_pair = [&](auto bkc, const double* f, int x) __attribute__((always_inline)) -> D2 {
+#ifdef W3D_EXPERIMENT_NOLOAD  // (perf attribution only, results wrong: every plane load hits one of 4 resident planes)
+      const int xs = (x & 3) + 1;
+#else
       const int xs = decltype(bkc)::value ? x : x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
+#endif
       return as_d2(__builtin_amdgcn_raw_buffer_load_b128(rsrc(f, xs), static_cast<int>(goff), 0, 0));
     };
 
@@ -471,7 +483,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
         }
         const double lapl = d2sum(c.x, xm.x, xq.x, ym.x, yp.x, zm, c.y);
         const double laph = d2sum(c.y, xm.y, xq.y, ym.y, yp.y, c.x, zq);
-        const D2 o = k == 1 ? Lm[kLate ? 0 : (D & 1)] : L[k > 1 ? k - 2 : 0][s0];
+        const D2 o = k == 1 ? Lm[(kLate && !kDeep) ? 0 : (D & 1)] : L[k > 1 ? k - 2 : 0][s0];
         v = D2m(leapfrog(c.x, o.x, lapl, p.tau2), leapfrog(c.y, o.y, laph, p.tau2));
         if constexpr (EDGE) {
           v.x = rl ? v.x : 0.0;
@@ -481,9 +493,11 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
           if (!xreal(xp)) v = D2m(0.0, 0.0);
         }
         if constexpr (k < S) {
-          L[k][s0] = v;
           constexpr int pl = (k - 1) * 2 + (D & 1);
           wr2(kb(pl), ok_(pl, 0, 0), v);
+#ifdef P2_COND_QUEUE  // (A/B only: the round-5 first version, queue slot written only when the stage runs)
+          L[k][s0] = v;
+#endif
         }
         constexpr bool kChk =
 #ifdef P2_NO_CHECK
@@ -509,6 +523,11 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
           }
         }
       }
+      // (also when the stage is skipped: the slot's previous plane is dead either way, and an unconditional write
+      // keeps it from staying live through the general iterations — 8 VGPRs of spills with the deep prefetch)
+#ifndef P2_COND_QUEUE
+      if constexpr (k < S) L[k][s0] = v;
+#endif
       if constexpr (k >= S - 1) {
         // every wave stores (non-owners beyond the plane: dropped). Interior tiles: the thread's load offset plus a
         // scalar offset (0 for the own waves' planes, out of range otherwise); edge tiles: the per-lane store offset
@@ -576,9 +595,15 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     P2_SCHED_FENCE();                                                                                             \
   }
       W3D_P2_STAGE(1)
-      if constexpr (kLate) Lm[0] = load_pair(bkc, p.prev, i + 1);  // (its register freed by stage 1)
+      if constexpr (kDeep)
+        Lm[F & 1] = load_pair(bkc, p.prev, i + 2);
+      else if constexpr (kLate)
+        Lm[0] = load_pair(bkc, p.prev, i + 1);  // (its register freed by stage 1)
       W3D_P2_STAGE(2)
-      if constexpr (kLate) L[0][(F + 2) & 3] = load_pair(bkc, p.cur, i + 2);
+      if constexpr (kDeep)
+        L[0][(F + 3) & 3] = load_pair(bkc, p.cur, i + 3);
+      else if constexpr (kLate)
+        L[0][(F + 2) & 3] = load_pair(bkc, p.cur, i + 2);
       W3D_P2_STAGE(3)
       W3D_P2_STAGE(4)
       W3D_P2_STAGE(5)
@@ -606,6 +631,10 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
       if constexpr (!INIT) {
         L[0][1] = load_pair(Gen{}, p.cur, i0 + 1);
         Lm[0] = load_pair(Gen{}, p.prev, i0);
+        if constexpr (kDeep) {
+          L[0][2] = load_pair(Gen{}, p.cur, i0 + 2);
+          Lm[1] = load_pair(Gen{}, p.prev, i0 + 1);
+        }
       }
       // head blocks (general) until the first block inside the bulk range, bulk blocks, then the general tail
       const int blo = max(max(wx0, p.sx0), 1 - p.gx0) + (S - 1);

@@ -77,6 +77,7 @@ struct Candidate {
   bool overlap = true;
   int sdma_streams = 0;            // copy streams (0: the solver's default)
   bool shells_concurrent = false;  // overlap: shells beside the interior instead of before it
+  int reserve_cus = 0;             // CUs kept off the passes for RCCL's kernels (SolverOptions::reserve_cus)
 };
 // the candidates for `world` ranks (fake: one rank of a `world`-rank job alone); push and copy-engine candidates only on
 // request (neither has run between two GPUs yet)

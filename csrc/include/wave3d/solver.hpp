@@ -79,6 +79,11 @@ struct SolverOptions {
   // it (false: they get the whole GPU and finish first, so the exchange starts earlier — measured faster with the copy
   // engines at 512³ and 2048³; concurrent helps the small block shells when no transfer follows; env W3D_SHELLS)
   bool shells_concurrent = false;
+  // CUs kept free of the passes for RCCL's copy kernels (0: none). The compute stream gets a CU mask without the top
+  // `reserve_cus` CUs (KFD deals mask bits to the XCDs round-robin, so a multiple of 8 frees the same number of CUs in
+  // every XCD); a pass occupies a whole CU (LDS, VGPRs), so without a reserve RCCL's kernels of an overlapped exchange
+  // wait for the pass's last workgroups. The passes' x chunking then targets the remaining CUs. Env W3D_RESERVE_CUS.
+  int reserve_cus = 0;
   // copy-engine transport: copy streams (each gets its own SDMA engine; 0 = auto: one per slab face, one for a block
   // rank's messages — in a replayed graph a second copy stream made the 2048³ 2x2x2 rank slower, 48.8 vs 43.6 ms)
   int sdma_streams = 0;

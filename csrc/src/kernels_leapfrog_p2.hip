@@ -152,8 +152,9 @@ void launch_leapfrog_p2(const Layout& l, const Coeffs& c, const double* prev, co
   P2Params& p = pl.prm;
   if (grid_blocks > 0) {
     W3D_REQUIRE(grid_blocks >= pl.nblocks && (!t.xcd_remap || grid_blocks % 8 == 0), "leapfrog_p2: bad grid_blocks");
+    // (the padded grid's extra blocks get no tile: xper stays the active blocks' per-XCD share, else the remap would
+    // hand every tile to the first XCDs — measured: a slab rank's 256 tiles on 4 of 8 XCDs, passes 2.2x slower)
     pl.nblocks = p.nblocks = grid_blocks;
-    p.xper = pl.nblocks / 8;
   }
   const i64 kb = (l.xg - 1) * l.plane;  // x base only: in-plane offsets are plane-relative
   p.prev = analytic_start ? out1 + kb : prev + kb;  // (the analytic start reads neither: any valid buffer)

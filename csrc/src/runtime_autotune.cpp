@@ -17,10 +17,11 @@ namespace wave3d {
 std::vector<Candidate> autotune_candidates(int world, bool with_push, bool with_sdma) {
   std::vector<Candidate> v;
   auto add = [&](const char* name, const char* decomp, const char* transport, int temporal, bool overlap,
-                 int streams = 0, bool conc = false) {
-    v.push_back(Candidate{name, decomp, transport, temporal, overlap, streams, conc});
+                 int streams = 0, bool conc = false, int reserve = 0) {
+    v.push_back(Candidate{name, decomp, transport, temporal, overlap, streams, conc, reserve});
   };
   if (world <= 1) {  // one rank: only the pass depth matters
+    add("slab-S5", "slab", "rccl", 5, true);
     add("slab-S4", "slab", "rccl", 4, true);
     add("slab-S3", "slab", "rccl", 3, true);
     add("slab-S2", "slab", "rccl", 2, true);
@@ -31,7 +32,12 @@ std::vector<Candidate> autotune_candidates(int world, bool with_push, bool with_
   // The copy-engine and push candidates are opt-in across devices: neither has yet run between two GPUs (every
   // rehearsal shared one GPU); a fake rank (one process) always includes the copy engines.
   add("slab-S4-seq", "slab", "rccl", 4, false);
+  add("slab-S5-seq", "slab", "rccl", 5, false);  // (pair-tiled 5-step passes: one exchange per 5 steps)
   add("slab-S4", "slab", "rccl", 4, true);
+  add("slab-S5", "slab", "rccl", 5, true);
+  // (overlapped RCCL with 16 CUs — two per XCD — kept free of the passes: RCCL's kernels start at once instead of after
+  // the pass's last workgroups; the pass loses 1/16 of the CUs)
+  add("slab-S4-rsv16", "slab", "rccl", 4, true, 0, false, 16);
   if (with_sdma) {
     add("slab-S4-sdma-seq", "slab", "sdma", 4, false);
     add("slab-S4-sdma", "slab", "sdma", 4, true);
@@ -47,6 +53,7 @@ std::vector<Candidate> autotune_candidates(int world, bool with_push, bool with_
     add("block-S4-seq", "block", "rccl", 4, false);
     add("block-S4", "block", "rccl", 4, true);
     add("block-S4-conc", "block", "rccl", 4, true, 0, true);  // (shells beside the interior)
+    add("block-S4-rsv16", "block", "rccl", 4, true, 0, false, 16);
     if (with_sdma) {
       add("block-S4-sdma-seq", "block", "sdma", 4, false);
       add("block-S4-sdma", "block", "sdma", 4, true);         // (one copy stream)
@@ -80,7 +87,8 @@ std::string signature(const GpuSolver& s) {
   const int depth = s.mode() == "single-step" ? 1 : s.options().temporal;
   return s.mode() + "/" + s.transport() + "/" + (s.overlapped() ? "ov" : "seq") + "/S" + std::to_string(depth) + "/" +
          std::to_string(d.px) + "x" + std::to_string(d.py) + "x" + std::to_string(d.pz) + "/cs" +
-         std::to_string(s.sdma() ? s.copy_streams() : 0) + (s.overlapped() && s.options().shells_concurrent ? "/conc" : "");
+         std::to_string(s.sdma() ? s.copy_streams() : 0) + (s.overlapped() && s.options().shells_concurrent ? "/conc" : "") +
+         (s.options().reserve_cus > 0 ? "/rsv" + std::to_string(s.options().reserve_cus) : "");
 }
 }  // namespace
 
@@ -163,6 +171,7 @@ AutotuneResult autotune(const Problem& prob, const SolverOptions& base, int rank
     o.sdma = c.transport == "sdma";
     if (c.sdma_streams > 0) o.sdma_streams = c.sdma_streams;
     o.shells_concurrent = o.shells_concurrent || c.shells_concurrent;
+    if (c.reserve_cus > 0) o.reserve_cus = c.reserve_cus;
     // a short in-kernel flag bound while tuning: a candidate whose peer is lost costs seconds (k_flag_sync ends the
     // rest of the solve's waits after the first timeout); baked into the graphs, so the chosen solver keeps it
     if (ao.flag_timeout_s > 0.0 && (o.flag_timeout_s <= 0.0 || o.flag_timeout_s > ao.flag_timeout_s))

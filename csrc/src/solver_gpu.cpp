@@ -149,6 +149,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   // (perf studies: tiling overrides of the LDS S-step kernel; W3D_TB_TARGET=B splits the x march into chunks when the
   // tile grid has fewer than B tiles, W3D_TB_MINCHUNK its minimum planes, W3D_TB_XCDBLOCKS=1 square XCD blocks)
   if (const char* v = std::getenv("W3D_TB_TARGET")) opt_.tiling_tb.target_blocks = std::atoi(v);
+  if (const char* v = std::getenv("W3D_RESERVE_CUS")) opt_.reserve_cus = std::atoi(v);
   if (const char* v = std::getenv("W3D_TB_MINCHUNK")) opt_.tiling_tb.min_chunk = std::atoi(v);
   if (const char* v = std::getenv("W3D_TB_XCDBLOCKS")) opt_.tiling_tb.xcd_blocks = *v == '1';
   W3D_REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
@@ -163,8 +164,9 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   // passes) or 2-deep ones (two-step passes). Decided from the SMALLEST rank box so every rank picks the same mode.
   mode_ = Mode::kSingleStep;
   W3D_REQUIRE(opt_.temporal >= 1 && opt_.temporal <= 5, "temporal must be 1..5");
-  // 5-step passes: the pair-tiled kernel on one rank only (multi-rank passes keep k_leapfrog_tb's S ≤ 4)
-  if (opt_.temporal == 5 && (world > 1 || !opt_.tb || !opt_.tiling_tb.p2)) opt_.temporal = 4;
+  // 5-step passes: the pair-tiled kernel only (one rank, slab ranks; below: 3-D blocks and the push transport keep
+  // k_leapfrog_tb's S ≤ 4)
+  if (opt_.temporal == 5 && (!opt_.tb || !opt_.tiling_tb.p2)) opt_.temporal = 4;
   if (opt_.temporal >= 2 && world == 1) mode_ = Mode::kFusedSingle;
   const bool slab = dims_.py == 1 && dims_.pz == 1;
   if (opt_.temporal >= 2 && world > 1) {
@@ -177,7 +179,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
       mn[2] = imin(mn[2], b.nz());
     }
     const int rem = prob_.K - (analytic_ok() ? 1 : 2);  // steps left to the passes (each takes 2..temporal)
-    const i64 T2 = 2 * opt_.temporal;
+    const i64 T2 = 2 * (slab ? opt_.temporal : std::min(opt_.temporal, 4));
     // 3-D blocks: S-deep ghosts on every split axis, one exchange (faces, edges, corners) between passes
     const bool block_fits = (dims_.px == 1 || mn[0] >= imax(T2, 8)) && (dims_.py == 1 || mn[1] >= imax(T2, 8)) &&
                             (dims_.pz == 1 || mn[2] >= imax(T2, 8));
@@ -191,6 +193,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
       mode_ = Mode::kDeep;
   }
   block_tb_ = mode_ == Mode::kDeepTb && !slab;
+  if (opt_.temporal == 5 && world > 1 && (mode_ != Mode::kDeepTb || block_tb_ || opt_.push)) opt_.temporal = 4;
   if (opt_.push && world > 1) {
     W3D_REQUIRE(mode_ == Mode::kDeepTb && !block_tb_, "push transport: slab LDS passes (deep-tb) only, not " + mode());
     push_ = true;
@@ -284,6 +287,15 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
     std::vector<uint32_t> mask(static_cast<size_t>((ncu + 31) / 32), 0u);
     for (int c = r * ncu / P; c < (r + 1) * ncu / P; ++c) mask[static_cast<size_t>(c / 32)] |= 1u << (c % 32);
     W3D_HIP(hipExtStreamCreateWithCUMask(&s0_, static_cast<uint32_t>(mask.size()), mask.data()));
+  } else if (opt_.reserve_cus > 0) {
+    int dev = 0, ncu = 0;
+    W3D_HIP(hipGetDevice(&dev));
+    W3D_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    W3D_REQUIRE(opt_.reserve_cus < ncu, "reserve_cus must leave the passes at least one CU");
+    std::vector<uint32_t> mask(static_cast<size_t>((ncu + 31) / 32), 0u);
+    for (int c = 0; c < ncu - opt_.reserve_cus; ++c) mask[static_cast<size_t>(c / 32)] |= 1u << (c % 32);
+    W3D_HIP(hipExtStreamCreateWithCUMask(&s0_, static_cast<uint32_t>(mask.size()), mask.data()));
+    if (opt_.tiling_tb.target_blocks == LeapfrogTbTiling{}.target_blocks) opt_.tiling_tb.target_blocks = ncu - opt_.reserve_cus;
   } else {
     W3D_HIP(hipStreamCreateWithFlags(&s0_, hipStreamNonBlocking));
   }
@@ -562,7 +574,8 @@ void GpuSolver::build_units() {
     // the pair-tiled passes (k_leapfrog_p2, one rank): µs per step at 512³ (profiles/r5/)
     static const double kStepCostP2[6] = {0.0, 610.0, 430.0, 290.0, 225.0, 180.0};
     static const double kAnalyticCostP2[6] = {0.0, 1e9, 300.0, 200.0, 135.0, 1e9};
-    const bool p2 = opt_.tiling_tb.p2 && world_ == 1 && leapfrog_p2_supported(lay_, full_, 2);
+    // (slab ranks too: their passes span the whole y/z range, shells included)
+    const bool p2 = opt_.tiling_tb.p2 && !block_tb_ && !push_ && leapfrog_p2_supported(lay_, full_, 2);
     const double* kStepCost = p2 ? kStepCostP2 : kStepCostTb;
     const double* kAnalyticCost = p2 ? kAnalyticCostP2 : kAnalyticCostTb;
     const int rem = K - n, smax = opt_.temporal, smin = mode_ == Mode::kDeepTb ? 2 : 1;

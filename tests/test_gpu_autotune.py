@@ -40,7 +40,7 @@ def _chosen_ok(meta):
 def test_autotune_one_rank(gpu, tmp_path):
     meta, err = _run(tmp_path, "128", "0.001", "20", "1", "--repeat", "2")
     tuned = meta["autotune_s"]
-    assert set(tuned) == {"slab-S4", "slab-S3", "slab-S2", "slab-S1"}  # (no neighbours: nothing else differs)
+    assert set(tuned) == {"slab-S5", "slab-S4", "slab-S3", "slab-S2", "slab-S1"}  # (no neighbours: nothing else differs)
     _chosen_ok(meta)
     assert "rejected" not in err  # every one-rank schedule reproduces the reference log bit for bit
     assert meta["steps"][-1][0] == 20 and meta["finite"] and meta["autotune_rounds"] == 5
@@ -79,7 +79,7 @@ def test_autotune_python_entry_point(gpu, tmp_path):
     """Solver(autotune=True) runs the CLI's autotune: same candidates, same choice on one rank."""
     spec = ProblemSpec(N=128, tau=1e-3, K=20)
     s = Solver(spec, backend="hip", device=0, autotune=True)
-    assert set(s.autotune_times) == {"slab-S4", "slab-S3", "slab-S2", "slab-S1"}
+    assert set(s.autotune_times) == {"slab-S5", "slab-S4", "slab-S3", "slab-S2", "slab-S1"}
     cli, _ = _run(tmp_path, "128", "0.001", "20", "1")
     assert s.schedule == cli["schedule"]
     r = s.run()

@@ -89,18 +89,19 @@ def test_rccl_self_block_deep_tb_graph(gpu, tmp_path, world, decomp, K):
 
 def test_cli_traffic_line_and_json(gpu, tmp_path):
     """Effective GB/s: the CLI prints the schedule's compulsory field traffic and halo volume per
-    solve and puts both (and the GB/s) into --json; a fake slab rank of 2 sends 4 + 3 planes after each pass."""
+    solve and puts both (and the GB/s) into --json; a fake slab rank of 2 sends 5 + 4 planes after each pass."""
     js = str(tmp_path / "one.json")
     out = subprocess.run([CLI, "128", "0.001", "20", "1", "--repeat", "2", "--warmup", "1", "--json", js, "--quiet"],
                          check=True, timeout=120, capture_output=True, text=True).stdout
     m = json.loads(open(js).read())
-    assert m["field_bytes"] == (2 + 4 * 4) * 127 ** 3 * 8 and m["halo_bytes"] == 0
+    # (analytic 4-step start writes 2 fields, three 5-step passes read 2 and write 2)
+    assert m["field_bytes"] == (2 + 3 * 4) * 127 ** 3 * 8 and m["halo_bytes"] == 0
     assert m["effective_gbs"] == pytest.approx(m["field_bytes"] / m["solve_s"] / 1e9, rel=1e-6)
     assert "Traffic: " in out and "GB/s effective" in out
     js = str(tmp_path / "fake.json")
     out = subprocess.run([CLI, "128", "0.001", "20", "1", "--fake-rank", "0/2", "--repeat", "2", "--warmup", "1",
                           "--json", js, "--quiet"], check=True, timeout=120, capture_output=True, text=True).stdout
     m = json.loads(open(js).read())
-    plane_bytes = m["halo_bytes"] / (4 * 7)  # four exchanges of 4 + 3 planes on the one face
+    plane_bytes = m["halo_bytes"] / (3 * 9)  # three exchanges of 5 + 4 planes on the one face
     assert m["halo_bytes"] > 0 and plane_bytes == int(plane_bytes) and plane_bytes >= 129 * 129 * 8
     assert "Traffic (this rank): " in out

@@ -11,7 +11,7 @@ import sys
 
 def short(name: str) -> str:
     n = name.replace("void ", "")
-    for ns in ("wave3d::(anonymous namespace)::", "wave3d::tbk::", "wave3d::"):
+    for ns in ("wave3d::(anonymous namespace)::", "wave3d::tbk::", "wave3d::p2k::", "wave3d::"):
         n = n.replace(ns, "")
     m = re.match(r"([A-Za-z_0-9]+(<[^>]*>)?)", n)
     return m.group(1) if m else n[:60]

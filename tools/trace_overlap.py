@@ -61,8 +61,13 @@ def _overlap(a: tuple[int, int], merged: list[tuple[int, int]]) -> int:
 def analyse(d: str) -> dict:
     kern = _rows(d, "kernel_trace.csv")
     copies = _rows(d, "memory_copy_trace.csv")
-    passes = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in kern if "k_leapfrog_tb" in r["Kernel_Name"]]
+    passes = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in kern
+              if "k_leapfrog_tb" in r["Kernel_Name"] or "k_leapfrog_p2" in r["Kernel_Name"]]
     merged = _merge(passes)
+    # RCCL's own copy kernels (the rccl transport, or --fake-traffic): how much of their time ran beside a pass
+    rccl = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in kern if "nccl" in r["Kernel_Name"].lower()]
+    rccl_ns = sum(b - a for a, b in rccl)
+    rccl_ov = sum(_overlap(a, merged) for a in rccl)
     per_kind = defaultdict(lambda: [0, 0])
     for r in kern:
         k = _short(r["Kernel_Name"])
@@ -82,7 +87,8 @@ def analyse(d: str) -> dict:
         per_kind[k][1] += a[1] - a[0]
     return {"copies": len(copies), "copy_ns": tot, "copy_ns_during_pass": ov,
             "copy_bytes": nbytes if size_key else None,
-            "pass_ns": sum(b - a for a, b in merged), "per_kind": dict(per_kind)}
+            "pass_ns": sum(b - a for a, b in merged), "per_kind": dict(per_kind),
+            "rccl_kernels": len(rccl), "rccl_ns": rccl_ns, "rccl_ns_during_pass": rccl_ov}
 
 
 def copy_volume(r: dict, json_path: str | None, solves: int | None) -> str:
@@ -107,8 +113,12 @@ def main(argv: list[str]) -> int:
     print(f"| memory copies | {r['copies']} ({copy_volume(r, a.json, a.solves)}) |")
     print(f"| copy time | {r['copy_ns'] / 1e6:.3f} ms |")
     frac = r["copy_ns_during_pass"] / r["copy_ns"] if r["copy_ns"] else 0.0
-    print(f"| copy time while a k_leapfrog_tb pass ran | {r['copy_ns_during_pass'] / 1e6:.3f} ms ({100 * frac:.1f} %) |")
-    print(f"| k_leapfrog_tb busy time (union) | {r['pass_ns'] / 1e6:.3f} ms |")
+    print(f"| copy time while a k_leapfrog_tb/p2 pass ran | {r['copy_ns_during_pass'] / 1e6:.3f} ms ({100 * frac:.1f} %) |")
+    print(f"| k_leapfrog_tb/p2 busy time (union) | {r['pass_ns'] / 1e6:.3f} ms |")
+    if r["rccl_kernels"]:
+        rf = r["rccl_ns_during_pass"] / r["rccl_ns"] if r["rccl_ns"] else 0.0
+        print(f"| RCCL kernels | {r['rccl_kernels']}, {r['rccl_ns'] / 1e6:.3f} ms |")
+        print(f"| RCCL kernel time while a pass ran | {r['rccl_ns_during_pass'] / 1e6:.3f} ms ({100 * rf:.1f} %) |")
     print("\n| kind | count | total ms |\n|---|---|---|")
     for k, (n, t) in sorted(r["per_kind"].items(), key=lambda kv: -kv[1][1]):
         print(f"| `{k}` | {n} | {t / 1e6:.3f} |")

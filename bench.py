@@ -238,8 +238,8 @@ def _qualify_sdma(a, rank: int, world: int, local: int) -> tuple[bool, str]:
     1e-12: the max is order-free, the sum's grouping follows the decomposition). Both run in fresh children."""
     small = ["64", "0.001", "20", "1", "--quiet", "--warmup", "1", "--repeat", "1"]
     ref = _child(a, rank, world, local, small, "qualify-ref", ranks=1)
-    got = _child(a, rank, world, local, small + ["--transport", "sdma", "--no-autotune", "--decomp", "slab",
-                                                  "--temporal", "4"], "qualify")
+    got = _child(a, rank, world, local, small + ["--transport", "sdma", "--decomp", "slab", "--temporal", "4"]
+                 + (["--no-rccl"] if a.no_rccl else []), "qualify")
     verdict = b"0"
     why = ""
     if rank == 0:
@@ -266,7 +266,9 @@ def run_native(a, rank: int, world: int, local: int) -> int:
     warm = max(a.warmup, 2 if multi else 1)
     temporal = 1 if a.no_temporal else a.temporal
     sdma_ok, sdma_why = False, ""
-    if multi and not a.cpu and not a.no_rccl and not a.no_autotune and not a.no_qualify:
+    # (before the autotune may time copy-engine candidates, and before an explicit copy-engine run: the rehearsal of
+    # ranks sharing one GPU qualifies the same way)
+    if multi and not a.cpu and not a.no_qualify and ((not a.no_rccl and not a.no_autotune) or a.native_transport == "sdma"):
         sdma_ok, sdma_why = _qualify_sdma(a, rank, world, local)
     autotune_sdma = a.autotune_sdma or sdma_ok
     if a.native_transport == "sdma" or autotune_sdma:
@@ -295,28 +297,34 @@ def run_native(a, rank: int, world: int, local: int) -> int:
     t0 = time.perf_counter()
     run = _child(a, rank, world, local, cmd, "main")
     fallback = None
-    if not run["ok"] and multi and not a.no_rccl:
+    if not run["ok"] and multi:
         # one fresh child with the conservative native schedule (no autotune, RCCL slabs, sequential exchange), so a
         # first contact with a node that breaks an autotune candidate still yields a labelled scaling point
         # the failing rank's own message (the others report only that a peer failed)
-        errs = [run["err"]]
+        errs = [(run["err"], run["why"])]
         if world > 1:
             import torch.distributed as dist
 
             errs = [None] * world
-            dist.all_gather_object(errs, run["err"])
-        own = [e for e in errs if e and "another rank" not in e and "peer" not in e]
-        first = (own or [e for e in errs if e] or ["unknown failure"])[0]
+            dist.all_gather_object(errs, (run["err"], run["why"]))
+        # (a rank whose child was killed because a peer failed reports why = "a peer rank failed": not the cause)
+        own = [e for e, why in errs if e and not why and "another rank" not in e and "peer" not in e]
+        first = (own or [e for e, _ in errs if e] or ["unknown failure"])[0]
         if rank == 0:
             print(f"[bench] native run failed ({first}); retrying once with the conservative schedule",
                   file=sys.stderr, flush=True)
         safe = base + ["--decomp", "slab", "--temporal", "4", "--no-overlap"]
+        via = "rccl"
         if a.cpu:
             safe.append("--cpu")
-        elif not a.no_phases:
-            safe.append("--phases")
+        else:
+            if a.no_rccl:  # (no RCCL at all: the transport the run asked for, host collectives through files)
+                safe += ["--no-rccl", "--transport", a.native_transport]
+                via = a.native_transport
+            if not a.no_phases:
+                safe.append("--phases")
         run = _child(a, rank, world, local, safe, "fallback")
-        fallback = {"schedule": "slab-S4-seq, no autotune" + ("" if a.cpu else ", rccl"), "first_failure": first}
+        fallback = {"schedule": "slab-S4-seq, no autotune" + ("" if a.cpu else ", " + via), "first_failure": first}
     wall = time.perf_counter() - t0
     res, tail = run["res"], run["tail"]
     if not run["ok"]:

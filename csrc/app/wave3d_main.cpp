@@ -186,7 +186,7 @@ int run_group(const Args& a, const SolverOptions& o, const hipDeviceProp_t& prop
     std::ofstream j(a.json);
     j << "{\"backend\": \"hip\", \"group\": " << a.group << ", \"transport\": " << jstr(a.group_transport)
       << ", \"graph\": " << (g.graph_enabled() ? "true" : "false") << ", \"schedule\": " << jstr(g.rank(0).mode())
-      << ", \"rccl_comms\": " << cc.size() << ", \"solve_s\": " << jnum(best) << ", \"steps\": [";
+      << ", \"temporal\": " << g.rank(0).options().temporal << ", \"rccl_comms\": " << cc.size() << ", \"solve_s\": " << jnum(best) << ", \"steps\": [";
     for (size_t i = 0; i < r.steps.size(); ++i)
       j << (i ? ", " : "") << "[" << r.steps[i] << ", " << jnum(r.max_err[i]) << ", " << jnum(r.rms_err[i]) << "]";
     j << "]}\n";

@@ -297,6 +297,13 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
   // plane i+2 into the slot stage 1 just consumed (two u^{n−1} slots), u^n plane i+3 into plane i−1's slot (dead after
   // stage 2); twice the bytes in flight per CU. Measured 2.7 % slower per solve (head-loop spills; the loads were not
   // what held the pass back: profiles/r5/p2_attribution.md)
+#ifndef P2_DEFER_STORE  // (experiment, off: measured 3.7 % slower per solve, profiles/r5/store_experiments.md)
+#define P2_DEFER_STORE 0
+#endif
+#ifndef P2_STORE_ALL  // (A/B: 1 = every wave stores in the analytic start too, the round-5 first version)
+#define P2_STORE_ALL 0
+#endif
+  constexpr bool kDefer = !INIT && P2_DEFER_STORE;
 #ifndef P2_DEEP
 #define P2_DEEP 0
 #endif
@@ -359,6 +366,9 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     // stages this wave computes (a scalar: the stage tests must stay scalar branches, not lane masks)
     int wst = __builtin_amdgcn_readfirstlane(wkind == 1 ? wlv : 0);
     const bool winner = wst == S;               // (scalar) the tile's own pairs
+#ifdef P2_STAGGER
+    const bool wodd = (__builtin_amdgcn_readfirstlane(tid) >> 6) & 1;
+#endif
     const int y = ty0 - (S - 1) + a, z = tz0 - E + 2 * b;
     const int el = z + p.za;                    // element of the pair's first node in its row
     const bool ldv = act && y >= p.ay0 && y < p.ay1 && el >= 0 && el + 2 <= p.pitch;
@@ -432,6 +442,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
       L[decltype(ic)::value / 4][decltype(ic)::value % 4] = D2m(0.0, 0.0);
     });
     D2 Lm[2] = {D2m(0.0, 0.0), D2m(0.0, 0.0)};
+    D2 vS = D2m(0.0, 0.0);  // (deferred stores: the level-S value of the previous iteration)
 
     const int i0 = wx0 - S + 1, i1 = wx1 + S - 2;
     auto xreal = [&](int x) __attribute__((always_inline)) {
@@ -528,13 +539,18 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
 #ifndef P2_COND_QUEUE
       if constexpr (k < S) L[k][s0] = v;
 #endif
-      if constexpr (k >= S - 1) {
-        // every wave stores (non-owners beyond the plane: dropped). Interior tiles: the thread's load offset plus a
-        // scalar offset (0 for the own waves' planes, out of range otherwise); edge tiles: the per-lane store offset
+      if constexpr (k == S && kDefer) vS = v;  // (stored at the start of the next iteration: flush)
+      if constexpr (k >= S - 1 && !kDefer) {
+        // Interior tiles: the thread's load offset plus a scalar offset (0 for the own waves' planes, out of range
+        // otherwise); edge tiles: the per-lane store offset. Passes that load: every wave stores (non-owners beyond
+        // the plane: dropped), so every wave's vector-memory sequence is the same and the compiler's waits for the
+        // loads can leave the stores in flight. The analytic start loads nothing: only the own waves store (−2 %)
 #ifndef W3D_EXPERIMENT_NOSTORE  // (perf attribution only, results wrong: the pass writes nothing to HBM)
-        const int sso = (xown && winner) ? 0 : static_cast<int>(0x80000000u);
-        __builtin_amdgcn_raw_buffer_store_b128(as_u4(v), rsrc(k == S ? p.out2 : p.out1, xp),
-                                               static_cast<int>(EDGE ? soff : goff), sso, 2 /* nt */);
+        if (P2_STORE_ALL || !INIT || winner) {
+          const int sso = (xown && winner) ? 0 : static_cast<int>(0x80000000u);
+          __builtin_amdgcn_raw_buffer_store_b128(as_u4(v), rsrc(k == S ? p.out2 : p.out1, xp),
+                                                 static_cast<int>(EDGE ? soff : goff), sso, 2 /* nt */);
+        }
 #endif
       }
     };
@@ -574,13 +590,42 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
       L[0][(F + 2) & 3] = u;  // (one store to the queue slot: SROA keeps the queue in registers)
     };
 
+    // deferred stores (kDefer), at the start of iteration i: levels S−1 and S of iteration i−1 (planes i−S+1, i−S),
+    // the own waves only. Every wave has waited for all its vector-memory operations just before (vmcnt(0) after
+    // the barrier), and its loads come after these stores, so no later wait depends on whether a wave stored: the
+    // compiler's waits stay exact for every wave (a store skipped by half the waves after the loads would make it
+    // wait for the other half's stores) and the non-own waves no longer issue out-of-range stores through the
+    // texture addresser (rocprofv3: SQ_VMEM_TA_ADDR_FIFO_FULL 21 % of the CU-busy cycles, profiles/r5/)
+    auto flush = [&](auto fc, auto ec, int i) __attribute__((always_inline)) {
+      constexpr int F = decltype(fc)::value;
+      constexpr bool EDGE = decltype(ec)::value;
+#ifndef W3D_EXPERIMENT_NOSTORE
+      if (winner) {
+        const int x1 = i - S + 1, x2 = i - S;
+        const int s1 = (x1 >= wx0 && x1 < wx1) ? 0 : static_cast<int>(0x80000000u);
+        const int s2 = (x2 >= wx0 && x2 < wx1) ? 0 : static_cast<int>(0x80000000u);
+        const int off = static_cast<int>(EDGE ? soff : goff);
+        __builtin_amdgcn_raw_buffer_store_b128(as_u4(L[S - 1][(F - S + 1 + 8) & 3]), rsrc(p.out1, x1), off, s1, 2);
+        __builtin_amdgcn_raw_buffer_store_b128(as_u4(vS), rsrc(p.out2, x2), off, s2, 2);
+      }
+#endif
+    };
+
     // iteration i with phase F
     auto iteration = [&](auto fc, auto bkc, auto ec, int i) __attribute__((always_inline)) {
       constexpr int F = decltype(fc)::value;
 #ifndef W3D_EXPERIMENT_NOBARRIER
       p2_barrier();  // every read of the slots overwritten below (iteration i−1) is done; i−1's writes visible
 #endif
+#ifdef P2_STAGGER  // (experiment: odd waves start each plane 64·P2_STAGGER cycles later, so the 16 waves' loads do not
+                   // all reach the texture addresser at once)
+      if (wodd) __builtin_amdgcn_s_sleep(P2_STAGGER);
+#endif
       opaque_bases();
+      if constexpr (kDefer) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's loads of iteration i−1 (and older stores)
+        flush(fc, ec, i);
+      }
       if (act) wr2(b0, o0((F + 1) & 1, 0, 0), L[0][(F + 1) & 3]);  // u^n plane i+1 → LDS
       if constexpr (INIT) {
         init_iter(fc, ec, i);
@@ -655,14 +700,32 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
         iteration(std::integral_constant<int, 2>{}, Bulk{}, ec, ib + 2);
         iteration(std::integral_constant<int, 3>{}, Bulk{}, ec, ib + 3);
       }
+      // (a tail that runs ends at one of the breaks, where the last iteration's deferred stores go out; whole blocks
+      // up to i1 leave ib = i1 + 1 at phase 0)
+      if constexpr (kDefer) {
+        if (ib > i1) flush(std::integral_constant<int, 0>{}, ec, ib);
+      }
       for (; ib <= i1; ib += 4) {
         iteration(std::integral_constant<int, 0>{}, Gen{}, ec, ib);
-        if (ib + 1 > i1) break;
+        if (ib + 1 > i1) {
+          if constexpr (kDefer) flush(std::integral_constant<int, 1>{}, ec, ib + 1);
+          break;
+        }
         iteration(std::integral_constant<int, 1>{}, Gen{}, ec, ib + 1);
-        if (ib + 2 > i1) break;
+        if (ib + 2 > i1) {
+          if constexpr (kDefer) flush(std::integral_constant<int, 2>{}, ec, ib + 2);
+          break;
+        }
         iteration(std::integral_constant<int, 2>{}, Gen{}, ec, ib + 2);
-        if (ib + 3 > i1) break;
+        if (ib + 3 > i1) {
+          if constexpr (kDefer) flush(std::integral_constant<int, 3>{}, ec, ib + 3);
+          break;
+        }
         iteration(std::integral_constant<int, 3>{}, Gen{}, ec, ib + 3);
+        if (ib + 4 > i1) {
+          if constexpr (kDefer) flush(std::integral_constant<int, 0>{}, ec, ib + 4);
+          break;
+        }
       }
     };
 #ifdef P2_SPLIT_EDGE

@@ -309,12 +309,12 @@ class GpuSolver {
   i64 sx0_ = 0, sx1_ = 0;         // deep mode: stage-1 x range (one ghost plane beyond each neighbour face)
   LBox sreal_;                    // deep-tb: stage-real ranges per axis (temporal − 1 nodes into each neighbour's ghosts)
   bool block_tb_ = false;         // deep-tb on a 3-D block decomposition (S-deep ghosts on every split axis)
-  DeepPlan deep_[5];              // block_tb_: exchange plan before a pass of s steps (index s = 2..temporal)
-  BoxCopyTable pack_tab_[5], unpack_tab_[5];  // ... and its device job tables (send / receive regions)
-  TbPack pk_host_[5];                          // fused z-face pack per exchange depth (fused_pack; w = 0: none)
+  DeepPlan deep_[6];              // block_tb_: exchange plan before a pass of s steps (index s = 2..temporal)
+  BoxCopyTable pack_tab_[6], unpack_tab_[6];  // ... and its device job tables (send / receive regions)
+  TbPack pk_host_[6];                          // fused z-face pack per exchange depth (fused_pack; w = 0: none)
   TbPack* pk_dev_ = nullptr;                   // ... the same five entries in device memory
   i64 deep_max_ = 0;              // largest staging buffer of those plans (doubles): the receive staging
-  i64 sbase_[5] = {};             // send staging: the region of depth s starts at sbase_[s] (one region per depth)
+  i64 sbase_[6] = {};             // send staging: the region of depth s starts at sbase_[s] (one region per depth)
   i64 send_total_ = 0;            // ... and its size (doubles)
   int deep_s_ = 2;                // depth of the exchange being issued
   std::vector<int> n_dshell_;     // partials per deep shell launch

@@ -70,6 +70,11 @@ P2Plan make_plan_p2(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, L
   W3D_REQUIRE(l.gx0 + b.x0 - S <= 0 || b.x0 - S >= -l.xg, "leapfrog_p2: halo deeper than the ghosts in x");
   W3D_REQUIRE(l.gx0 + b.x1 + S - 1 >= l.N || b.x1 + S - 1 < l.nx + l.xg, "leapfrog_p2: halo deeper than the ghosts in x");
   W3D_REQUIRE(real.x0 >= -l.xg && real.x1 <= l.nx + l.xg, "leapfrog_p2: real range outside the allocation in x");
+  // y / z (3-D block ranks): u^n is read S nodes beyond the box, within the ghosts unless beyond the global boundary
+  W3D_REQUIRE(l.gy0 + b.y0 - S <= 0 || b.y0 - S >= -l.yg, "leapfrog_p2: halo deeper than the ghosts in y");
+  W3D_REQUIRE(l.gy0 + b.y1 + S - 1 >= l.N || b.y1 + S - 1 < l.ny + l.yg, "leapfrog_p2: halo deeper than the ghosts in y");
+  W3D_REQUIRE(l.gz0 + b.z0 - S <= 0 || b.z0 - S >= -l.zg, "leapfrog_p2: halo deeper than the ghosts in z");
+  W3D_REQUIRE(l.gz0 + b.z1 + S - 1 >= l.N || b.z1 + S - 1 < l.nz + l.zg, "leapfrog_p2: halo deeper than the ghosts in z");
   W3D_REQUIRE(l.plane < (i64{1} << 27), "leapfrog_p2: plane too large for 32-bit buffer offsets");
   P2Plan pl;
   P2Params& p = pl.prm;
@@ -120,11 +125,13 @@ P2Plan make_plan_p2(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, L
 }  // namespace
 
 bool leapfrog_p2_supported(const Layout& l, const LBox& box, int stages) {
-  // the pass's tiles span the rank's whole y/z compute range (one rank, or x slabs), pairs start on 16-byte nodes
+  // the pass's tiles span the rank's whole y/z compute range (one rank, x slabs, or a 3-D block's whole box), pairs
+  // start on 16-byte nodes. (A y/z sub-box of the rank is refused: a pair that straddles its last z node stores its
+  // second node too — harmless beyond the rank's box, where the next exchange rewrites the ghost, but not into nodes
+  // another box of the same rank owns.)
   const LBox full = compute_box(l);
   return stages >= 2 && stages <= 5 && box.y0 == full.y0 && box.y1 == full.y1 && box.z0 == full.z0 &&
-         box.z1 == full.z1 && l.gy0 == 0 && l.gz0 == 0 && l.ny == l.N + 1 && l.nz == l.N + 1 && l.yg >= 1 &&
-         l.zg >= 1 && (box.z0 + l.zg + l.zs) % 2 == 0;
+         box.z1 == full.z1 && l.yg >= 1 && l.zg >= 1 && (box.z0 + l.zg + l.zs) % 2 == 0;
 }
 
 int leapfrog_p2_partials(const Layout& l, const LBox& box, const LeapfrogTbTiling& t) {

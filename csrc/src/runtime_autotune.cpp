@@ -51,6 +51,7 @@ std::vector<Candidate> autotune_candidates(int world, bool with_push, bool with_
   add("slab-S1", "slab", "rccl", 1, true);
   if (world >= 4) {  // (2 ranks: "block" is the slab)
     add("block-S4-seq", "block", "rccl", 4, false);
+    add("block-S5-seq", "block", "rccl", 5, false);  // (pair-tiled 5-step passes over the whole block)
     add("block-S4", "block", "rccl", 4, true);
     add("block-S4-conc", "block", "rccl", 4, true, 0, true);  // (shells beside the interior)
     add("block-S4-rsv16", "block", "rccl", 4, true, 0, false, 16);

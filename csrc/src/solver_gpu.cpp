@@ -193,7 +193,11 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
       mode_ = Mode::kDeep;
   }
   block_tb_ = mode_ == Mode::kDeepTb && !slab;
-  if (opt_.temporal == 5 && world > 1 && (mode_ != Mode::kDeepTb || block_tb_ || opt_.push)) opt_.temporal = 4;
+  // (3-D blocks: 5-step passes with the exchange after each pass only — the overlapped schedule's shell boxes are y/z
+  // sub-boxes of the rank, which the pair-tiled kernel does not take; their z-face pack is the pack kernel's)
+  if (opt_.temporal == 5 && world > 1 && (mode_ != Mode::kDeepTb || (block_tb_ && opt_.overlap) || opt_.push))
+    opt_.temporal = 4;
+  if (block_tb_ && opt_.temporal == 5) opt_.fused_pack = false;
   if (opt_.push && world > 1) {
     W3D_REQUIRE(mode_ == Mode::kDeepTb && !block_tb_, "push transport: slab LDS passes (deep-tb) only, not " + mode());
     push_ = true;
@@ -574,8 +578,9 @@ void GpuSolver::build_units() {
     // the pair-tiled passes (k_leapfrog_p2, one rank): µs per step at 512³ (profiles/r5/)
     static const double kStepCostP2[6] = {0.0, 610.0, 430.0, 290.0, 225.0, 180.0};
     static const double kAnalyticCostP2[6] = {0.0, 1e9, 300.0, 200.0, 135.0, 1e9};
-    // (slab ranks too: their passes span the whole y/z range, shells included)
-    const bool p2 = opt_.tiling_tb.p2 && !block_tb_ && !push_ && leapfrog_p2_supported(lay_, full_, 2);
+    // (slab ranks too: their passes span the whole y/z range, shells included; block ranks when the exchange follows
+    // the pass: every pass is then the rank's whole box)
+    const bool p2 = opt_.tiling_tb.p2 && !push_ && (!block_tb_ || !opt_.overlap) && leapfrog_p2_supported(lay_, full_, 2);
     const double* kStepCost = p2 ? kStepCostP2 : kStepCostTb;
     const double* kAnalyticCost = p2 ? kAnalyticCostP2 : kAnalyticCostTb;
     const int rem = K - n, smax = opt_.temporal, smin = mode_ == Mode::kDeepTb ? 2 : 1;

@@ -105,3 +105,16 @@ def test_cli_traffic_line_and_json(gpu, tmp_path):
     plane_bytes = m["halo_bytes"] / (3 * 9)  # three exchanges of 5 + 4 planes on the one face
     assert m["halo_bytes"] > 0 and plane_bytes == int(plane_bytes) and plane_bytes >= 129 * 129 * 8
     assert "Traffic (this rank): " in out
+
+
+@pytest.mark.parametrize("world,decomp,N", [(4, "2x2x1", 66), (8, "2x2x2", 77), (6, "1x2x3", 71), (8, "2x2x2", 128)])
+def test_rccl_self_block_p2_five_step_passes(gpu, tmp_path, world, decomp, N):
+    """3-D block ranks with the exchange after each pass run the pair-tiled 5-step passes over their whole box (y/z
+    ghosts 5 deep, the z-face pack by the pack kernel): bit-identical to one GPU, also with NaN-poisoned ghosts. Odd
+    extents put a pair across a block's last z node (its second node lands in the ghost the next exchange rewrites)."""
+    K = 20
+    _, f1 = _single(N, K)
+    for extra in (("--no-overlap",), ("--no-overlap", "--poison-ghosts")):
+        meta, f, _ = _group(tmp_path, N, K, world, decomp, extra=extra)
+        assert meta["schedule"] == "deep-tb-block" and meta["temporal"] == 5 and meta["graph"] is True
+        assert np.array_equal(f, f1)

@@ -172,6 +172,30 @@ def test_bench_two_ranks_sdma_rehearsal(gpu, tmp_path):
     assert line["n_gpus"] == 2 and line["distinct_gpus"] == 1 and "rehearsal" in line
     assert line["config"]["transport"] == "sdma" and line["config"]["schedule"].endswith("-sdma")
     assert line["correct"] is True and line["final_max_err"] == pytest.approx(3.960129e-09, rel=1e-6)
+    # (VERDICT r4 #3a: the copy-engine qualification child ran first, both processes on this one GPU)
+    assert line["sdma_qualified"] is True and "equals the one-rank log" in line["sdma_qualification"], \
+        line.get("sdma_qualification")
+
+
+def test_bench_fallback_child_on_one_gpu(gpu, tmp_path):
+    """VERDICT r4 #3b on the GPU: 2 bench ranks sharing one GPU; the main native run fails on rank 1 right after setup
+    (fault injection), every rank stops its child, and ONE fresh child with the conservative schedule (slabs, 4-step
+    passes, sequential exchange, no autotune) produces the JSON line, labelled with that schedule and the failure."""
+    out = tmp_path / "b.jsonl"
+    env = dict(ENV, W3D_BENCH_FAIL_SETUP_RANK="1")
+    env.pop("W3D_BENCH_FAIL_FALLBACK", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(29950 + os.getpid() % 40), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--share-gpus", "--no-rccl", "--native-transport", "sdma", "--steps", "3", "--warmup", "2",
+           "--out", str(out)]
+    p = subprocess.run(cmd, timeout=300, env=env, capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "retrying once with the conservative schedule" in p.stderr
+    line = json.loads(out.read_text().splitlines()[-1])
+    assert line["fallback_schedule"] == "slab-S4-seq, no autotune, sdma"
+    assert "injected fault" in line["first_failure"]
+    assert line["config"]["schedule"].startswith("slab") and line["config"]["overlap"] is False
+    assert line["correct"] is True and line["final_max_err"] == pytest.approx(3.960129e-09, rel=1e-6)
 
 
 def test_sdma_unconnected_solver_refuses_to_run(gpu):

@@ -123,13 +123,13 @@ def test_oracle_sweep(gpu, N, L, tau, K, ce, temporal):
 
 
 def test_traffic_accounting(gpu):
-    """GpuSolver::traffic (SURVEY.md §5.5 effective GB/s): K = 20 on one rank is the analytic-start pass (3 steps,
-    writes two levels) plus four 4-step passes (read two, write two) over the 63³ updated nodes; no halo."""
+    """GpuSolver::traffic (SURVEY.md §5.5 effective GB/s): K = 20 on one rank is the analytic-start pass (4 steps,
+    writes two levels) plus three 5-step passes (read two, write two) over the 63³ updated nodes; no halo."""
     spec = ProblemSpec(N=64, tau=1e-3, K=20)
     s = Solver(spec, backend="hip", device=0)
     s.run()
     t = s.traffic()
-    assert t["field_bytes"] == (2 + 4 * 4) * 63 ** 3 * 8
+    assert t["field_bytes"] == (2 + 3 * 4) * 63 ** 3 * 8
     assert t["halo_bytes"] == 0
 
 

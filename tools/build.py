@@ -38,6 +38,8 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unus
 HIP_FLAGS = COMMON + [f"--offload-arch={ARCH}", "-fno-gpu-rdc", "-munsafe-fp-atomics"]
 # (perf-attribution experiments only: e.g. W3D_EXTRA_DEFS=-DW3D_EXPERIMENT_NOLOAD builds a variant whose results are wrong)
 HIP_FLAGS += os.environ.get("W3D_EXTRA_DEFS", "").split()
+# (... and W3D_EXTRA_DEFS_P2 for the pair-tiled pass's translation units only: a variant rebuilds 5 objects, not all)
+P2_EXTRA = os.environ.get("W3D_EXTRA_DEFS_P2", "").split()
 # x86-64-v3: std::fma (stencil.hpp) is one vfmadd instruction, not a libm call
 CPU_FLAGS = COMMON + ["-fopenmp", "-march=x86-64-v3"]
 
@@ -86,6 +88,8 @@ def _hash_inputs(src: Path, flags: list[str]) -> str:
 def _compile(src_rel: str, kind: str, extra: list[str], force: bool, verbose: bool) -> Path:
     src = CSRC / src_rel
     flags = (HIP_FLAGS if kind == "hip" else CPU_FLAGS) + extra
+    if src_rel.startswith("src/kernels_leapfrog_p2"):
+        flags = flags + P2_EXTRA
     if kind == "hip" and src.suffix == ".cpp":
         flags = flags + ["-x", "hip"]
     tag = _hash_inputs(src, flags)
@@ -130,17 +134,21 @@ def cli_path() -> Path:
     return ROOT / "bin" / "wave3d"
 
 
-def build(jobs: int = 8, force: bool = False, cli: bool = True, verbose: bool = False) -> dict:
+def build(jobs: int = 8, force: bool = False, cli: bool = True, verbose: bool = False, cli_out: str = "") -> dict:
     if not Path(HIPCC).exists():
         raise RuntimeError(f"hipcc not found at {HIPCC}")
     py_inc = _pybind_includes()
-    units = [(s, k, []) for s, k in LIB_SOURCES] + [(s, k, py_inc) for s, k in EXT_SOURCES]
-    if cli:
+    units = [(s, k, []) for s, k in LIB_SOURCES] + ([] if cli_out else [(s, k, py_inc) for s, k in EXT_SOURCES])
+    if cli or cli_out:
         units += [(s, k, []) for s, k in CLI_SOURCES]
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         futs = {s: ex.submit(_compile, s, k, e, force, verbose) for s, k, e in units}
         objs = {s: f.result() for s, f in futs.items()}
     lib_objs = [objs[s] for s, _ in LIB_SOURCES]
+    if cli_out:  # (an experiment build: the CLI alone, at its own path; bin/ and the extension stay as they are)
+        Path(cli_out).parent.mkdir(parents=True, exist_ok=True)
+        _link(lib_objs + [objs[s] for s, _ in CLI_SOURCES], Path(cli_out), shared=False, verbose=verbose)
+        return {"cli": cli_out}
     ext = ext_path()
     _link(lib_objs + [objs[s] for s, _ in EXT_SOURCES], ext, shared=True, verbose=verbose)
     out = {"extension": str(ext)}
@@ -163,10 +171,11 @@ def main() -> int:
     ap.add_argument("--no-cli", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--clean", action="store_true")
+    ap.add_argument("--cli-out", default="", help="experiment builds: link only the CLI, to this path")
     a = ap.parse_args()
     if a.clean and BUILD.exists():
         shutil.rmtree(BUILD)
-    res = build(jobs=a.jobs, force=a.force, cli=not a.no_cli, verbose=a.verbose)
+    res = build(jobs=a.jobs, force=a.force, cli=not a.no_cli, verbose=a.verbose, cli_out=a.cli_out)
     for k, v in res.items():
         print(f"built {k}: {v}")
     return 0

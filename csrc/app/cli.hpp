@@ -34,6 +34,7 @@ struct Args {
   int fake_rank = -1, fake_world = 0;
   bool fake_traffic = false;  // --fake-traffic: the fake rank sends / receives its real messages to itself over RCCL
   int reserve_cus = 0;        // --reserve-cus N: CUs kept off the passes for RCCL's kernels
+  int capture_selftest = -1;  // --capture-selftest M: the capture guard's probe topology M, then exit (tests)
   int group = 0;                       // --group P: all P ranks in this process on one GPU
   int bench_steps = 0;                 // --bench-steps K: timed block of K solves (bench.py contract)
   bool autotune = false;               // --autotune: time the multi-rank schedule candidates, keep the fastest

@@ -64,6 +64,8 @@ constexpr Personality kPersonalities[] = {
                "  --fake-traffic     with --fake-rank: every exchange sends and receives the rank's exact messages to\n"
                "                     itself over a one-rank RCCL communicator (real RCCL kernels and bytes; values wrong)\n"
                "  --reserve-cus N    keep N CUs (a multiple of 8: N/8 per XCD) off the passes for RCCL's copy kernels\n"
+               "  --capture-selftest M  run the stream-capture guard on probe topology M (0 production, 2 the\n"
+               "                     round-4 split it refuses) on this runtime, print the result, exit\n"
                "  --group P          all P ranks of the decomposition in this process on one GPU (rehearsal of the\n"
                "                     multi-rank path; --group-transport rccl-self (default: RCCL send/recv, each rank\n"
                "                     over a one-rank communicator), loopback (device copies) or push)\n"
@@ -153,6 +155,7 @@ Args parse(int argc, char** argv) {
     }
     else if (s == "--fake-traffic") a.fake_traffic = true;
     else if (s == "--reserve-cus") a.reserve_cus = std::stoi(next());
+    else if (s == "--capture-selftest") a.capture_selftest = std::stoi(next());
     else if (s == "--group") a.group = std::stoi(next());
     else if (s == "--bench-steps") a.bench_steps = std::stoi(next());
     else if (s == "--autotune") a.autotune = true;

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "cli.hpp"
+#include "wave3d/capture_guard.hpp"
 #include "wave3d/cpu.hpp"
 #include "wave3d/cpu_dist.hpp"
 #include "wave3d/runtime.hpp"
@@ -210,6 +211,10 @@ int run_gpu(const Args& a) {
   W3D_HIP(hipSetDevice(dev));
   hipDeviceProp_t prop;
   W3D_HIP(hipGetDeviceProperties(&prop, dev));
+  if (a.capture_selftest >= 0) {  // (tests: the stream-capture guard on this process's ROCm runtime)
+    std::printf("capture selftest mode %d: %s\n", a.capture_selftest, capture::selftest(a.capture_selftest).c_str());
+    return 0;
+  }
   const SolverOptions base = options_from(a, fake);
   if (a.group > 0) return run_group(a, base, prop);
 

@@ -221,6 +221,15 @@ __device__ __forceinline__ double lds_rd1(const double* p) {
 }
 // (a scheduling fence between stages: the compiler would otherwise hoist later stages' LDS reads into earlier ones
 // and run out of the 128 VGPRs of a 1024-thread workgroup)
+// cache-policy bits of the plane loads / stores (gfx950 CPol: 1 = sc0, 2 = nt, 16 = sc1): non-temporal stores (the new
+// levels are read by the next pass, two planes later at the earliest), default-policy loads (the tile halos are read
+// again by the neighbouring tiles of the same XCD)
+#ifndef P2_STORE_AUX
+#define P2_STORE_AUX 2
+#endif
+#ifndef P2_LOAD_AUX
+#define P2_LOAD_AUX 0
+#endif
 #ifndef P2_NO_SCHED_FENCE
 #define P2_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 #else
@@ -409,7 +418,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
 #else
       const int xs = decltype(bkc)::value ? x : x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
 #endif
-      return as_d2(__builtin_amdgcn_raw_buffer_load_b128(rsrc(f, xs), static_cast<int>(goff), 0, 0));
+      return as_d2(__builtin_amdgcn_raw_buffer_load_b128(rsrc(f, xs), static_cast<int>(goff), 0, P2_LOAD_AUX));
     };
 
     __syncthreads();  // tables
@@ -549,7 +558,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
         if (P2_STORE_ALL || !INIT || winner) {
           const int sso = (xown && winner) ? 0 : static_cast<int>(0x80000000u);
           __builtin_amdgcn_raw_buffer_store_b128(as_u4(v), rsrc(k == S ? p.out2 : p.out1, xp),
-                                                 static_cast<int>(EDGE ? soff : goff), sso, 2 /* nt */);
+                                                 static_cast<int>(EDGE ? soff : goff), sso, P2_STORE_AUX);
         }
 #endif
       }
@@ -605,8 +614,9 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
         const int s1 = (x1 >= wx0 && x1 < wx1) ? 0 : static_cast<int>(0x80000000u);
         const int s2 = (x2 >= wx0 && x2 < wx1) ? 0 : static_cast<int>(0x80000000u);
         const int off = static_cast<int>(EDGE ? soff : goff);
-        __builtin_amdgcn_raw_buffer_store_b128(as_u4(L[S - 1][(F - S + 1 + 8) & 3]), rsrc(p.out1, x1), off, s1, 2);
-        __builtin_amdgcn_raw_buffer_store_b128(as_u4(vS), rsrc(p.out2, x2), off, s2, 2);
+        __builtin_amdgcn_raw_buffer_store_b128(as_u4(L[S - 1][(F - S + 1 + 8) & 3]), rsrc(p.out1, x1), off, s1,
+                                               P2_STORE_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(as_u4(vS), rsrc(p.out2, x2), off, s2, P2_STORE_AUX);
       }
 #endif
     };

@@ -7,6 +7,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "wave3d/capture_guard.hpp"
 #include "wave3d/cpu.hpp"
 #include "wave3d/decomp.hpp"
 #include "wave3d/kernels.hpp"
@@ -400,6 +401,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("target_blocks", &LeapfrogTbTiling::target_blocks)
       .def_readwrite("min_chunk", &LeapfrogTbTiling::min_chunk)
       .def_readwrite("p2", &LeapfrogTbTiling::p2);
+  m.def("capture_guard_selftest", &wave3d::capture::selftest, py::arg("mode"),
+        "the probe topologies through the stream-capture guard (0: production, 2: the round-4 sibling wait)");
   m.def("gpu_leapfrog_p2_supported", &leapfrog_p2_supported);
   m.def("gpu_leapfrog_tb_lds_bytes", &leapfrog_tb_lds_bytes);
   m.def("gpu_leapfrog_tb_partials", &leapfrog_tb_partials);

@@ -1,4 +1,5 @@
 // GPU solver runtime. See wave3d/solver.hpp.
+#include "wave3d/capture_guard.hpp"
 #include "wave3d/solver.hpp"
 
 #include <rccl/rccl.h>
@@ -771,14 +772,14 @@ void GpuSolver::unit_shell(int i) {
       build_msgs(i);
       hipStream_t xs = xstream();
       if (opt_.shells_concurrent) {
-        W3D_HIP(hipEventRecord(ev_shell_, s0_));  // (the unit's inputs are ready: fork)
-        W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
+        capture::record(ev_shell_, s0_);  // (the unit's inputs are ready: fork)
+        capture::wait(xs, ev_shell_);
         for (const LBox& b : tb_shells(i)) tb_pass(u, b, kPhaseShell, xs);
       } else {
         // (serial: the shells own the GPU and finish first, so the exchange starts as early as possible)
         for (const LBox& b : tb_shells(i)) tb_pass(u, b, kPhaseShell, s0_);
-        W3D_HIP(hipEventRecord(ev_shell_, s0_));
-        W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
+        capture::record(ev_shell_, s0_);
+        capture::wait(xs, ev_shell_);
       }
       return;
     }
@@ -790,7 +791,7 @@ void GpuSolver::unit_shell(int i) {
   }
   if (needs_exchange(i)) {
     build_msgs(i);
-    W3D_HIP(hipEventRecord(ev_shell_, s0_));
+    capture::record(ev_shell_, s0_);
   }
 }
 
@@ -854,10 +855,10 @@ void GpuSolver::unit_exchange_rccl(int i) {
   if (!needs_exchange(i)) return;
   hipStream_t xs = xstream();
   // (deep-tb: the shells ran on xs itself, after its wait for the unit's inputs)
-  if (xs != s0_ && mode_ != Mode::kDeepTb) W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
+  if (xs != s0_ && mode_ != Mode::kDeepTb) capture::wait(xs, ev_shell_);
   if (opt_.poison_ghosts) poison(xs);
   timed(kPhaseComm, xs, [&] { exchange(xs); });
-  if (xs != s0_) W3D_HIP(hipEventRecord(ev_halo_, xs));
+  if (xs != s0_) capture::record(ev_halo_, xs);
 }
 
 // One LDS S-step pass of unit u over `box` on stream st (s0 unless given). Its checked levels' partials go to slot
@@ -995,7 +996,7 @@ void GpuSolver::unit_interior(int i) {
     if (!b.empty()) tb_pass(u, b, kPhaseCompute);
     // (the shells ran on the side stream: join it before the reductions read their partials)
     if (wait) {
-      W3D_HIP(hipStreamWaitEvent(s0_, ev_halo_, 0));
+      capture::wait(s0_, ev_halo_);
       joined = true;
     }
     const int slots = mode_ == Mode::kDeepTb ? kTbSlots : 1;
@@ -1030,7 +1031,7 @@ void GpuSolver::unit_interior(int i) {
     });
     np = n_full_;
   }
-  if (wait && !joined) W3D_HIP(hipStreamWaitEvent(s0_, ev_halo_, 0));
+  if (wait && !joined) capture::wait(s0_, ev_halo_);
   if (chk && np > 0) timed(kPhaseCheck, s0_, [&] { launch_reduce(partials_, np, errlog_ + nc, s0_); });
   if (opt_.debug_sync) W3D_HIP(hipDeviceSynchronize());
   if (u.fused()) {
@@ -1118,16 +1119,16 @@ void GpuSolver::collect_phases(RunResult& r) {
 void GpuSolver::lb_pack(int i) {
   if (!needs_exchange(i)) return;
   hipStream_t xs = xstream();
-  if (xs != s0_ && mode_ != Mode::kDeepTb) W3D_HIP(hipStreamWaitEvent(xs, ev_shell_, 0));
+  if (xs != s0_ && mode_ != Mode::kDeepTb) capture::wait(xs, ev_shell_);
   pack_halo(xs);
-  W3D_HIP(hipEventRecord(ev_packed_, xs));
+  capture::record(ev_packed_, xs);
 }
 
 void GpuSolver::lb_pull(int i, const std::vector<GpuSolver*>& ranks, hipEvent_t all_packed) {
   if (!needs_exchange(i)) return;
   hipStream_t xs = xstream();
   if (opt_.poison_ghosts) poison(xs);
-  W3D_HIP(hipStreamWaitEvent(xs, all_packed, 0));  // every peer's faces are packed
+  capture::wait(xs, all_packed);  // every peer's faces are packed
   if (comm_) {  // rccl-self: the production exchange (RCCL send/recv on xs) over this rank's one-rank communicator
     timed(kPhaseComm, xs, [&] { exchange(xs, &ranks); });
   } else {
@@ -1138,15 +1139,15 @@ void GpuSolver::lb_pull(int i, const std::vector<GpuSolver*>& ranks, hipEvent_t 
     }
     unpack_halo(xs);
   }
-  W3D_HIP(hipEventRecord(ev_halo_, xs));
+  capture::record(ev_halo_, xs);
 }
 
 void GpuSolver::lb_fence(int i, hipEvent_t all_pulled) {
   // the peers have read this rank's send regions once their pulls are done: keep both streams behind them (the side
   // stream only when this schedule uses it: a captured stream that only ever waits trips HIP 7.2's end of capture)
   if (!needs_exchange(i)) return;
-  W3D_HIP(hipStreamWaitEvent(s0_, all_pulled, 0));
-  if (xstream() != s0_) W3D_HIP(hipStreamWaitEvent(s1_, all_pulled, 0));
+  capture::wait(s0_, all_pulled);
+  if (xstream() != s0_) capture::wait(s1_, all_pulled);
 }
 
 void GpuSolver::gather_errors(RunResult& r) {
@@ -1206,13 +1207,17 @@ RunResult GpuSolver::run() {
     bool ok = hipStreamBeginCapture(s0_, hipStreamCaptureModeThreadLocal) == hipSuccess;
     std::string thrown;
     if (ok) {
+      capture::begin(s0_);  // (every cross-stream wait checked: wave3d/capture_guard.hpp)
       try {
         enqueue_solve();
+        capture::finish();
       } catch (const std::exception& ex) {
         ok = false;
         thrown = ex.what();
+        capture::close();
       }
       const hipError_t e = hipStreamEndCapture(s0_, &g);
+      capture::abandon();
       ok = ok && e == hipSuccess && g != nullptr;
     }
     // (an error of the schedule itself is not a capture problem: report it instead of retrying eagerly on streams the
@@ -1672,15 +1677,15 @@ void GpuGroup::enqueue() {
     bool any = false;
     for (auto* s : rs)
       if (s->needs_exchange(i)) {
-        W3D_HIP(hipStreamWaitEvent(gs_, s->ev_packed_, 0));
+        capture::wait(gs_, s->ev_packed_);
         any = true;
       }
-    if (any) W3D_HIP(hipEventRecord(all_packed_, gs_));
+    if (any) capture::record(all_packed_, gs_);
     for (auto* s : rs) s->lb_pull(i, rs, all_packed_);
     step("pull", i);
     for (auto* s : rs)
-      if (s->needs_exchange(i)) W3D_HIP(hipStreamWaitEvent(gs_, s->ev_halo_, 0));
-    if (any) W3D_HIP(hipEventRecord(all_pulled_, gs_));
+      if (s->needs_exchange(i)) capture::wait(gs_, s->ev_halo_);
+    if (any) capture::record(all_pulled_, gs_);
     for (auto* s : rs) s->lb_fence(i, all_pulled_);
     step("fence", i);
     if (!late)
@@ -1700,11 +1705,11 @@ void GpuGroup::enqueue() {
 void GpuGroup::join() {
   for (size_t q = 0; q < ranks_.size(); ++q) {
     GpuSolver* s = ranks_[q].get();
-    W3D_HIP(hipEventRecord(join_[2 * q], s->s0_));
-    W3D_HIP(hipStreamWaitEvent(gs_, join_[2 * q], 0));
+    capture::record(join_[2 * q], s->s0_);
+    capture::wait(gs_, join_[2 * q]);
     if (s->xstream() != s->s0_) {
-      W3D_HIP(hipEventRecord(join_[2 * q + 1], s->s1_));
-      W3D_HIP(hipStreamWaitEvent(gs_, join_[2 * q + 1], 0));
+      capture::record(join_[2 * q + 1], s->s1_);
+      capture::wait(gs_, join_[2 * q + 1]);
     }
   }
 }
@@ -1753,19 +1758,23 @@ RunResult GpuGroup::run() {
     bool ok = hipStreamBeginCapture(gs_, hipStreamCaptureModeThreadLocal) == hipSuccess;
     if (dbg) std::fprintf(stderr, "[group] begin capture ok=%d\n", ok ? 1 : 0);
     if (ok) {
+      capture::begin(gs_);
       try {
-        W3D_HIP(hipEventRecord(fork_, gs_));
+        capture::record(fork_, gs_);
         for (auto* s : rs) {
-          W3D_HIP(hipStreamWaitEvent(s->s0_, fork_, 0));
-          if (s->xstream() != s->s0_) W3D_HIP(hipStreamWaitEvent(s->s1_, fork_, 0));
+          capture::wait(s->s0_, fork_);
+          if (s->xstream() != s->s0_) capture::wait(s->s1_, fork_);
         }
         enqueue();
         join();
+        capture::finish();
       } catch (const std::exception& ex) {
         if (dbg) std::fprintf(stderr, "[group] capture enqueue failed: %s\n", ex.what());
         ok = false;
+        capture::close();
       }
       const hipError_t e = hipStreamEndCapture(gs_, &g);
+      capture::abandon();
       if (dbg) std::fprintf(stderr, "[group] end capture: %s graph=%p\n", hipGetErrorString(e), (void*)g);
       ok = ok && e == hipSuccess && g != nullptr;
     }

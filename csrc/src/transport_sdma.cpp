@@ -37,6 +37,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "wave3d/capture_guard.hpp"
 #include "wave3d/solver.hpp"
 
 namespace wave3d {
@@ -248,11 +249,11 @@ void GpuSolver::unit_exchange_sdma(int i) {
     // per copy stream: wait until its links' receivers have finished with the regions the copies overwrite, copy,
     // then raise the links' "arrived" words with 4-byte copy-engine writes behind the data (stream order: after the
     // copies have completed; no compute queue is held while the copies run)
-    W3D_HIP(hipEventRecord(xfork_, xs));
+    capture::record(xfork_, xs);
     const size_t P = static_cast<size_t>(lay_.plane), nc = xcs_.size();
     for (size_t c = 0; c < nc; ++c) {
       hipStream_t cs = xcs_[c];
-      W3D_HIP(hipStreamWaitEvent(cs, xfork_, 0));
+      capture::wait(cs, xfork_);
       FlagOp w, none;
       w.value = i == 0 ? xend(1 - xpar_) : xval(i - 1);
       w.status = reinterpret_cast<unsigned*>(errlog_);
@@ -281,11 +282,11 @@ void GpuSolver::unit_exchange_sdma(int i) {
       const unsigned* val = xvals_ + xpar_ * (prob_.K + 1) + i;  // (= xval(i))
       for (size_t k = c; k < xlinks_.size(); k += nc)
         W3D_HIP(hipMemcpyAsync(xsig(xlinks_[k], 0), val, sizeof(unsigned), hipMemcpyDeviceToDeviceNoCU, cs));
-      W3D_HIP(hipEventRecord(xcev_[c], cs));
-      W3D_HIP(hipStreamWaitEvent(xs, xcev_[c], 0));
+      capture::record(xcev_[c], cs);
+      capture::wait(xs, xcev_[c]);
     }
   });
-  if (xs != s0_) W3D_HIP(hipEventRecord(ev_halo_, xs));
+  if (xs != s0_) capture::record(ev_halo_, xs);
 }
 
 // s0, before unit i: the ghosts of exchange i − 1 have arrived (block: unpack them), then the regions exchange i

@@ -1,5 +1,6 @@
 """End-to-end native GPU solver: golden log, oracle, bit-exact vs CPU, graph == eager, native code actually loaded."""
 import math
+import os
 
 import pytest
 import torch
@@ -148,3 +149,22 @@ def test_run_batch_pipelined_logs(gpu):
             assert r.steps == r1.steps and r.max_err == r1.max_err
             assert r.rms_err == r1.rms_err and r.solve_s > 0 and r.finite
         assert s.field_hash(0) == h1
+
+
+def test_capture_guard_refuses_the_round4_split(gpu):
+    """HIP 7.2's hipStreamEndCapture crashes (SIGSEGV in the runtime) when a stream forked from a
+    non-origin stream waits on its sibling's event inside a capture (tools/probes/capture_probe3.hip modes 2 and 5,
+    profiles/r5/capture/). Every cross-stream wait of a captured schedule goes through wave3d::capture::wait, which
+    refuses that wait before it enters the capture; the production topology captures and replays. Run in bin/wave3d
+    (the system ROCm 7.2 runtime: the HIP 7.0 runtime PyTorch bundles does not capture multi-stream schedules at all)."""
+    import subprocess
+
+    cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bin", "wave3d")
+
+    def run(m):
+        return subprocess.run([cli, "64", "0.001", "20", "--capture-selftest", str(m)], check=True, timeout=60,
+                              capture_output=True, text=True).stdout
+
+    assert "mode 0: ok" in run(0)
+    out = run(2)
+    assert "capture topology refused" in out and "sibling" in out

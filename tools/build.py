@@ -57,6 +57,7 @@ LIB_SOURCES = [
     ("src/kernels_leapfrog_p2_s4.hip", "hip"),
     ("src/kernels_leapfrog_p2_s5.hip", "hip"),
     ("src/solver_gpu.cpp", "hip"),
+    ("src/capture_guard.cpp", "hip"),
     ("src/transport_sdma.cpp", "hip"),
     ("src/runtime_launch.cpp", "hip"),
     ("src/runtime_io.cpp", "hip"),

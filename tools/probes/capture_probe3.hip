@@ -10,6 +10,9 @@
 //   mode 2  round-4 split: two copy streams per face (4), the signal stream waits for its sibling's event first
 //   mode 3  split, joined through the origin: both copy streams join xs, the signal goes out on xs itself
 //   mode 4  split, second fork: both join xs, xs forks again to the signal stream (a fresh event)
+//   mode 5  mode 2 (sibling wait) plus a direct join of the first copy stream into xs
+//   mode 6  the in-process group's pattern: b waits on a once before its own work (a sibling event, then b's own work),
+//           both join xs directly
 // Prints the step before every capture-level call so a crash names it. Build:
 //   hipcc --offload-arch=gfx950 -O2 tools/probes/capture_probe3.hip -o build/probes/capture_probe3
 #include <hip/hip_runtime.h>
@@ -101,11 +104,18 @@ int main(int argc, char** argv) {
       copy(a, 2 * face);
       copy(b, 2 * face + 1);
       CK(hipEventRecord(ea, a));
-      if (mode == 2) {  // sibling-to-sibling: b waits for a, then raises the signal behind both
+      if (mode == 2 || mode == 5) {  // sibling-to-sibling: b waits for a, then raises the signal behind both
         step("sibling wait", mode, u);
         CK(hipStreamWaitEvent(b, ea, 0));
         signal(b, face);
         CK(hipEventRecord(eb, b));
+        CK(hipStreamWaitEvent(xs, eb, 0));
+        if (mode == 5) CK(hipStreamWaitEvent(xs, ea, 0));
+      } else if (mode == 6) {
+        CK(hipStreamWaitEvent(b, ea, 0));
+        signal(b, face);
+        CK(hipEventRecord(eb, b));
+        CK(hipStreamWaitEvent(xs, ea, 0));
         CK(hipStreamWaitEvent(xs, eb, 0));
       } else {
         CK(hipEventRecord(eb, b));

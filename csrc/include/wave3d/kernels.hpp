@@ -9,6 +9,8 @@
 //   k_pack/unpack : strided y/z halo faces ↔ contiguous RCCL staging buffers (reference kernel K6).
 #pragma once
 
+#include <vector>
+
 #include <hip/hip_runtime.h>
 
 #include "wave3d/cpu.hpp"
@@ -156,6 +158,9 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
 // launch_leapfrog_tb dispatches to it when tiling.p2 is set and it applies.
 bool leapfrog_p2_supported(const Layout& l, const LBox& box, int stages);
 int leapfrog_p2_partials(const Layout& l, const LBox& box, const LeapfrogTbTiling& t);
+// (tests) the pair-tiled pass's thread → position table for S stages (kNT descriptors: (a+2) | (b+2)<<8 | lv<<16 |
+// kind<<20) and its geometry {E, HY, HZ, PZ, tile, LDS bytes at xlen 512 (pass, analytic start), max xlen (same)}
+std::vector<int> leapfrog_p2_table(int stages, std::vector<long>* geometry = nullptr);
 void leapfrog_p2_prepare();
 void launch_leapfrog_p2(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
                         double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,

@@ -17,7 +17,7 @@ namespace p2k {
 
 constexpr int kT = 32;      // output tile edge (y and z)
 constexpr int kNT = 1024;   // threads per workgroup: 16 waves, 4 per SIMD (128 VGPRs each)
-constexpr int kTabWave = 15;  // the wave that tabulates the check's row factors (it holds no positions)
+constexpr int kTabWave = 15;  // the wave that holds no positions
 constexpr unsigned kOob = 0xFFFFFFF0u;  // buffer offset beyond every plane: loads return 0, stores are dropped
 
 // Geometry of an S-step tile (region coordinates: row a = y − (ty0 − (S−1)), z_r = z − (tz0 − E)).
@@ -69,7 +69,7 @@ constexpr int p2_nxt(int xlen) {
 //   * the remaining region pairs in "onion" order (pairs needed by more stages first), 64 per wave, each wave computing
 //     only the stages its deepest pair needs; the chunks go to the SIMD (wave w ↦ SIMD w mod 4) with the least stage
 //     work so far — the four SIMDs end within one stage-set of each other;
-//   * the u^n ring pairs fill two of the remaining waves; wave 15 tabulates the check's row factors.
+//   * the u^n ring pairs fill two of the remaining waves; wave 15 holds no positions (it only loads the tables).
 // Idle lanes of a partial wave duplicate that wave's first pair (same loads, same values to the same LDS slot).
 struct Tab {
   int d[kNT];
@@ -219,8 +219,6 @@ __device__ __forceinline__ double lds_rd1(const double* p) {
   typedef __attribute__((address_space(3))) const volatile double lds_vd;  // a ds_read_b64, never paired
   return *(lds_vd*)p;
 }
-// (a scheduling fence between stages: the compiler would otherwise hoist later stages' LDS reads into earlier ones
-// and run out of the 128 VGPRs of a 1024-thread workgroup)
 // cache-policy bits of the plane loads / stores (gfx950 CPol: 1 = sc0, 2 = nt, 16 = sc1): non-temporal stores (the new
 // levels are read by the next pass, two planes later at the earliest), default-policy loads (the tile halos are read
 // again by the neighbouring tiles of the same XCD)
@@ -230,6 +228,8 @@ __device__ __forceinline__ double lds_rd1(const double* p) {
 #ifndef P2_LOAD_AUX
 #define P2_LOAD_AUX 0
 #endif
+// (a scheduling fence between stages: the compiler would otherwise hoist later stages' LDS reads into earlier ones
+// and run out of the 128 VGPRs of a 1024-thread workgroup)
 #ifndef P2_NO_SCHED_FENCE
 #define P2_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 #else
@@ -306,6 +306,9 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
   // plane i+2 into the slot stage 1 just consumed (two u^{n−1} slots), u^n plane i+3 into plane i−1's slot (dead after
   // stage 2); twice the bytes in flight per CU. Measured 2.7 % slower per solve (head-loop spills; the loads were not
   // what held the pass back: profiles/r5/p2_attribution.md)
+#ifndef P2_LAM_MASK  // (A/B: 0 = the Dirichlet selects after every stage, the round-5 first version)
+#define P2_LAM_MASK 1
+#endif
 #ifndef P2_DEFER_STORE  // (experiment, off: measured 3.7 % slower per solve, profiles/r5/store_experiments.md)
 #define P2_DEFER_STORE 0
 #endif
@@ -316,7 +319,9 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
 #ifndef P2_DEEP
 #define P2_DEEP 0
 #endif
-  constexpr bool kDeep = kLate && S == 5 && P2_DEEP;
+  // (P2_DEEP: 1 = both fields, 2 = u^n only, 3 = u^{n−1} only)
+  constexpr bool kDeepPrev = kLate && S == 5 && (P2_DEEP == 1 || P2_DEEP == 3);
+  constexpr bool kDeepCur = kLate && S == 5 && (P2_DEEP == 1 || P2_DEEP == 2);
   extern __shared__ double lds[];
   const int tid = static_cast<int>(threadIdx.x);
   int blk = static_cast<int>(blockIdx.x);
@@ -387,6 +392,9 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     const bool sty = inner && y < p.y1 && z < p.z1;      // own pair stored (z + 1 ≤ z1: the box spans the z interior)
     const unsigned soff = sty ? goff : kOob;
     const bool okl = sty && rl, okh = sty && rh && z + 1 < p.z1;  // own + real: checked
+#if P2_LAM_MASK
+    const double lam_lo = rl ? p.tau2 : 0.0, lam_hi = rh ? p.tau2 : 0.0;  // (τ² per node: 0 on Dirichlet nodes)
+#endif
     // per-thread LDS byte bases (all accesses: a compile-time offset from one of them)
     const int lo0 = (a + 1) * R0 + (b + 1);     // level-0 / φ slot index of the pair
     const int lk = a * R1 + b;                  // compact slot index (region pairs)
@@ -503,12 +511,20 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
         }
         const double lapl = d2sum(c.x, xm.x, xq.x, ym.x, yp.x, zm, c.y);
         const double laph = d2sum(c.y, xm.y, xq.y, ym.y, yp.y, c.x, zq);
-        const D2 o = k == 1 ? Lm[(kLate && !kDeep) ? 0 : (D & 1)] : L[k > 1 ? k - 2 : 0][s0];
+        const D2 o = k == 1 ? Lm[(kLate && !kDeepPrev) ? 0 : (D & 1)] : L[k > 1 ? k - 2 : 0][s0];
+#if P2_LAM_MASK
+        // Dirichlet nodes through τ²: a node outside the global interior has τ² = 0 and c = old = +0 at every level
+        // (zero loads, zero φ, and this very update), so fma(0, Δ, fma(2, +0, −(+0))) = +0 — the select's value, bit
+        // for bit, without the 4 selects per pair and stage
+        v = D2m(leapfrog(c.x, o.x, lapl, lam_lo), leapfrog(c.y, o.y, laph, lam_hi));
+        (void)EDGE;
+#else
         v = D2m(leapfrog(c.x, o.x, lapl, p.tau2), leapfrog(c.y, o.y, laph, p.tau2));
         if constexpr (EDGE) {
           v.x = rl ? v.x : 0.0;
           v.y = rh ? v.y : 0.0;
         }
+#endif
         if constexpr (!BK) {
           if (!xreal(xp)) v = D2m(0.0, 0.0);
         }
@@ -591,7 +607,15 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
           u.y = rh ? u.y : 0.0;
         }
         if (!xin) u = D2m(0.0, 0.0);
+#if P2_LAM_MASK
+        if constexpr (EDGE) {  // (u⁰ = φ is not 0 on every Dirichlet node — s(N) = sin(π) — so it is zeroed here)
+          Lm[(F + 1) & 1] = D2m(rl ? f1.x : 0.0, rh ? f1.y : 0.0);
+        } else {
+          Lm[(F + 1) & 1] = f1;
+        }
+#else
         Lm[(F + 1) & 1] = f1;
+#endif
       } else if (act) {
         wr2(b0, o0(s3, 0, 0), f3);
         u = u1_pair(i + 2);
@@ -649,16 +673,21 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
           i - (K - 1));                                                                                           \
     P2_SCHED_FENCE();                                                                                             \
   }
+#ifdef P2_CUR_EARLY  // (experiment: u^n plane i+2 loaded before stage 1 — its slot, plane i−2's, is already dead)
+      if constexpr (kLate && !kDeepCur) L[0][(F + 2) & 3] = load_pair(bkc, p.cur, i + 2);
+#endif
       W3D_P2_STAGE(1)
-      if constexpr (kDeep)
+      if constexpr (kDeepPrev)
         Lm[F & 1] = load_pair(bkc, p.prev, i + 2);
       else if constexpr (kLate)
         Lm[0] = load_pair(bkc, p.prev, i + 1);  // (its register freed by stage 1)
       W3D_P2_STAGE(2)
-      if constexpr (kDeep)
+      if constexpr (kDeepCur)
         L[0][(F + 3) & 3] = load_pair(bkc, p.cur, i + 3);
+#ifndef P2_CUR_EARLY
       else if constexpr (kLate)
         L[0][(F + 2) & 3] = load_pair(bkc, p.cur, i + 2);
+#endif
       W3D_P2_STAGE(3)
       W3D_P2_STAGE(4)
       W3D_P2_STAGE(5)
@@ -677,7 +706,12 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
           wr2(b0, o0(3, 0, 0), phi_pair(i0 + 1));
           wr2(b0, o0(2, 0, 0), phi_pair(i0 + 2));
         }
-        if (reg) Lm[0] = phi_pair(i0);
+        if (reg) {
+          Lm[0] = phi_pair(i0);
+#if P2_LAM_MASK
+          Lm[0] = D2m(rl ? Lm[0].x : 0.0, rh ? Lm[0].y : 0.0);  // (see init_iter)
+#endif
+        }
       } else {
         L[0][3] = load_pair(Gen{}, p.cur, i0 - 1);
         L[0][0] = load_pair(Gen{}, p.cur, i0);
@@ -686,10 +720,8 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
       if constexpr (!INIT) {
         L[0][1] = load_pair(Gen{}, p.cur, i0 + 1);
         Lm[0] = load_pair(Gen{}, p.prev, i0);
-        if constexpr (kDeep) {
-          L[0][2] = load_pair(Gen{}, p.cur, i0 + 2);
-          Lm[1] = load_pair(Gen{}, p.prev, i0 + 1);
-        }
+        if constexpr (kDeepCur) L[0][2] = load_pair(Gen{}, p.cur, i0 + 2);
+        if constexpr (kDeepPrev) Lm[1] = load_pair(Gen{}, p.prev, i0 + 1);
       }
       // head blocks (general) until the first block inside the bulk range, bulk blocks, then the general tail
       const int blo = max(max(wx0, p.sx0), 1 - p.gx0) + (S - 1);

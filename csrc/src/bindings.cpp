@@ -403,6 +403,11 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("p2", &LeapfrogTbTiling::p2);
   m.def("capture_guard_selftest", &wave3d::capture::selftest, py::arg("mode"),
         "the probe topologies through the stream-capture guard (0: production, 2: the round-4 sibling wait)");
+  m.def("leapfrog_p2_table", [](int stages) {
+        std::vector<long> geo;
+        std::vector<int> t = wave3d::leapfrog_p2_table(stages, &geo);
+        return py::make_tuple(t, geo);
+      }, py::arg("stages"), "the pair-tiled pass's compile-time thread table and geometry (host copy, no GPU)");
   m.def("gpu_leapfrog_p2_supported", &leapfrog_p2_supported);
   m.def("gpu_leapfrog_tb_lds_bytes", &leapfrog_tb_lds_bytes);
   m.def("gpu_leapfrog_tb_partials", &leapfrog_tb_partials);

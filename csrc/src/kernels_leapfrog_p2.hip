@@ -141,6 +141,28 @@ int leapfrog_p2_partials(const Layout& l, const LBox& box, const LeapfrogTbTilin
   return make_plan_p2(l, box, t1, real, false).nblocks;
 }
 
+std::vector<int> leapfrog_p2_table(int stages, std::vector<long>* geometry) {
+  auto one = [&](auto sc) {
+    constexpr int S = decltype(sc)::value;
+    using G = p2k::Geo<S>;
+    constexpr p2k::TabBuild<S> t = p2k::make_tab<S>();
+    if (geometry)
+      *geometry = {G::E, G::HY, G::HZ, G::PZ, p2k::kT,
+                   static_cast<long>(p2k::p2_lds_bytes<false, S>(p2k::p2_nxt<S>(512))),
+                   S <= 4 ? static_cast<long>(p2k::p2_lds_bytes<true, S>(p2k::p2_nxt<S>(512))) : 0L,
+                   static_cast<long>(p2_max_xlen(S, false)), S <= 4 ? static_cast<long>(p2_max_xlen(S, true)) : 0L};
+    return std::vector<int>(t.t.d, t.t.d + p2k::kNT);
+  };
+  switch (stages) {
+    case 2: return one(std::integral_constant<int, 2>{});
+    case 3: return one(std::integral_constant<int, 3>{});
+    case 4: return one(std::integral_constant<int, 4>{});
+    case 5: return one(std::integral_constant<int, 5>{});
+    default: fail("leapfrog_p2_table: stages must be 2..5");
+  }
+  return {};
+}
+
 void leapfrog_p2_prepare() {
   prepare_p2_s2();
   prepare_p2_s3();

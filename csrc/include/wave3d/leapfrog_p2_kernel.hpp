@@ -298,9 +298,9 @@ template <int S, int CM, bool INIT, bool CH>
 __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
   using G = Geo<S>;
   constexpr int E = G::E, R0 = G::R0, R1 = G::R1;
-  // late loads (S ≥ 4): u^{n−1} plane i+1 is loaded after stage 1 (into the register stage 1 just consumed) and u^n
-  // plane i+2 after stage 2 (plane i−1's slot is dead by then): 8 VGPRs fewer at the stage peak, and the vector-memory
-  // sequence of an iteration is loads, loads, stores — the next commit waits for its load, never for a store
+  // late loads (S ≥ 4): u^{n−1} plane i+1 is loaded after stage 1 (into the register stage 1 just consumed), u^n plane
+  // i+2 before stage 1 (into plane i−2's dead slot); the vector-memory sequence of an iteration is load, load, stores —
+  // the next commit waits for its load, never for a store
   constexpr bool kLate = !INIT && S >= 4;
   // deep prefetch (experiment, off: -DP2_DEEP=1): the same two load points, each one plane further ahead — u^{n−1}
   // plane i+2 into the slot stage 1 just consumed (two u^{n−1} slots), u^n plane i+3 into plane i−1's slot (dead after
@@ -673,7 +673,11 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
           i - (K - 1));                                                                                           \
     P2_SCHED_FENCE();                                                                                             \
   }
-#ifdef P2_CUR_EARLY  // (experiment: u^n plane i+2 loaded before stage 1 — its slot, plane i−2's, is already dead)
+#ifndef P2_CUR_LATE
+      // u^n plane i+2 right after the commit: its slot (plane i−2's) has been dead since stage 2 of iteration i−1, and
+      // issued here it has the whole iteration (≈ 2 µs) to arrive — after stage 2, as first built, it had ≈ 60 % of one
+      // and the next commit waited for it: −13 % per 5-step pass (profiles/r5/stores/abn_cur_early.log). (Loading it
+      // one iteration earlier still, into the same slot, spills.)
       if constexpr (kLate && !kDeepCur) L[0][(F + 2) & 3] = load_pair(bkc, p.cur, i + 2);
 #endif
       W3D_P2_STAGE(1)
@@ -684,7 +688,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
       W3D_P2_STAGE(2)
       if constexpr (kDeepCur)
         L[0][(F + 3) & 3] = load_pair(bkc, p.cur, i + 3);
-#ifndef P2_CUR_EARLY
+#ifdef P2_CUR_LATE  // (A/B: the first version's load point)
       else if constexpr (kLate)
         L[0][(F + 2) & 3] = load_pair(bkc, p.cur, i + 2);
 #endif

@@ -545,8 +545,9 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
           if (((p.check_mask >> (k - 1)) & 1) && inner && xown) {
             // u_a = ((s_x·s_y)·ct)·s_z (stencil.hpp analytic_row); s_x of the plane: one LDS broadcast read
             const double sxp = sxw[xp + xtab0];
-            const double rf = (sxp * rdd(rt, 0)) * p.ct[k - 1];
-            const D2 sz = rd2(szp, 0);
+            // (the analytic start holds the pair's s_y, s_z, s_z+1 in registers for φ: the same table entries)
+            const double rf = (sxp * (INIT ? fy : rdd(rt, 0))) * p.ct[k - 1];
+            const D2 sz = INIT ? D2m(fzl, fzh) : rd2(szp, 0);
             double e0 = fabs(v.x - rf * sz.x), e1 = fabs(v.y - rf * sz.y);
             if constexpr (EDGE) {
               e0 = okl ? e0 : 0.0;  // (adding 0 leaves max and Σ bit-identical)

@@ -89,6 +89,50 @@ constexpr int pair_level(int a, int b) {
   return lv;
 }
 
+// LDS bank-friendly lane order of a 64-pair chunk (onion / ring waves): lane l gets a pair whose slot index is ≡
+// kTgt[l] (mod 16), so the 16 lanes of each ds_read_b128 group ({0–3,12–15,20–27}, …) hit 16 different 16-byte bank
+// quads and the 8 lanes of each ds_write_b128 block 8 different ones (MI355X_MICROARCH.md §LDS); pairs without a
+// matching lane fill the rest. (Row-major chunks measured 2× the conflict-free LDS cycles: profiles/r5/lds_banks.md.)
+constexpr int kTgt[64] = {0,  1,  2,  3,  4,  5,  6,  7,  0,  1,  2,  3,  4,  5,  6,  7,   //
+                          8,  9,  10, 11, 12, 13, 14, 15, 8,  9,  10, 11, 12, 13, 14, 15,  //
+                          0,  1,  2,  3,  4,  5,  6,  7,  0,  1,  2,  3,  4,  5,  6,  7,   //
+                          8,  9,  10, 11, 12, 13, 14, 15, 8,  9,  10, 11, 12, 13, 14, 15};
+// (the read groups: {0–3,12–15,20–27} gets 0–3, 4–7, 12–15 + 8–11; {4–11,16–19,28–31} gets 4–7, 0–3, 8–11, 12–15 —
+// all 16 residues once; every contiguous 8-lane write block holds residues r and r+4 … distinct mod 8)
+constexpr void bank_order(const int* ea, const int* eb, int n, int rstride, int rbase, int* oa, int* ob) {
+  bool used[64] = {};
+  int lane_e[64] = {};
+  bool filled[64] = {};
+  for (int l = 0; l < 64; ++l) {
+    for (int j = 0; j < n; ++j)
+      if (!used[j] && (((ea[j] + rbase) * rstride + eb[j]) % 16 + 16) % 16 == kTgt[l]) {
+        used[j] = true;
+        lane_e[l] = j;
+        filled[l] = true;
+        break;
+      }
+  }
+  int j = 0;
+  for (int l = 0; l < 64; ++l) {
+    if (filled[l]) continue;
+    while (j < n && used[j]) ++j;
+    if (j < n) {
+      used[j] = true;
+      lane_e[l] = j;
+    } else {
+      lane_e[l] = -1;  // (an idle lane)
+    }
+  }
+  int first = -1;  // idle lanes repeat the pair of the lowest filled lane
+  for (int l = 0; l < 64 && first < 0; ++l)
+    if (lane_e[l] >= 0) first = lane_e[l];
+  for (int l = 0; l < 64; ++l) {
+    const int e = lane_e[l] >= 0 ? lane_e[l] : first;
+    oa[l] = ea[e];
+    ob[l] = eb[e];
+  }
+}
+
 template <int S>
 struct TabBuild {
   Tab t{};
@@ -156,10 +200,10 @@ constexpr TabBuild<S> make_tab() {
     used[w] = true;
     const int lv = ll[c * 64];
     load[best] += lv;
-    for (int l = 0; l < 64; ++l) {
-      const int j = c * 64 + l < n ? c * 64 + l : c * 64;
-      r.t.d[w * 64 + l] = tab_enc(la[j], lb[j], lv, 1);
-    }
+    int oa[64] = {}, ob[64] = {};
+    const int cn = n - c * 64 < 64 ? n - c * 64 : 64;
+    bank_order(la + c * 64, lb + c * 64, cn, G::R1, 0, oa, ob);  // (the compact level planes: most of the accesses)
+    for (int l = 0; l < 64; ++l) r.t.d[w * 64 + l] = tab_enc(oa[l], ob[l], lv, 1);
   }
   // u^n ring: row −1, row HY, then pair columns −1 and PZ
   int ra[4 * kNT / 4] = {}, rb[4 * kNT / 4] = {};
@@ -184,11 +228,17 @@ constexpr TabBuild<S> make_tab() {
   for (int w = 8; w < 16 && q < m; ++w) {
     if (used[w]) continue;
     used[w] = true;
-    const int q0 = q;
-    for (int l = 0; l < 64; ++l) {
-      const int j = q < m ? q++ : q0;
-      r.t.d[w * 64 + l] = tab_enc(ra[j], rb[j], 0, 2);
+    const int cn = m - q < 64 ? m - q : 64;
+    int oa[64] = {}, ob[64] = {};
+    // (ring waves only write the level-0 plane: slot ((a + 1)·R0 + b + 1))
+    int sa[64] = {}, sb[64] = {};
+    for (int l = 0; l < cn; ++l) {
+      sa[l] = ra[q + l];
+      sb[l] = rb[q + l] + 1;
     }
+    bank_order(sa, sb, cn, G::R0, 1, oa, ob);
+    for (int l = 0; l < 64; ++l) r.t.d[w * 64 + l] = tab_enc(oa[l], ob[l] - 1, 0, 2);
+    q += cn;
   }
   r.ring_left = m - q;
   return r;

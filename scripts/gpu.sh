@@ -178,6 +178,9 @@ run_fakesweep() {
         timeout -k 5 120 ./bin/wave3d 512 0.001 20 1 --fake-rank "$r/$P" --decomp "$dec" --no-overlap --repeat 10 \
           --warmup 2 --quiet --json /tmp/fs.json > /dev/null || return 1
         python3 -c "import json,sys;d=json.load(open('/tmp/fs.json'));print(json.dumps({'P':$P,'decomp':'x'.join(map(str,d['dims'])),'schedule':'$dec-seq','rank':$r,'solve_s':d['solve_s']}))" >> "$out" || return 1
+        timeout -k 5 120 ./bin/wave3d 512 0.001 20 1 --fake-rank "$r/$P" --decomp "$dec" --no-overlap --fake-traffic \
+          --repeat 10 --warmup 2 --quiet --json /tmp/fs.json > /dev/null || return 1
+        python3 -c "import json,sys;d=json.load(open('/tmp/fs.json'));print(json.dumps({'P':$P,'decomp':'x'.join(map(str,d['dims'])),'schedule':'$dec-seq-rccltraffic','rank':$r,'solve_s':d['solve_s']}))" >> "$out" || return 1
       done
     done
   done

@@ -37,13 +37,18 @@ def load(path):
     return pts
 
 
-def table(pts, traffic: bool = False):
-    """Fastest schedule per P among the compute-only ones (traffic=False) or the copy-engine ones (True; P = 1 is the
-    one-GPU solve either way)."""
-    t1 = min(v for k, v in pts[1].items() if "sdma" not in k)
+def _kind(sched: str) -> str:
+    return "sdma" if "sdma" in sched else "rccl" if "traffic" in sched else ""
+
+
+def table(pts, traffic=False):
+    """Fastest schedule per P among the compute-only ones (traffic falsy), the copy-engine ones (True or "sdma") or the
+    ones with their RCCL messages sent to themselves ("rccl", round 5 --fake-traffic); P = 1 is the one-GPU solve."""
+    want = "sdma" if traffic is True else (traffic or "")
+    t1 = min(v for k, v in pts[1].items() if not _kind(k))
     rows = []
     for P in sorted(pts):
-        cand = {k: v for k, v in pts[P].items() if P == 1 or (("sdma" in k) == traffic)}
+        cand = {k: v for k, v in pts[P].items() if P == 1 or _kind(k) == want}
         if not cand:
             continue
         sched, t = min(cand.items(), key=lambda kv: kv[1])
@@ -61,7 +66,10 @@ def main(argv=None) -> int:
     rows = table(pts)
     trows = table(pts, traffic=True)
     trows = trows if len(trows) > 1 else []
-    for title, rr in (("compute only", rows), ("with copy-engine traffic on one GPU's engines", trows)):
+    rrows = table(pts, traffic="rccl")
+    rrows = rrows if len(rrows) > 1 else []
+    for title, rr in (("compute only", rows), ("with copy-engine traffic on one GPU's engines", trows),
+                      ("with the rank's RCCL messages sent to itself (--fake-traffic; no xGMI hop)", rrows)):
         if not rr:
             continue
         print(f"\n{title}\n")
@@ -84,6 +92,9 @@ def main(argv=None) -> int:
         if trows:
             a1.plot([r["P"] for r in trows], [r["speedup"] for r in trows], "^-",
                     label="MI355X, fake rank + its copy-engine traffic (one GPU's engines)")
+        if rrows:
+            a1.plot([r["P"] for r in rrows], [r["speedup"] for r in rrows], "v-",
+                    label="MI355X, fake rank + its RCCL messages to itself")
         a1.plot([1, ps[-1]], [1, ps[-1]], ":", color="gray", label="ideal")
         a1.plot(list(REF_S), [REF_S[1] / REF_S[p] for p in REF_S], "s--", label="P100 reference (readme.md:99-100)")
         a1.set_xlabel("GPUs")
@@ -93,6 +104,8 @@ def main(argv=None) -> int:
         a2.plot(ps, [r["eff"] for r in rows], "o-", label="MI355X, per-rank compute")
         if trows:
             a2.plot([r["P"] for r in trows], [r["eff"] for r in trows], "^-", label="MI355X, + copy-engine traffic")
+        if rrows:
+            a2.plot([r["P"] for r in rrows], [r["eff"] for r in rrows], "v-", label="MI355X, + RCCL self-traffic")
         a2.plot(list(REF_S), [REF_S[1] / REF_S[p] / p for p in REF_S], "s--", label="P100 reference")
         a2.set_xlabel("GPUs")
         a2.set_ylabel("efficiency")

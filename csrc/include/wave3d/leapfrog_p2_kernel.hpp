@@ -351,7 +351,11 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
   // late loads (S ≥ 4): u^{n−1} plane i+1 is loaded after stage 1 (into the register stage 1 just consumed), u^n plane
   // i+2 before stage 1 (into plane i−2's dead slot); the vector-memory sequence of an iteration is load, load, stores —
   // the next commit waits for its load, never for a store
+#ifdef P2_NO_LATE  // (experiment: both loads at the iteration start, as the S ≤ 3 passes do)
+  constexpr bool kLate = false;
+#else
   constexpr bool kLate = !INIT && S >= 4;
+#endif
   // deep prefetch (experiment, off: -DP2_DEEP=1): the same two load points, each one plane further ahead — u^{n−1}
   // plane i+2 into the slot stage 1 just consumed (two u^{n−1} slots), u^n plane i+3 into plane i−1's slot (dead after
   // stage 2); twice the bytes in flight per CU. Measured 2.7 % slower per solve (head-loop spills; the loads were not

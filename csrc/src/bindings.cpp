@@ -459,6 +459,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("push_cp_wait", &SolverOptions::push_cp_wait)
       .def_readwrite("sdma", &SolverOptions::sdma)
       .def_readwrite("shells_concurrent", &SolverOptions::shells_concurrent)
+      .def_readwrite("reserve_cus", &SolverOptions::reserve_cus)
+      .def_readwrite("fake_traffic", &SolverOptions::fake_traffic)
       .def_readwrite("fused_pack", &SolverOptions::fused_pack)
       .def_readwrite("sdma_streams", &SolverOptions::sdma_streams)
       .def_readwrite("flag_timeout_s", &SolverOptions::flag_timeout_s)

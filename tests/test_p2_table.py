@@ -79,3 +79,13 @@ def test_p2_lds_budget(S):
     assert 0 < lds <= 160 * 1024 and maxlen >= 512
     if S <= 4:
         assert 0 < lds_init <= 160 * 1024 and maxlen_init >= 512
+
+
+def test_round5_solver_options_exposed():
+    """The round-5 options reach Python with their C++ defaults: 5-step passes, the pair-tiled kernel on, no CUs kept
+    off the passes, no fake-rank self-traffic."""
+    o = C.SolverOptions()
+    assert o.temporal == 5 and o.tiling_tb.p2 is True
+    assert o.reserve_cus == 0 and o.fake_traffic is False
+    o.reserve_cus = 16
+    assert o.reserve_cus == 16

@@ -300,6 +300,14 @@ __device__ __forceinline__ void static_for(Fn&& f) {
   }
 }
 
+// max(|e|, m) in one v_max_f64 with the |·| source modifier (fmax() adds a canonicalising v_max_f64 of the loop-carried
+// accumulator per use; for the finite, non-negative values here both give the same result)
+__device__ __forceinline__ double max_abs(double e, double m) {
+  double r;
+  asm("v_max_f64 %0, |%1|, %2" : "=v"(r) : "v"(e), "v"(m));
+  return r;
+}
+
 // a 16-byte pair (a plain aggregate: HIP's double2 is a union wrapper that SROA does not always split)
 struct D2 {
   double x, y;
@@ -363,6 +371,18 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
 #ifndef P2_LAM_MASK  // (A/B: 0 = the Dirichlet selects after every stage, the round-5 first version)
 #define P2_LAM_MASK 1
 #endif
+#ifndef P2_PREV_RING_OOB  // (A/B: 0 = the ring waves load u^{n−1} too, the round-5 first version)
+#define P2_PREV_RING_OOB 1
+#endif
+#ifndef P2_SPLIT_STORE  // (A/B: 0 = every wave issues both stores, non-owners out of range — the round-5 first version)
+#define P2_SPLIT_STORE 1
+#endif
+#ifndef P2_CHECK_REG  // (0 = the 5-step passes read the own row's s_y and pair's s_z from LDS at every check, as the
+#define P2_CHECK_REG 1  // 4-step load passes do: they have no registers to spare)
+#endif
+#ifndef P2_CHECK_SPLIT  // (A/B: 0 = one accumulator per level with per-plane masks, the round-5 first version)
+#define P2_CHECK_SPLIT 1
+#endif
 #ifndef P2_DEFER_STORE  // (experiment, off: measured 3.7 % slower per solve, profiles/r5/store_experiments.md)
 #define P2_DEFER_STORE 0
 #endif
@@ -370,6 +390,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
 #define P2_STORE_ALL 0
 #endif
   constexpr bool kDefer = !INIT && P2_DEFER_STORE;
+  constexpr bool kSplitSt = !INIT && S == 5 && P2_SPLIT_STORE && !kDefer;
 #ifndef P2_DEEP
 #define P2_DEEP 0
 #endif
@@ -385,10 +406,17 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
   }
   const int ntiles = p.nty * p.ntz;
   const bool active = blk < ntiles * (CH ? p.nxc : 1);
-  double emax[S], esum[S];
+  // error-check accumulators, one per node of the pair (lo, hi) and checked level; a pair's nodes that are not checked
+  // (Dirichlet, or beyond the box) are masked out once, in the reduction, not at every plane
+  // (registers: ≤ 3 checked levels, in the 5-step passes and the 4-step analytic start — the production passes; the
+  // others are at or near 128 VGPRs already)
+  constexpr bool kSplitAcc = P2_CHECK_SPLIT && __builtin_popcount(CM) <= 3 && (S == 5 || (INIT && S == 4));
+  double emax[S][2], esum[S][2];
   static_for<0, S>([&](auto kc) __attribute__((always_inline)) {
-    emax[decltype(kc)::value] = esum[decltype(kc)::value] = 0.0;
+    constexpr int k = decltype(kc)::value;
+    emax[k][0] = esum[k][0] = emax[k][1] = esum[k][1] = 0.0;
   });
+  bool okl = false, okh = false;  // this thread's nodes are own + real: checked
 
   if (active) {
     const int chunk = CH ? blk / ntiles : 0;
@@ -434,6 +462,9 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     // stages this wave computes (a scalar: the stage tests must stay scalar branches, not lane masks)
     int wst = __builtin_amdgcn_readfirstlane(wkind == 1 ? wlv : 0);
     const bool winner = wst == S;               // (scalar) the tile's own pairs
+    // levels this wave checks (a scalar int, re-asserted per iteration like wst: a loop-invariant bool is kept as a
+    // 64-bit lane mask, and each stage's test then cost a v_cndmask + v_cmp pair to negate it)
+    int wchk = __builtin_amdgcn_readfirstlane(winner ? p.check_mask : 0);
 #ifdef P2_STAGGER
     const bool wodd = (__builtin_amdgcn_readfirstlane(tid) >> 6) & 1;
 #endif
@@ -445,7 +476,8 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     const bool rl = ry && inside(p.gz0 + z), rh = ry && inside(p.gz0 + z + 1);
     const bool sty = inner && y < p.y1 && z < p.z1;      // own pair stored (z + 1 ≤ z1: the box spans the z interior)
     const unsigned soff = sty ? goff : kOob;
-    const bool okl = sty && rl, okh = sty && rh && z + 1 < p.z1;  // own + real: checked
+    okl = sty && rl;
+    okh = sty && rh && z + 1 < p.z1;
 #if P2_LAM_MASK
     const double lam_lo = rl ? p.tau2 : 0.0, lam_hi = rh ? p.tau2 : 0.0;  // (τ² per node: 0 on Dirichlet nodes)
 #endif
@@ -458,11 +490,29 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     lchar* bB = bA + 4 * G::P1 * 16;
     lchar* rt = lds_base + (2 * G::pairs(INIT) + a + 2) * 8;                          // check: s_y of the own row
     lchar* szp = lds_base + (2 * G::pairs(INIT) + G::NY + 2 * b + 4) * 8;           // check: own (s_z, s_z+1)
+    // Split stores (kSplitSt): the 8 waves that do not own the tile store level S−1 of the own pairs — lane j of
+    // wave 8 + w the pair of lane j of own wave w, read back from the level's compact LDS plane one iteration after
+    // it was computed — and the own waves store level S only. Every wave then issues exactly one store per iteration,
+    // all of them real (before, each of the 16 waves issued two, half of them with every lane out of range), and the
+    // in-order vmcnt sequence stays the same for every wave. (rt: that pair's compact-slot base; soff2: its offset)
+    unsigned soff2 = kOob;
+    if constexpr (kSplitSt) {
+      const int d2 = p2_desc<S>(tid & (kNT / 2 - 1));
+      const int a2 = (d2 & 0xFF) - 2, b2 = ((d2 >> 8) & 0xFF) - 2;
+      const int y2 = ty0 - (S - 1) + a2, z2 = tz0 - E + 2 * b2, el2 = z2 + p.za;
+      const bool st2 = y2 >= p.ay0 && y2 < p.ay1 && el2 >= 0 && el2 + 2 <= p.pitch && y2 < p.y1 && z2 < p.z1;
+      soff2 = st2 ? static_cast<unsigned>(((y2 + p.ya) * p.pitch + el2) * 8) : kOob;
+      rt = lds_base + (G::lk0(INIT) + a2 * R1 + b2 - R1 - 1) * 16 + 4 * G::P1 * 16;
+    }
     // (re-declared opaque at every iteration: otherwise the loop-invariant "base + offset" of every access is hoisted
     // out of the x march into a register of its own — 15 address VGPRs and spills — instead of the offset field)
     auto opaque_bases = [&]() __attribute__((always_inline)) {
-      asm volatile("" : "+v"(b0), "+v"(bA), "+v"(bB), "+v"(rt), "+v"(szp), "+s"(wst));
+      if constexpr (kSplitSt)
+        asm volatile("" : "+v"(b0), "+v"(bA), "+v"(bB), "+v"(rt), "+s"(wst), "+s"(wchk));
+      else
+        asm volatile("" : "+v"(b0), "+v"(bA), "+v"(bB), "+v"(rt), "+v"(szp), "+s"(wst), "+s"(wchk));
       wst = __builtin_amdgcn_readfirstlane(wst);  // (an asm output is not known uniform: re-assert it)
+      wchk = __builtin_amdgcn_readfirstlane(wchk);
     };
     // slot / neighbour offsets (bytes): level-0 or φ slot s, compact plane pl = (k−1)·2 + parity
     auto o0 = [](int sl, int dy, int dz) constexpr { return sl * G::P0 * 16 + ((dy + 1) * R0 + dz + 1) * 16; };
@@ -470,17 +520,22 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     auto kb = [&](int pl) __attribute__((always_inline)) { return pl < 4 ? bA : bB; };
 
     // plane buffers: base = field + (x + 1)·plane, P·8 bytes (every in-plane offset < P)
-    auto rsrc = [&](const double* f, int xs) __attribute__((always_inline)) {
-      return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(f) + static_cast<i64>(xs + 1) * P, (short)0,
-                                               static_cast<int>(P * 8), 0x00020000);
+    auto rsrc = [&](const double* f, int xs, int bytes) __attribute__((always_inline)) {
+      return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(f) + static_cast<i64>(xs + 1) * P, (short)0, bytes,
+                                               0x00020000);
     };
+    const int pbytes = static_cast<int>(P * 8);
+    // u^{n−1} is read by the region waves only (the stage-1 update); the u^n ring waves get a zero-size descriptor for
+    // it — same instruction sequence, no memory traffic (a scalar: wd is wave-uniform)
+    const int prev_bytes = (((wd >> 20) & 0x3) == 1 || !P2_PREV_RING_OOB) ? pbytes : 0;
     auto load_pair = [&](auto bkc, const double* f, int x) __attribute__((always_inline)) -> D2 {
 #ifdef W3D_EXPERIMENT_NOLOAD  // (perf attribution only, results wrong: every plane load hits one of 4 resident planes)
       const int xs = (x & 3) + 1;
 #else
       const int xs = decltype(bkc)::value ? x : x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
 #endif
-      return as_d2(__builtin_amdgcn_raw_buffer_load_b128(rsrc(f, xs), static_cast<int>(goff), 0, P2_LOAD_AUX));
+      return as_d2(__builtin_amdgcn_raw_buffer_load_b128(rsrc(f, xs, f == p.cur ? pbytes : prev_bytes),
+                                                         static_cast<int>(goff), 0, P2_LOAD_AUX));
     };
 
     __syncthreads();  // tables
@@ -596,21 +651,28 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
             ((CM >> (k - 1)) & 1) != 0;
 #endif
         if constexpr (kChk) {
-          if (((p.check_mask >> (k - 1)) & 1) && inner && xown) {
+          if (((wchk >> (k - 1)) & 1) && xown) {  // (wchk: 0 outside the own waves)
             // u_a = ((s_x·s_y)·ct)·s_z (stencil.hpp analytic_row); s_x of the plane: one LDS broadcast read
             const double sxp = sxw[xp + xtab0];
             // (the analytic start holds the pair's s_y, s_z, s_z+1 in registers for φ: the same table entries)
-            const double rf = (sxp * (INIT ? fy : rdd(rt, 0))) * p.ct[k - 1];
-            const D2 sz = INIT ? D2m(fzl, fzh) : rd2(szp, 0);
-            double e0 = fabs(v.x - rf * sz.x), e1 = fabs(v.y - rf * sz.y);
-            if constexpr (EDGE) {
-              e0 = okl ? e0 : 0.0;  // (adding 0 leaves max and Σ bit-identical)
-              e1 = okh ? e1 : 0.0;
+            constexpr bool kRegF = INIT || (P2_CHECK_REG && S == 5);
+            const double rf = (sxp * (kRegF ? fy : rdd(rt, 0))) * p.ct[k - 1];
+            const D2 sz = kRegF ? D2m(fzl, fzh) : rd2(szp, 0);
+            // (d·d = |d|·|d|; the masks okl / okh are applied in the reduction — per plane they were 4 v_cndmask_b32
+            // and a canonicalising v_max_f64 per pair and level, a quarter of the check's VALU)
+            const double d0 = v.x - rf * sz.x, d1 = v.y - rf * sz.y;
+            if constexpr (kSplitAcc) {
+              emax[k - 1][0] = max_abs(d0, emax[k - 1][0]);
+              esum[k - 1][0] = err_sq_acc(d0, esum[k - 1][0]);
+              emax[k - 1][1] = max_abs(d1, emax[k - 1][1]);
+              esum[k - 1][1] = err_sq_acc(d1, esum[k - 1][1]);
+            } else {  // (4 or 5 checked levels: one accumulator pair per level, masked per plane — no spills)
+              const double e0 = okl ? fabs(d0) : 0.0, e1 = okh ? fabs(d1) : 0.0;
+              emax[k - 1][0] = fmax(e0, emax[k - 1][0]);
+              esum[k - 1][0] = err_sq_acc(e0, esum[k - 1][0]);
+              emax[k - 1][0] = fmax(e1, emax[k - 1][0]);
+              esum[k - 1][0] = err_sq_acc(e1, esum[k - 1][0]);
             }
-            emax[k - 1] = fmax(e0, emax[k - 1]);
-            esum[k - 1] = err_sq_acc(e0, esum[k - 1]);
-            emax[k - 1] = fmax(e1, emax[k - 1]);
-            esum[k - 1] = err_sq_acc(e1, esum[k - 1]);
           }
         }
       }
@@ -620,7 +682,20 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
       if constexpr (k < S) L[k][s0] = v;
 #endif
       if constexpr (k == S && kDefer) vS = v;  // (stored at the start of the next iteration: flush)
-      if constexpr (k >= S - 1 && !kDefer) {
+      if constexpr (kSplitSt && k == S) {
+#ifndef W3D_EXPERIMENT_NOSTORE
+        const int sso = xown ? 0 : static_cast<int>(0x80000000u);
+        if (winner) {
+          __builtin_amdgcn_raw_buffer_store_b128(as_u4(v), rsrc(p.out2, xp, pbytes),
+                                                 static_cast<int>(EDGE ? soff : goff), sso, P2_STORE_AUX);
+        } else {
+          constexpr int pl = (S - 2) * 2 + (D & 1);  // level S−1, plane xp: written by stage S−1 last iteration
+          __builtin_amdgcn_raw_buffer_store_b128(as_u4(rd2(rt, ok_(pl, 0, 0))), rsrc(p.out1, xp, pbytes),
+                                                 static_cast<int>(soff2), sso, P2_STORE_AUX);
+        }
+#endif
+      }
+      if constexpr (k >= S - 1 && !kDefer && !kSplitSt) {
         // Interior tiles: the thread's load offset plus a scalar offset (0 for the own waves' planes, out of range
         // otherwise); edge tiles: the per-lane store offset. Passes that load: every wave stores (non-owners beyond
         // the plane: dropped), so every wave's vector-memory sequence is the same and the compiler's waits for the
@@ -628,7 +703,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
 #ifndef W3D_EXPERIMENT_NOSTORE  // (perf attribution only, results wrong: the pass writes nothing to HBM)
         if (P2_STORE_ALL || !INIT || winner) {
           const int sso = (xown && winner) ? 0 : static_cast<int>(0x80000000u);
-          __builtin_amdgcn_raw_buffer_store_b128(as_u4(v), rsrc(k == S ? p.out2 : p.out1, xp),
+          __builtin_amdgcn_raw_buffer_store_b128(as_u4(v), rsrc(k == S ? p.out2 : p.out1, xp, pbytes),
                                                  static_cast<int>(EDGE ? soff : goff), sso, P2_STORE_AUX);
         }
 #endif
@@ -693,9 +768,9 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
         const int s1 = (x1 >= wx0 && x1 < wx1) ? 0 : static_cast<int>(0x80000000u);
         const int s2 = (x2 >= wx0 && x2 < wx1) ? 0 : static_cast<int>(0x80000000u);
         const int off = static_cast<int>(EDGE ? soff : goff);
-        __builtin_amdgcn_raw_buffer_store_b128(as_u4(L[S - 1][(F - S + 1 + 8) & 3]), rsrc(p.out1, x1), off, s1,
+        __builtin_amdgcn_raw_buffer_store_b128(as_u4(L[S - 1][(F - S + 1 + 8) & 3]), rsrc(p.out1, x1, pbytes), off, s1,
                                                P2_STORE_AUX);
-        __builtin_amdgcn_raw_buffer_store_b128(as_u4(vS), rsrc(p.out2, x2), off, s2, P2_STORE_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(as_u4(vS), rsrc(p.out2, x2, pbytes), off, s2, P2_STORE_AUX);
       }
 #endif
     };
@@ -849,7 +924,12 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     constexpr int k = decltype(kc)::value;
     if constexpr ((CM >> k) & 1) {
       if ((p.check_mask >> k) & 1) {
-        double m = emax[k], sm = esum[k];
+        // (masked nodes hold finite or non-finite garbage: selected away, never added; max(+0, ·) and + 0 are exact)
+        double m = emax[k][0], sm = esum[k][0];
+        if constexpr (kSplitAcc) {
+          m = fmax(okl ? emax[k][0] : 0.0, okh ? emax[k][1] : 0.0);
+          sm = (okl ? esum[k][0] : 0.0) + (okh ? esum[k][1] : 0.0);
+        }
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
           const double om = __shfl_xor(m, o, 64);

@@ -99,7 +99,17 @@ constexpr int kTgt[64] = {0,  1,  2,  3,  4,  5,  6,  7,  0,  1,  2,  3,  4,  5,
                           8,  9,  10, 11, 12, 13, 14, 15, 8,  9,  10, 11, 12, 13, 14, 15};
 // (the read groups: {0–3,12–15,20–27} gets 0–3, 4–7, 12–15 + 8–11; {4–11,16–19,28–31} gets 4–7, 0–3, 8–11, 12–15 —
 // all 16 residues once; every contiguous 8-lane write block holds residues r and r+4 … distinct mod 8)
+#ifndef P2_BANK_ORDER  // (A/B: 0 = row-major lanes, consecutive lanes on consecutive 16-byte pairs in memory)
+#define P2_BANK_ORDER 1
+#endif
 constexpr void bank_order(const int* ea, const int* eb, int n, int rstride, int rbase, int* oa, int* ob) {
+  if (!P2_BANK_ORDER) {
+    for (int l = 0; l < 64; ++l) {
+      oa[l] = ea[l < n ? l : 0];
+      ob[l] = eb[l < n ? l : 0];
+    }
+    return;
+  }
   bool used[64] = {};
   int lane_e[64] = {};
   bool filled[64] = {};
@@ -377,6 +387,9 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
 #ifndef P2_SPLIT_STORE  // (A/B: 0 = every wave issues both stores, non-owners out of range — the round-5 first version)
 #define P2_SPLIT_STORE 1
 #endif
+#ifndef P2_SPLIT_STORE_INIT  // (experiment: the split stores in the 4-step analytic start too)
+#define P2_SPLIT_STORE_INIT 0
+#endif
 #ifndef P2_CHECK_REG  // (0 = the 5-step passes read the own row's s_y and pair's s_z from LDS at every check, as the
 #define P2_CHECK_REG 1  // 4-step load passes do: they have no registers to spare)
 #endif
@@ -390,7 +403,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
 #define P2_STORE_ALL 0
 #endif
   constexpr bool kDefer = !INIT && P2_DEFER_STORE;
-  constexpr bool kSplitSt = !INIT && S == 5 && P2_SPLIT_STORE && !kDefer;
+  constexpr bool kSplitSt = ((!INIT && S == 5) || (INIT && S == 4 && P2_SPLIT_STORE_INIT)) && P2_SPLIT_STORE && !kDefer;
 #ifndef P2_DEEP
 #define P2_DEEP 0
 #endif

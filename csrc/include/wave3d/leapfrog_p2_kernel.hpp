@@ -387,6 +387,9 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
 #ifndef P2_SPLIT_STORE  // (A/B: 0 = every wave issues both stores, non-owners out of range — the round-5 first version)
 #define P2_SPLIT_STORE 1
 #endif
+#ifndef P2_INIT_NOFENCE  // no scheduling fences between the analytic start's stages: it has the registers to overlap
+#define P2_INIT_NOFENCE 1   // one stage's LDS reads with the last one's arithmetic (−2.3 % for that pass, profiles/r5/memops)
+#endif
 #ifndef P2_SPLIT_STORE_INIT  // (experiment: the split stores in the 4-step analytic start too)
 #define P2_SPLIT_STORE_INIT 0
 #endif
@@ -814,7 +817,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
   if constexpr (K <= S) {                                                                                         \
     stage(std::integral_constant<int, K>{}, std::integral_constant<int, (F - (K - 1) + 8) & 3>{}, bkc, ec,        \
           i - (K - 1));                                                                                           \
-    P2_SCHED_FENCE();                                                                                             \
+    if constexpr (!(INIT && P2_INIT_NOFENCE)) P2_SCHED_FENCE();                                                   \
   }
 #ifndef P2_CUR_LATE
       // u^n plane i+2 right after the commit: its slot (plane i−2's) has been dead since stage 2 of iteration i−1, and

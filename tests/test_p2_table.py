@@ -89,3 +89,20 @@ def test_round5_solver_options_exposed():
     assert o.reserve_cus == 0 and o.fake_traffic is False
     o.reserve_cus = 16
     assert o.reserve_cus == 16
+
+
+@pytest.mark.parametrize("S", [4, 5])
+def test_p2_split_store_partners(S):
+    """Split stores (leapfrog_p2_kernel.hpp kSplitSt): thread 512 + t of waves 8-15 stores level S-1 of the pair that
+    thread t of the own waves 0-7 holds (the kernel reads p2_desc(tid & 511)), so the 8 non-owning waves cover the
+    tile's 512 own pairs exactly once, one lane each, and every wave issues one store per plane. The zero-size u^{n-1}
+    descriptor goes to the kind-2 (u^n ring) waves, which compute no stage and so never read u^{n-1}."""
+    tab, geo = C.leapfrog_p2_table(S)
+    E = geo[0]
+    own = {(S - 1 + r, E // 2 + c) for r in range(KT) for c in range(KT // 2)}
+    partners = [_decode(tab[t & 511])[:2] for t in range(512, 1024)]
+    assert sorted(partners) == sorted(own)
+    for w in range(16):
+        a, b, lv, kind = _decode(tab[w * 64])
+        if kind == 2:
+            assert lv == 0

@@ -387,6 +387,9 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
 #ifndef P2_SPLIT_STORE  // (A/B: 0 = every wave issues both stores, non-owners out of range — the round-5 first version)
 #define P2_SPLIT_STORE 1
 #endif
+#ifndef P2_INIT_PHIQ  // (analytic start: the pair's own φ of the two previous planes from registers, not LDS)
+#define P2_INIT_PHIQ 1
+#endif
 #ifndef P2_INIT_NOFENCE  // no scheduling fences between the analytic start's stages: it has the registers to overlap
 #define P2_INIT_NOFENCE 1   // one stage's LDS reads with the last one's arithmetic (−2.3 % for that pass, profiles/r5/memops)
 #endif
@@ -584,6 +587,8 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
       L[decltype(ic)::value / 4][decltype(ic)::value % 4] = D2m(0.0, 0.0);
     });
     D2 Lm[2] = {D2m(0.0, 0.0), D2m(0.0, 0.0)};
+    D2 phq[2] = {D2m(0.0, 0.0), D2m(0.0, 0.0)};  // (analytic start: the pair's own φ by plane parity)
+    (void)phq;
     D2 vS = D2m(0.0, 0.0);  // (deferred stores: the level-S value of the previous iteration)
 
     const int i0 = wx0 - S + 1, i1 = wx1 + S - 2;
@@ -739,9 +744,24 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
       const D2 f3 = D2m((sx3 * fy) * fzl, (sx3 * fy) * fzh);
       D2 u = D2m(0.0, 0.0);
       if (reg) {
-        const D2 f1 = rd2(b0, o0(s3, 0, 0));
+        D2 f1, c;
+#if P2_INIT_PHIQ
+        if constexpr (S == 4) {  // (the pair's own φ(i+1), φ(i+2): computed here two and one iterations ago; S ≤ 3
+                                 // analytic starts have no registers to spare)
+          f1 = phq[(F + 1) & 1];  // (φ(i+1) and φ(i+3) share the parity slot: read, then replaced)
+          wr2(b0, o0(s3, 0, 0), f3);
+          c = phq[F & 1];
+          phq[(F + 1) & 1] = f3;
+        } else {
+          f1 = rd2(b0, o0(s3, 0, 0));
+          wr2(b0, o0(s3, 0, 0), f3);
+          c = rd2(b0, o0(s2, 0, 0));
+        }
+#else
+        f1 = rd2(b0, o0(s3, 0, 0));
         wr2(b0, o0(s3, 0, 0), f3);
-        const D2 c = rd2(b0, o0(s2, 0, 0));
+        c = rd2(b0, o0(s2, 0, 0));
+#endif
         const D2 ym = rd2(b0, o0(s2, -1, 0)), yp = rd2(b0, o0(s2, 1, 0));
         const double zm = rd1(b0, o0(s2, 0, -1) + 8), zq = rd1(b0, o0(s2, 0, 1));
         const double lapl = d2sum(c.x, f1.x, f3.x, ym.x, yp.x, zm, c.y);
@@ -853,8 +873,13 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
           L[0][3] = u1_pair(i0 - 1);
           L[0][0] = u1_pair(i0);
           L[0][1] = u1_pair(i0 + 1);
-          wr2(b0, o0(3, 0, 0), phi_pair(i0 + 1));
-          wr2(b0, o0(2, 0, 0), phi_pair(i0 + 2));
+          const D2 p1 = phi_pair(i0 + 1), p2 = phi_pair(i0 + 2);
+          wr2(b0, o0(3, 0, 0), p1);
+          wr2(b0, o0(2, 0, 0), p2);
+          if constexpr (S == 4) {
+            phq[1] = p1;  // (plane i0+1: odd parity; i0+2: even)
+            phq[0] = p2;
+          }
         }
         if (reg) {
           Lm[0] = phi_pair(i0);

@@ -43,15 +43,16 @@ struct Geo {
   static constexpr int G1 = R1 + 1;   // guard pairs before / after the compact block (edge reads stay inside LDS)
   static constexpr int NY = HY + 4;   // y sin table: a ∈ [−2, HY + 2)
   static constexpr int NZ = HZ + 8;   // z sin table: z_r ∈ [−4, HZ + 4)
-  // (in pairs) level-0 slots [0, 2·P0), φ slots (analytic start) [2·P0, 4·P0), then the compact levels
-  static constexpr int lk0(bool init) { return (init ? 4 : 2) * P0 + G1; }
-  static constexpr int pairs(bool init) { return lk0(init) + 2 * (S - 1) * P1 + G1; }
+  // (in pairs) level-0 slots [0, 2·P0), then the compact levels (the analytic start needs no more: φ and its
+  // neighbours are table products)
+  static constexpr int lk0() { return 2 * P0 + G1; }
+  static constexpr int pairs() { return lk0() + 2 * (S - 1) * P1 + G1; }
   static constexpr int tab_doubles(int nxt) { return NY + NZ + nxt; }
 };
 
-template <bool INIT, int S>
+template <int S>
 constexpr size_t p2_lds_bytes(int nxt) {
-  return static_cast<size_t>(Geo<S>::pairs(INIT)) * 16 + static_cast<size_t>(Geo<S>::tab_doubles(nxt)) * 8;
+  return static_cast<size_t>(Geo<S>::pairs()) * 16 + static_cast<size_t>(Geo<S>::tab_doubles(nxt)) * 8;
 }
 // x sin table length for a chunk of xlen planes: x ∈ [x0 − S − 1, x1 + S + 2]
 template <int S>
@@ -99,17 +100,7 @@ constexpr int kTgt[64] = {0,  1,  2,  3,  4,  5,  6,  7,  0,  1,  2,  3,  4,  5,
                           8,  9,  10, 11, 12, 13, 14, 15, 8,  9,  10, 11, 12, 13, 14, 15};
 // (the read groups: {0–3,12–15,20–27} gets 0–3, 4–7, 12–15 + 8–11; {4–11,16–19,28–31} gets 4–7, 0–3, 8–11, 12–15 —
 // all 16 residues once; every contiguous 8-lane write block holds residues r and r+4 … distinct mod 8)
-#ifndef P2_BANK_ORDER  // (A/B: 0 = row-major lanes, consecutive lanes on consecutive 16-byte pairs in memory)
-#define P2_BANK_ORDER 1
-#endif
 constexpr void bank_order(const int* ea, const int* eb, int n, int rstride, int rbase, int* oa, int* ob) {
-  if (!P2_BANK_ORDER) {
-    for (int l = 0; l < 64; ++l) {
-      oa[l] = ea[l < n ? l : 0];
-      ob[l] = eb[l < n ? l : 0];
-    }
-    return;
-  }
   bool used[64] = {};
   int lane_e[64] = {};
   bool filled[64] = {};
@@ -275,26 +266,11 @@ struct P2Params {
   double ct[5];
 };
 
-__device__ __forceinline__ double lds_rd1(const double* p) {
-  typedef __attribute__((address_space(3))) const volatile double lds_vd;  // a ds_read_b64, never paired
-  return *(lds_vd*)p;
-}
 // cache-policy bits of the plane loads / stores (gfx950 CPol: 1 = sc0, 2 = nt, 16 = sc1): non-temporal stores (the new
 // levels are read by the next pass, two planes later at the earliest), default-policy loads (the tile halos are read
 // again by the neighbouring tiles of the same XCD)
-#ifndef P2_STORE_AUX
-#define P2_STORE_AUX 2
-#endif
-#ifndef P2_LOAD_AUX
-#define P2_LOAD_AUX 0
-#endif
-// (a scheduling fence between stages: the compiler would otherwise hoist later stages' LDS reads into earlier ones
-// and run out of the 128 VGPRs of a 1024-thread workgroup)
-#ifndef P2_NO_SCHED_FENCE
-#define P2_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define P2_SCHED_FENCE()
-#endif
+constexpr int kStoreAux = 2;
+constexpr int kLoadAux = 0;
 __device__ __forceinline__ void p2_barrier() {
   // LDS writes done, then the workgroup barrier; global loads stay in flight (a __syncthreads() would add vmcnt(0))
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -359,63 +335,29 @@ __device__ __forceinline__ int p2_desc(int tid) {
 // in one in-order vmcnt: with a wave-dependent sequence the compiler's count is the minimum over paths and the commit
 // of u^n waits for the previous iteration's stores; with one sequence it waits for exactly the load it needs.
 // Register queues: plane x of level j at slot (x − i0) & 3 (a 16-byte pair each), u^{n−1} at (x − i0) & 1.
-// LDS addressing: three per-thread byte bases (level-0/φ slots, compact levels 1–2, compact levels 3–4), every access
+// LDS addressing: three per-thread byte bases (level-0 slots, compact levels 1–2, compact levels 3–4), every access
 // an immediate offset from one of them (a 1024-thread workgroup has 128 VGPRs per lane: no room for one address
 // register per plane).
+//
+// Perf-attribution builds only (results wrong; tools/build.py W3D_EXTRA_DEFS_P2=-D…, profiles/r5/p2_attribution.md):
+//   W3D_EXPERIMENT_NOLOAD    every plane load hits one of 4 resident planes (no HBM reads)
+//   W3D_EXPERIMENT_NOSTORE   the pass writes nothing to HBM
+//   W3D_EXPERIMENT_NOBARRIER the per-plane barrier removed
+//   W3D_EXPERIMENT_NOCHECK   no fused error check; W3D_EXPERIMENT_NORED no partial reduction
+// Variants measured and removed (their numbers stay in profiles/r5/: store_experiments.md, memops/README.md,
+// p2_attribution.md): deferred stores, two-plane-ahead prefetch, staggered waves, conditional queue writes, the late
+// u^n load point, row-major halo lanes, split stores in the analytic start, stores from every wave, a separate
+// interior-tile body, Dirichlet selects after every stage, the ring waves loading u^{n−1}, a φ plane in LDS.
 template <int S, int CM, bool INIT, bool CH>
 __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
   using G = Geo<S>;
   constexpr int E = G::E, R0 = G::R0, R1 = G::R1;
-  // late loads (S ≥ 4): u^{n−1} plane i+1 is loaded after stage 1 (into the register stage 1 just consumed), u^n plane
-  // i+2 before stage 1 (into plane i−2's dead slot); the vector-memory sequence of an iteration is load, load, stores —
-  // the next commit waits for its load, never for a store
-#ifdef P2_NO_LATE  // (experiment: both loads at the iteration start, as the S ≤ 3 passes do)
-  constexpr bool kLate = false;
-#else
+  // late loads (S ≥ 4): u^n plane i+2 right after the commit (into plane i−2's dead slot), u^{n−1} plane i+1 after
+  // stage 1 (into the register stage 1 just consumed); the vector-memory sequence of an iteration is load, load,
+  // stores — the next commit waits for its load, never for a store
   constexpr bool kLate = !INIT && S >= 4;
-#endif
-  // deep prefetch (experiment, off: -DP2_DEEP=1): the same two load points, each one plane further ahead — u^{n−1}
-  // plane i+2 into the slot stage 1 just consumed (two u^{n−1} slots), u^n plane i+3 into plane i−1's slot (dead after
-  // stage 2); twice the bytes in flight per CU. Measured 2.7 % slower per solve (head-loop spills; the loads were not
-  // what held the pass back: profiles/r5/p2_attribution.md)
-#ifndef P2_LAM_MASK  // (A/B: 0 = the Dirichlet selects after every stage, the round-5 first version)
-#define P2_LAM_MASK 1
-#endif
-#ifndef P2_PREV_RING_OOB  // (A/B: 0 = the ring waves load u^{n−1} too, the round-5 first version)
-#define P2_PREV_RING_OOB 1
-#endif
-#ifndef P2_SPLIT_STORE  // (A/B: 0 = every wave issues both stores, non-owners out of range — the round-5 first version)
-#define P2_SPLIT_STORE 1
-#endif
-#ifndef P2_INIT_PHIQ  // (analytic start: the pair's own φ of the two previous planes from registers, not LDS)
-#define P2_INIT_PHIQ 1
-#endif
-#ifndef P2_INIT_NOFENCE  // no scheduling fences between the analytic start's stages: it has the registers to overlap
-#define P2_INIT_NOFENCE 1   // one stage's LDS reads with the last one's arithmetic (−2.3 % for that pass, profiles/r5/memops)
-#endif
-#ifndef P2_SPLIT_STORE_INIT  // (experiment: the split stores in the 4-step analytic start too)
-#define P2_SPLIT_STORE_INIT 0
-#endif
-#ifndef P2_CHECK_REG  // (0 = the 5-step passes read the own row's s_y and pair's s_z from LDS at every check, as the
-#define P2_CHECK_REG 1  // 4-step load passes do: they have no registers to spare)
-#endif
-#ifndef P2_CHECK_SPLIT  // (A/B: 0 = one accumulator per level with per-plane masks, the round-5 first version)
-#define P2_CHECK_SPLIT 1
-#endif
-#ifndef P2_DEFER_STORE  // (experiment, off: measured 3.7 % slower per solve, profiles/r5/store_experiments.md)
-#define P2_DEFER_STORE 0
-#endif
-#ifndef P2_STORE_ALL  // (A/B: 1 = every wave stores in the analytic start too, the round-5 first version)
-#define P2_STORE_ALL 0
-#endif
-  constexpr bool kDefer = !INIT && P2_DEFER_STORE;
-  constexpr bool kSplitSt = ((!INIT && S == 5) || (INIT && S == 4 && P2_SPLIT_STORE_INIT)) && P2_SPLIT_STORE && !kDefer;
-#ifndef P2_DEEP
-#define P2_DEEP 0
-#endif
-  // (P2_DEEP: 1 = both fields, 2 = u^n only, 3 = u^{n−1} only)
-  constexpr bool kDeepPrev = kLate && S == 5 && (P2_DEEP == 1 || P2_DEEP == 3);
-  constexpr bool kDeepCur = kLate && S == 5 && (P2_DEEP == 1 || P2_DEEP == 2);
+  // split stores (5-step passes): the own waves store level S, the other 8 waves level S−1 (below)
+  constexpr bool kSplitSt = !INIT && S == 5;
   extern __shared__ double lds[];
   const int tid = static_cast<int>(threadIdx.x);
   int blk = static_cast<int>(blockIdx.x);
@@ -429,7 +371,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
   // (Dirichlet, or beyond the box) are masked out once, in the reduction, not at every plane
   // (registers: ≤ 3 checked levels, in the 5-step passes and the 4-step analytic start — the production passes; the
   // others are at or near 128 VGPRs already)
-  constexpr bool kSplitAcc = P2_CHECK_SPLIT && __builtin_popcount(CM) <= 3 && (S == 5 || (INIT && S == 4));
+  constexpr bool kSplitAcc = __builtin_popcount(CM) <= 3 && (S == 5 || (INIT && S == 4));
   double emax[S][2], esum[S][2];
   static_for<0, S>([&](auto kc) __attribute__((always_inline)) {
     constexpr int k = decltype(kc)::value;
@@ -449,15 +391,10 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     auto inside = [&](int g) __attribute__((always_inline)) {
       return static_cast<unsigned>(g - 1) < static_cast<unsigned>(N - 1);
     };
-    // interior tile: every stage-1 region node lies in the global interior (no Dirichlet selects, every own node is
-    // stored and checked); otherwise an edge tile
-    const bool edge =
-        !(inside(p.gy0 + ty0 - (S - 1)) && inside(p.gy0 + ty0 + kT + S - 2) && inside(p.gz0 + tz0 - E) &&
-          inside(p.gz0 + tz0 + kT + E - 1));
 
-    // ---- LDS: level-0 slots, φ slots (INIT), compact levels, then the sin / row-factor tables
+    // ---- LDS: level-0 slots, compact levels, then the sin / row-factor tables
     lchar* const lds_base = (lchar*)(lds);  // (C-style: an address-space cast)
-    double* const syw = lds + 2 * G::pairs(INIT);
+    double* const syw = lds + 2 * G::pairs();
     double* const szw = syw + G::NY;
     double* const sxw = szw + G::NZ;
     const int xtab0 = S + 1 - wx0;  // plane x ↔ sxw[x + xtab0]
@@ -484,9 +421,6 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     // levels this wave checks (a scalar int, re-asserted per iteration like wst: a loop-invariant bool is kept as a
     // 64-bit lane mask, and each stage's test then cost a v_cndmask + v_cmp pair to negate it)
     int wchk = __builtin_amdgcn_readfirstlane(winner ? p.check_mask : 0);
-#ifdef P2_STAGGER
-    const bool wodd = (__builtin_amdgcn_readfirstlane(tid) >> 6) & 1;
-#endif
     const int y = ty0 - (S - 1) + a, z = tz0 - E + 2 * b;
     const int el = z + p.za;                    // element of the pair's first node in its row
     const bool ldv = act && y >= p.ay0 && y < p.ay1 && el >= 0 && el + 2 <= p.pitch;
@@ -497,18 +431,19 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     const unsigned soff = sty ? goff : kOob;
     okl = sty && rl;
     okh = sty && rh && z + 1 < p.z1;
-#if P2_LAM_MASK
-    const double lam_lo = rl ? p.tau2 : 0.0, lam_hi = rh ? p.tau2 : 0.0;  // (τ² per node: 0 on Dirichlet nodes)
-#endif
+    // Dirichlet nodes through τ²: a node outside the global interior has τ² = 0 and c = old = +0 at every level (zero
+    // loads, zero φ, and this very update), so fma(0, Δ, fma(2, +0, −(+0))) = +0 — the select's value, bit for bit,
+    // without 4 selects per pair and stage
+    const double lam_lo = rl ? p.tau2 : 0.0, lam_hi = rh ? p.tau2 : 0.0;
     // per-thread LDS byte bases (all accesses: a compile-time offset from one of them)
-    const int lo0 = (a + 1) * R0 + (b + 1);     // level-0 / φ slot index of the pair
+    const int lo0 = (a + 1) * R0 + (b + 1);     // level-0 slot index of the pair
     const int lk = a * R1 + b;                  // compact slot index (region pairs)
     // (32-bit LDS-address-space pointers: a generic pointer is a 64-bit register pair)
     lchar* b0 = lds_base + (lo0 - R0 - 1) * 16;  // (neighbour offsets from −R0−1 pairs up: never negative)
-    lchar* bA = lds_base + (G::lk0(INIT) + lk - R1 - 1) * 16;
+    lchar* bA = lds_base + (G::lk0() + lk - R1 - 1) * 16;
     lchar* bB = bA + 4 * G::P1 * 16;
-    lchar* rt = lds_base + (2 * G::pairs(INIT) + a + 2) * 8;                          // check: s_y of the own row
-    lchar* szp = lds_base + (2 * G::pairs(INIT) + G::NY + 2 * b + 4) * 8;           // check: own (s_z, s_z+1)
+    lchar* rt = lds_base + (2 * G::pairs() + a + 2) * 8;                          // check: s_y of the own row
+    lchar* szp = lds_base + (2 * G::pairs() + G::NY + 2 * b + 4) * 8;           // check: own (s_z, s_z+1)
     // Split stores (kSplitSt): the 8 waves that do not own the tile store level S−1 of the own pairs — lane j of
     // wave 8 + w the pair of lane j of own wave w, read back from the level's compact LDS plane one iteration after
     // it was computed — and the own waves store level S only. Every wave then issues exactly one store per iteration,
@@ -521,7 +456,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
       const int y2 = ty0 - (S - 1) + a2, z2 = tz0 - E + 2 * b2, el2 = z2 + p.za;
       const bool st2 = y2 >= p.ay0 && y2 < p.ay1 && el2 >= 0 && el2 + 2 <= p.pitch && y2 < p.y1 && z2 < p.z1;
       soff2 = st2 ? static_cast<unsigned>(((y2 + p.ya) * p.pitch + el2) * 8) : kOob;
-      rt = lds_base + (G::lk0(INIT) + a2 * R1 + b2 - R1 - 1) * 16 + 4 * G::P1 * 16;
+      rt = lds_base + (G::lk0() + a2 * R1 + b2 - R1 - 1) * 16 + 4 * G::P1 * 16;
     }
     // (re-declared opaque at every iteration: otherwise the loop-invariant "base + offset" of every access is hoisted
     // out of the x march into a register of its own — 15 address VGPRs and spills — instead of the offset field)
@@ -533,7 +468,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
       wst = __builtin_amdgcn_readfirstlane(wst);  // (an asm output is not known uniform: re-assert it)
       wchk = __builtin_amdgcn_readfirstlane(wchk);
     };
-    // slot / neighbour offsets (bytes): level-0 or φ slot s, compact plane pl = (k−1)·2 + parity
+    // slot / neighbour offsets (bytes): level-0 slot s, compact plane pl = (k−1)·2 + parity
     auto o0 = [](int sl, int dy, int dz) constexpr { return sl * G::P0 * 16 + ((dy + 1) * R0 + dz + 1) * 16; };
     auto ok_ = [](int pl, int dy, int dz) constexpr { return (pl & 3) * G::P1 * 16 + ((dy + 1) * R1 + dz + 1) * 16; };
     auto kb = [&](int pl) __attribute__((always_inline)) { return pl < 4 ? bA : bB; };
@@ -546,15 +481,24 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     const int pbytes = static_cast<int>(P * 8);
     // u^{n−1} is read by the region waves only (the stage-1 update); the u^n ring waves get a zero-size descriptor for
     // it — same instruction sequence, no memory traffic (a scalar: wd is wave-uniform)
-    const int prev_bytes = (((wd >> 20) & 0x3) == 1 || !P2_PREV_RING_OOB) ? pbytes : 0;
+    const int prev_bytes = ((wd >> 20) & 0x3) == 1 ? pbytes : 0;
     auto load_pair = [&](auto bkc, const double* f, int x) __attribute__((always_inline)) -> D2 {
-#ifdef W3D_EXPERIMENT_NOLOAD  // (perf attribution only, results wrong: every plane load hits one of 4 resident planes)
+#ifdef W3D_EXPERIMENT_NOLOAD
       const int xs = (x & 3) + 1;
 #else
       const int xs = decltype(bkc)::value ? x : x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
 #endif
       return as_d2(__builtin_amdgcn_raw_buffer_load_b128(rsrc(f, xs, f == p.cur ? pbytes : prev_bytes),
-                                                         static_cast<int>(goff), 0, P2_LOAD_AUX));
+                                                         static_cast<int>(goff), 0, kLoadAux));
+    };
+    auto store_pair = [&](D2 v, double* f, int x, unsigned off, bool real) __attribute__((always_inline)) {
+#ifndef W3D_EXPERIMENT_NOSTORE
+      // (a scalar offset past the plane drops the whole wave's store: the x test stays scalar)
+      __builtin_amdgcn_raw_buffer_store_b128(as_u4(v), rsrc(f, x, pbytes), static_cast<int>(off),
+                                             real ? 0 : static_cast<int>(0x80000000u), kStoreAux);
+#else
+      (void)v, (void)f, (void)x, (void)off, (void)real;
+#endif
     };
 
     __syncthreads();  // tables
@@ -589,7 +533,6 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     D2 Lm[2] = {D2m(0.0, 0.0), D2m(0.0, 0.0)};
     D2 phq[2] = {D2m(0.0, 0.0), D2m(0.0, 0.0)};  // (analytic start: the pair's own φ by plane parity)
     (void)phq;
-    D2 vS = D2m(0.0, 0.0);  // (deferred stores: the level-S value of the previous iteration)
 
     const int i0 = wx0 - S + 1, i1 = wx1 + S - 2;
     auto xreal = [&](int x) __attribute__((always_inline)) {
@@ -614,10 +557,9 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     };
 
     // stage k at plane xp; D = (xp − i0) & 3 (static)
-    auto stage = [&](auto kc, auto dc, auto bkc, auto ec, int xp) __attribute__((always_inline)) {
+    auto stage = [&](auto kc, auto dc, auto bkc, int xp) __attribute__((always_inline)) {
       constexpr int k = decltype(kc)::value, D = decltype(dc)::value;
-      constexpr bool BK = decltype(bkc)::value, EDGE = decltype(ec)::value;
-      constexpr int F = (D + k - 1) & 3;
+      constexpr bool BK = decltype(bkc)::value;
       constexpr int sm = (D + 3) & 3, s0 = D, sp = (D + 1) & 3;
       const bool inr = BK || (xp >= wx0 - (S - k) && xp < wx1 + (S - k));
       const bool xown = BK || (xp >= wx0 && xp < wx1);
@@ -641,32 +583,17 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
         }
         const double lapl = d2sum(c.x, xm.x, xq.x, ym.x, yp.x, zm, c.y);
         const double laph = d2sum(c.y, xm.y, xq.y, ym.y, yp.y, c.x, zq);
-        const D2 o = k == 1 ? Lm[(kLate && !kDeepPrev) ? 0 : (D & 1)] : L[k > 1 ? k - 2 : 0][s0];
-#if P2_LAM_MASK
-        // Dirichlet nodes through τ²: a node outside the global interior has τ² = 0 and c = old = +0 at every level
-        // (zero loads, zero φ, and this very update), so fma(0, Δ, fma(2, +0, −(+0))) = +0 — the select's value, bit
-        // for bit, without the 4 selects per pair and stage
+        const D2 o = k == 1 ? Lm[kLate ? 0 : (D & 1)] : L[k > 1 ? k - 2 : 0][s0];
         v = D2m(leapfrog(c.x, o.x, lapl, lam_lo), leapfrog(c.y, o.y, laph, lam_hi));
-        (void)EDGE;
-#else
-        v = D2m(leapfrog(c.x, o.x, lapl, p.tau2), leapfrog(c.y, o.y, laph, p.tau2));
-        if constexpr (EDGE) {
-          v.x = rl ? v.x : 0.0;
-          v.y = rh ? v.y : 0.0;
-        }
-#endif
         if constexpr (!BK) {
           if (!xreal(xp)) v = D2m(0.0, 0.0);
         }
         if constexpr (k < S) {
           constexpr int pl = (k - 1) * 2 + (D & 1);
           wr2(kb(pl), ok_(pl, 0, 0), v);
-#ifdef P2_COND_QUEUE  // (A/B only: the round-5 first version, queue slot written only when the stage runs)
-          L[k][s0] = v;
-#endif
         }
         constexpr bool kChk =
-#ifdef P2_NO_CHECK
+#ifdef W3D_EXPERIMENT_NOCHECK
             false;
 #else
             ((CM >> (k - 1)) & 1) != 0;
@@ -675,8 +602,9 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
           if (((wchk >> (k - 1)) & 1) && xown) {  // (wchk: 0 outside the own waves)
             // u_a = ((s_x·s_y)·ct)·s_z (stencil.hpp analytic_row); s_x of the plane: one LDS broadcast read
             const double sxp = sxw[xp + xtab0];
-            // (the analytic start holds the pair's s_y, s_z, s_z+1 in registers for φ: the same table entries)
-            constexpr bool kRegF = INIT || (P2_CHECK_REG && S == 5);
+            // (the analytic start and the 5-step passes hold the pair's s_y, s_z, s_z+1 in registers; the other
+            // passes have no registers to spare and read them from LDS)
+            constexpr bool kRegF = INIT || S == 5;
             const double rf = (sxp * (kRegF ? fy : rdd(rt, 0))) * p.ct[k - 1];
             const D2 sz = kRegF ? D2m(fzl, fzh) : rd2(szp, 0);
             // (d·d = |d|·|d|; the masks okl / okh are applied in the reduction — per plane they were 4 v_cndmask_b32
@@ -698,265 +626,158 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
         }
       }
       // (also when the stage is skipped: the slot's previous plane is dead either way, and an unconditional write
-      // keeps it from staying live through the general iterations — 8 VGPRs of spills with the deep prefetch)
-#ifndef P2_COND_QUEUE
+      // keeps it from staying live through the general iterations)
       if constexpr (k < S) L[k][s0] = v;
-#endif
-      if constexpr (k == S && kDefer) vS = v;  // (stored at the start of the next iteration: flush)
       if constexpr (kSplitSt && k == S) {
-#ifndef W3D_EXPERIMENT_NOSTORE
-        const int sso = xown ? 0 : static_cast<int>(0x80000000u);
         if (winner) {
-          __builtin_amdgcn_raw_buffer_store_b128(as_u4(v), rsrc(p.out2, xp, pbytes),
-                                                 static_cast<int>(EDGE ? soff : goff), sso, P2_STORE_AUX);
+          store_pair(v, p.out2, xp, soff, xown);
         } else {
           constexpr int pl = (S - 2) * 2 + (D & 1);  // level S−1, plane xp: written by stage S−1 last iteration
-          __builtin_amdgcn_raw_buffer_store_b128(as_u4(rd2(rt, ok_(pl, 0, 0))), rsrc(p.out1, xp, pbytes),
-                                                 static_cast<int>(soff2), sso, P2_STORE_AUX);
+          store_pair(rd2(rt, ok_(pl, 0, 0)), p.out1, xp, soff2, xown);
         }
-#endif
-      }
-      if constexpr (k >= S - 1 && !kDefer && !kSplitSt) {
-        // Interior tiles: the thread's load offset plus a scalar offset (0 for the own waves' planes, out of range
-        // otherwise); edge tiles: the per-lane store offset. Passes that load: every wave stores (non-owners beyond
-        // the plane: dropped), so every wave's vector-memory sequence is the same and the compiler's waits for the
-        // loads can leave the stores in flight. The analytic start loads nothing: only the own waves store (−2 %)
-#ifndef W3D_EXPERIMENT_NOSTORE  // (perf attribution only, results wrong: the pass writes nothing to HBM)
-        if (P2_STORE_ALL || !INIT || winner) {
-          const int sso = (xown && winner) ? 0 : static_cast<int>(0x80000000u);
-          __builtin_amdgcn_raw_buffer_store_b128(as_u4(v), rsrc(k == S ? p.out2 : p.out1, xp, pbytes),
-                                                 static_cast<int>(EDGE ? soff : goff), sso, P2_STORE_AUX);
-        }
-#endif
+      } else if constexpr (!kSplitSt && k >= S - 1) {
+        // the thread's store offset plus a scalar offset (0 for the own waves' planes, out of range otherwise).
+        // Passes that load: every wave stores (non-owners beyond the plane: dropped), so every wave's vector-memory
+        // sequence is the same and the compiler's waits for the loads can leave the stores in flight. The analytic
+        // start loads nothing: only the own waves store (−2 %)
+        if (!INIT || winner) store_pair(v, k == S ? p.out2 : p.out1, xp, soff, xown && winner);
       }
     };
 
-    // analytic start, iteration i: u¹ of plane i+2 (into L[0]) and u⁰ = φ of plane i+1 (into Lm) for the region pairs
-    // from a φ plane in LDS (two parity slots, ring included): φ(i+3) is computed once per node (2 products), φ(i+2)'s
-    // y/z neighbours are read from its slot, φ(i+1) is the thread's own entry of the slot φ(i+3) then overwrites.
-    // Ring pairs compute u¹ from the tables (their φ neighbours lie outside the φ plane). Bit-identical to
-    // k_init_first: every neighbour value is the same product.
-    auto init_iter = [&](auto fc, auto ec, int i) __attribute__((always_inline)) {
+    // analytic start, iteration i: u¹ of plane i+2 (into L[0]) and u⁰ = φ of plane i+1 (into Lm) for the region
+    // pairs. φ(i+3) is computed once per node (2 products) and kept in a register queue with φ(i+1), φ(i+2) (S = 4; the
+    // S ≤ 3 starts have no registers to spare and form them again); φ(i+2)'s y/z neighbours are the products the
+    // neighbouring pairs form, (s_x·s_y(a±1))·s_z and (s_x·s_y)·s_z(z−1 / z+2): four table reads and seven products
+    // instead of a φ plane in LDS (measured: −1 % for the pass, profiles/r6/). Ring pairs compute u¹ from the tables.
+    // Bit-identical to k_init_first: every neighbour value is the same product.
+    auto init_iter = [&](auto fc, int i) __attribute__((always_inline)) {
       constexpr int F = decltype(fc)::value;
-      constexpr bool EDGE = decltype(ec)::value;
-      constexpr int s3 = 2 + ((F + 3) & 1), s2 = 2 + ((F + 2) & 1);
       const double sx3 = sxw[i + 3 + xtab0];
       const D2 f3 = D2m((sx3 * fy) * fzl, (sx3 * fy) * fzh);
       D2 u = D2m(0.0, 0.0);
       if (reg) {
         D2 f1, c;
-#if P2_INIT_PHIQ
-        if constexpr (S == 4) {  // (the pair's own φ(i+1), φ(i+2): computed here two and one iterations ago; S ≤ 3
-                                 // analytic starts have no registers to spare)
+        if constexpr (S == 4) {
           f1 = phq[(F + 1) & 1];  // (φ(i+1) and φ(i+3) share the parity slot: read, then replaced)
-          wr2(b0, o0(s3, 0, 0), f3);
           c = phq[F & 1];
           phq[(F + 1) & 1] = f3;
         } else {
-          f1 = rd2(b0, o0(s3, 0, 0));
-          wr2(b0, o0(s3, 0, 0), f3);
-          c = rd2(b0, o0(s2, 0, 0));
+          f1 = phi_pair(i + 1);
+          c = phi_pair(i + 2);
         }
-#else
-        f1 = rd2(b0, o0(s3, 0, 0));
-        wr2(b0, o0(s3, 0, 0), f3);
-        c = rd2(b0, o0(s2, 0, 0));
-#endif
-        const D2 ym = rd2(b0, o0(s2, -1, 0)), yp = rd2(b0, o0(s2, 1, 0));
-        const double zm = rd1(b0, o0(s2, 0, -1) + 8), zq = rd1(b0, o0(s2, 0, 1));
+        const double sx2 = sxw[i + 2 + xtab0];
+        const double ry_m = sx2 * syw[a + 1], ry_p = sx2 * syw[a + 3], cy2 = sx2 * fy;
+        const D2 ym = D2m(ry_m * fzl, ry_m * fzh), yp = D2m(ry_p * fzl, ry_p * fzh);
+        const double zm = cy2 * szw[2 * b + 3], zq = cy2 * szw[2 * b + 6];
         const double lapl = d2sum(c.x, f1.x, f3.x, ym.x, yp.x, zm, c.y);
         const double laph = d2sum(c.y, f1.y, f3.y, ym.y, yp.y, c.x, zq);
-        const bool xin = inside(p.gx0 + i + 2);
         u = D2m(first_step(c.x, lapl, p.half_tau2), first_step(c.y, laph, p.half_tau2));
-        if constexpr (EDGE) {
-          u.x = rl ? u.x : 0.0;
-          u.y = rh ? u.y : 0.0;
-        }
-        if (!xin) u = D2m(0.0, 0.0);
-#if P2_LAM_MASK
-        if constexpr (EDGE) {  // (u⁰ = φ is not 0 on every Dirichlet node — s(N) = sin(π) — so it is zeroed here)
-          Lm[(F + 1) & 1] = D2m(rl ? f1.x : 0.0, rh ? f1.y : 0.0);
-        } else {
-          Lm[(F + 1) & 1] = f1;
-        }
-#else
-        Lm[(F + 1) & 1] = f1;
-#endif
+        u.x = rl ? u.x : 0.0;
+        u.y = rh ? u.y : 0.0;
+        if (!inside(p.gx0 + i + 2)) u = D2m(0.0, 0.0);
+        // (u⁰ = φ is not 0 on every Dirichlet node — s(N) = sin(π) — so it is zeroed here)
+        Lm[(F + 1) & 1] = D2m(rl ? f1.x : 0.0, rh ? f1.y : 0.0);
       } else if (act) {
-        wr2(b0, o0(s3, 0, 0), f3);
         u = u1_pair(i + 2);
       }
       L[0][(F + 2) & 3] = u;  // (one store to the queue slot: SROA keeps the queue in registers)
     };
 
-    // deferred stores (kDefer), at the start of iteration i: levels S−1 and S of iteration i−1 (planes i−S+1, i−S),
-    // the own waves only. Every wave has waited for all its vector-memory operations just before (vmcnt(0) after
-    // the barrier), and its loads come after these stores, so no later wait depends on whether a wave stored: the
-    // compiler's waits stay exact for every wave (a store skipped by half the waves after the loads would make it
-    // wait for the other half's stores) and the non-own waves no longer issue out-of-range stores through the
-    // texture addresser (rocprofv3: SQ_VMEM_TA_ADDR_FIFO_FULL 21 % of the CU-busy cycles, profiles/r5/)
-    auto flush = [&](auto fc, auto ec, int i) __attribute__((always_inline)) {
-      constexpr int F = decltype(fc)::value;
-      constexpr bool EDGE = decltype(ec)::value;
-#ifndef W3D_EXPERIMENT_NOSTORE
-      if (winner) {
-        const int x1 = i - S + 1, x2 = i - S;
-        const int s1 = (x1 >= wx0 && x1 < wx1) ? 0 : static_cast<int>(0x80000000u);
-        const int s2 = (x2 >= wx0 && x2 < wx1) ? 0 : static_cast<int>(0x80000000u);
-        const int off = static_cast<int>(EDGE ? soff : goff);
-        __builtin_amdgcn_raw_buffer_store_b128(as_u4(L[S - 1][(F - S + 1 + 8) & 3]), rsrc(p.out1, x1, pbytes), off, s1,
-                                               P2_STORE_AUX);
-        __builtin_amdgcn_raw_buffer_store_b128(as_u4(vS), rsrc(p.out2, x2, pbytes), off, s2, P2_STORE_AUX);
-      }
-#endif
-    };
-
     // iteration i with phase F
-    auto iteration = [&](auto fc, auto bkc, auto ec, int i) __attribute__((always_inline)) {
+    auto iteration = [&](auto fc, auto bkc, int i) __attribute__((always_inline)) {
       constexpr int F = decltype(fc)::value;
 #ifndef W3D_EXPERIMENT_NOBARRIER
       p2_barrier();  // every read of the slots overwritten below (iteration i−1) is done; i−1's writes visible
 #endif
-#ifdef P2_STAGGER  // (experiment: odd waves start each plane 64·P2_STAGGER cycles later, so the 16 waves' loads do not
-                   // all reach the texture addresser at once)
-      if (wodd) __builtin_amdgcn_s_sleep(P2_STAGGER);
-#endif
       opaque_bases();
-      if constexpr (kDefer) {
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's loads of iteration i−1 (and older stores)
-        flush(fc, ec, i);
-      }
       if (act) wr2(b0, o0((F + 1) & 1, 0, 0), L[0][(F + 1) & 3]);  // u^n plane i+1 → LDS
       if constexpr (INIT) {
-        init_iter(fc, ec, i);
+        init_iter(fc, i);
       } else if constexpr (!kLate) {
         L[0][(F + 2) & 3] = load_pair(bkc, p.cur, i + 2);
         Lm[(F + 1) & 1] = load_pair(bkc, p.prev, i + 1);
-      }
-#define W3D_P2_STAGE(K)                                                                                           \
-  if constexpr (K <= S) {                                                                                         \
-    stage(std::integral_constant<int, K>{}, std::integral_constant<int, (F - (K - 1) + 8) & 3>{}, bkc, ec,        \
-          i - (K - 1));                                                                                           \
-    if constexpr (!(INIT && P2_INIT_NOFENCE)) P2_SCHED_FENCE();                                                   \
-  }
-#ifndef P2_CUR_LATE
-      // u^n plane i+2 right after the commit: its slot (plane i−2's) has been dead since stage 2 of iteration i−1, and
-      // issued here it has the whole iteration (≈ 2 µs) to arrive — after stage 2, as first built, it had ≈ 60 % of one
-      // and the next commit waited for it: −13 % per 5-step pass (profiles/r5/stores/abn_cur_early.log). (Loading it
-      // one iteration earlier still, into the same slot, spills.)
-      if constexpr (kLate && !kDeepCur) L[0][(F + 2) & 3] = load_pair(bkc, p.cur, i + 2);
-#endif
-      W3D_P2_STAGE(1)
-      if constexpr (kDeepPrev)
-        Lm[F & 1] = load_pair(bkc, p.prev, i + 2);
-      else if constexpr (kLate)
-        Lm[0] = load_pair(bkc, p.prev, i + 1);  // (its register freed by stage 1)
-      W3D_P2_STAGE(2)
-      if constexpr (kDeepCur)
-        L[0][(F + 3) & 3] = load_pair(bkc, p.cur, i + 3);
-#ifdef P2_CUR_LATE  // (A/B: the first version's load point)
-      else if constexpr (kLate)
+      } else {
+        // u^n plane i+2 right after the commit: its slot (plane i−2's) has been dead since stage 2 of iteration i−1,
+        // and issued here it has the whole iteration (≈ 2 µs) to arrive — after stage 2, as first built, the next
+        // commit waited for it: −13 % per 5-step pass (profiles/r5/stores/abn_cur_early.log)
         L[0][(F + 2) & 3] = load_pair(bkc, p.cur, i + 2);
-#endif
+      }
+      // (scheduling fences between the load passes' stages: the compiler would otherwise hoist later stages' LDS
+      // reads into earlier ones and run out of the 128 VGPRs; the analytic start has the registers to overlap one
+      // stage's reads with the last one's arithmetic, −2.3 %, profiles/r5/memops)
+#define W3D_P2_STAGE(K)                                                                                       \
+  if constexpr (K <= S) {                                                                                     \
+    stage(std::integral_constant<int, K>{}, std::integral_constant<int, (F - (K - 1) + 8) & 3>{}, bkc,        \
+          i - (K - 1));                                                                                       \
+    if constexpr (!INIT) __builtin_amdgcn_sched_barrier(0);                                                   \
+  }
+      W3D_P2_STAGE(1)
+      if constexpr (kLate) Lm[0] = load_pair(bkc, p.prev, i + 1);  // (its register freed by stage 1)
+      W3D_P2_STAGE(2)
       W3D_P2_STAGE(3)
       W3D_P2_STAGE(4)
       W3D_P2_STAGE(5)
 #undef W3D_P2_STAGE
     };
 
-    auto march = [&](auto ec) __attribute__((always_inline)) {
-      using Gen = std::false_type;
-      using Bulk = std::true_type;
-      // prologue: u^n planes i0−1, i0 (registers; plane i0 also to LDS), plane i0+1 and u^{n−1} plane i0 in flight
-      if constexpr (INIT) {
-        if (act) {
-          L[0][3] = u1_pair(i0 - 1);
-          L[0][0] = u1_pair(i0);
-          L[0][1] = u1_pair(i0 + 1);
-          const D2 p1 = phi_pair(i0 + 1), p2 = phi_pair(i0 + 2);
-          wr2(b0, o0(3, 0, 0), p1);
-          wr2(b0, o0(2, 0, 0), p2);
-          if constexpr (S == 4) {
-            phq[1] = p1;  // (plane i0+1: odd parity; i0+2: even)
-            phq[0] = p2;
-          }
-        }
-        if (reg) {
-          Lm[0] = phi_pair(i0);
-#if P2_LAM_MASK
-          Lm[0] = D2m(rl ? Lm[0].x : 0.0, rh ? Lm[0].y : 0.0);  // (see init_iter)
-#endif
-        }
-      } else {
-        L[0][3] = load_pair(Gen{}, p.cur, i0 - 1);
-        L[0][0] = load_pair(Gen{}, p.cur, i0);
-      }
-      if (act) wr2(b0, o0(0, 0, 0), L[0][0]);
-      if constexpr (!INIT) {
-        L[0][1] = load_pair(Gen{}, p.cur, i0 + 1);
-        Lm[0] = load_pair(Gen{}, p.prev, i0);
-        if constexpr (kDeepCur) L[0][2] = load_pair(Gen{}, p.cur, i0 + 2);
-        if constexpr (kDeepPrev) Lm[1] = load_pair(Gen{}, p.prev, i0 + 1);
-      }
-      // head blocks (general) until the first block inside the bulk range, bulk blocks, then the general tail
-      const int blo = max(max(wx0, p.sx0), 1 - p.gx0) + (S - 1);
-      const int bhi = min(min(wx1, p.sx1), N - p.gx0);
-      int ib = i0;
-      const int nhead = blo > i0 ? (blo - i0 + 3) / 4 : 0;
-      for (int hb = 0; hb < nhead && ib + 3 <= i1; ++hb, ib += 4) {
-        iteration(std::integral_constant<int, 0>{}, Gen{}, ec, ib);
-        iteration(std::integral_constant<int, 1>{}, Gen{}, ec, ib + 1);
-        iteration(std::integral_constant<int, 2>{}, Gen{}, ec, ib + 2);
-        iteration(std::integral_constant<int, 3>{}, Gen{}, ec, ib + 3);
-      }
-      // (a known-empty vector-memory counter at the bulk loop's entry: its waits are then counted exactly)
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      for (; ib + 3 < bhi; ib += 4) {
-        iteration(std::integral_constant<int, 0>{}, Bulk{}, ec, ib);
-        iteration(std::integral_constant<int, 1>{}, Bulk{}, ec, ib + 1);
-        iteration(std::integral_constant<int, 2>{}, Bulk{}, ec, ib + 2);
-        iteration(std::integral_constant<int, 3>{}, Bulk{}, ec, ib + 3);
-      }
-      // (a tail that runs ends at one of the breaks, where the last iteration's deferred stores go out; whole blocks
-      // up to i1 leave ib = i1 + 1 at phase 0)
-      if constexpr (kDefer) {
-        if (ib > i1) flush(std::integral_constant<int, 0>{}, ec, ib);
-      }
-      for (; ib <= i1; ib += 4) {
-        iteration(std::integral_constant<int, 0>{}, Gen{}, ec, ib);
-        if (ib + 1 > i1) {
-          if constexpr (kDefer) flush(std::integral_constant<int, 1>{}, ec, ib + 1);
-          break;
-        }
-        iteration(std::integral_constant<int, 1>{}, Gen{}, ec, ib + 1);
-        if (ib + 2 > i1) {
-          if constexpr (kDefer) flush(std::integral_constant<int, 2>{}, ec, ib + 2);
-          break;
-        }
-        iteration(std::integral_constant<int, 2>{}, Gen{}, ec, ib + 2);
-        if (ib + 3 > i1) {
-          if constexpr (kDefer) flush(std::integral_constant<int, 3>{}, ec, ib + 3);
-          break;
-        }
-        iteration(std::integral_constant<int, 3>{}, Gen{}, ec, ib + 3);
-        if (ib + 4 > i1) {
-          if constexpr (kDefer) flush(std::integral_constant<int, 0>{}, ec, ib + 4);
-          break;
+    // prologue: u^n planes i0−1, i0 (registers; plane i0 also to LDS), plane i0+1 and u^{n−1} plane i0 in flight
+    using Gen = std::false_type;
+    using Bulk = std::true_type;
+    if constexpr (INIT) {
+      if (act) {
+        L[0][3] = u1_pair(i0 - 1);
+        L[0][0] = u1_pair(i0);
+        L[0][1] = u1_pair(i0 + 1);
+        if constexpr (S == 4) {
+          phq[1] = phi_pair(i0 + 1);  // (plane i0+1: odd parity; i0+2: even)
+          phq[0] = phi_pair(i0 + 2);
         }
       }
-    };
-#ifdef P2_SPLIT_EDGE
-    if (edge)
-      march(std::true_type{});
-    else
-      march(std::false_type{});
-#else
-    (void)edge;
-    march(std::true_type{});  // (one body: the Dirichlet selects run in every tile, all-true in interior tiles)
-#endif
+      if (reg) {
+        const D2 f0 = phi_pair(i0);
+        Lm[0] = D2m(rl ? f0.x : 0.0, rh ? f0.y : 0.0);  // (see init_iter)
+      }
+    } else {
+      L[0][3] = load_pair(Gen{}, p.cur, i0 - 1);
+      L[0][0] = load_pair(Gen{}, p.cur, i0);
+    }
+    if (act) wr2(b0, o0(0, 0, 0), L[0][0]);
+    if constexpr (!INIT) {
+      L[0][1] = load_pair(Gen{}, p.cur, i0 + 1);
+      Lm[0] = load_pair(Gen{}, p.prev, i0);
+    }
+    // head blocks (general) until the first block inside the bulk range, bulk blocks, then the general tail
+    const int blo = max(max(wx0, p.sx0), 1 - p.gx0) + (S - 1);
+    const int bhi = min(min(wx1, p.sx1), N - p.gx0);
+    int ib = i0;
+    const int nhead = blo > i0 ? (blo - i0 + 3) / 4 : 0;
+    for (int hb = 0; hb < nhead && ib + 3 <= i1; ++hb, ib += 4) {
+      iteration(std::integral_constant<int, 0>{}, Gen{}, ib);
+      iteration(std::integral_constant<int, 1>{}, Gen{}, ib + 1);
+      iteration(std::integral_constant<int, 2>{}, Gen{}, ib + 2);
+      iteration(std::integral_constant<int, 3>{}, Gen{}, ib + 3);
+    }
+    // (a known-empty vector-memory counter at the bulk loop's entry: its waits are then counted exactly)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    for (; ib + 3 < bhi; ib += 4) {
+      iteration(std::integral_constant<int, 0>{}, Bulk{}, ib);
+      iteration(std::integral_constant<int, 1>{}, Bulk{}, ib + 1);
+      iteration(std::integral_constant<int, 2>{}, Bulk{}, ib + 2);
+      iteration(std::integral_constant<int, 3>{}, Bulk{}, ib + 3);
+    }
+    // (whole blocks up to i1 leave ib = i1 + 1 at phase 0)
+    for (; ib <= i1; ib += 4) {
+      iteration(std::integral_constant<int, 0>{}, Gen{}, ib);
+      if (ib + 1 > i1) break;
+      iteration(std::integral_constant<int, 1>{}, Gen{}, ib + 1);
+      if (ib + 2 > i1) break;
+      iteration(std::integral_constant<int, 2>{}, Gen{}, ib + 2);
+      if (ib + 3 > i1) break;
+      iteration(std::integral_constant<int, 3>{}, Gen{}, ib + 3);
+    }
   }
 
-#ifdef P2_NO_RED
+#ifdef W3D_EXPERIMENT_NORED
   return;
 #endif
   if (p.partials == nullptr) return;

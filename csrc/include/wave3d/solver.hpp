@@ -399,7 +399,8 @@ class GpuSolver {
     double* u[4] = {nullptr, nullptr, nullptr, nullptr};  // slab: the peer's field buffers
     double* recv = nullptr;        // block: the peer's receive staging
     i64 peer_nx = 0;               // slab: the peer's owned planes
-    i64 recv_off[5] = {0, 0, 0, 0, 0};  // block: offset of this rank's message in the peer's staging, per depth s
+    i64 recv_off[6] = {0, 0, 0, 0, 0, 0};  // block: offset of this rank's message in the peer's staging, per depth
+                                           // s = 2..5 (indexed by s, like deep_[] and sbase_[])
     bool ipc = false;              // mapped with hipIpcOpenMemHandle (closed in the destructor)
   };
   bool sdma_ = false;

@@ -38,18 +38,38 @@ struct P2Plan {
   int nblocks = 0;
 };
 
-// LDS budget of a pass: the largest x chunk whose sin table still fits next to the planes
-int p2_max_xlen(int S, bool init) {
+// LDS budget of a pass: the largest x chunk whose sin table still fits next to the planes (the analytic start uses
+// the same planes: its φ values are table products)
+int p2_max_xlen(int S) {
   const size_t cap = 160 * 1024 - 2 * 16 * sizeof(double) - 256;  // minus the reduction arrays (+ alignment slack)
   size_t base = 0;
   switch (S) {
-    case 2: base = init ? p2_lds_bytes<true, 2>(0) : p2_lds_bytes<false, 2>(0); break;
-    case 3: base = init ? p2_lds_bytes<true, 3>(0) : p2_lds_bytes<false, 3>(0); break;
-    case 4: base = init ? p2_lds_bytes<true, 4>(0) : p2_lds_bytes<false, 4>(0); break;
-    default: base = p2_lds_bytes<false, 5>(0); break;
+    case 2: base = p2_lds_bytes<2>(0); break;
+    case 3: base = p2_lds_bytes<3>(0); break;
+    case 4: base = p2_lds_bytes<4>(0); break;
+    default: base = p2_lds_bytes<5>(0); break;
   }
   if (base >= cap) return 0;
   return static_cast<int>((cap - base) / sizeof(double)) - (2 * S + 4);
+}
+
+// workgroup grid of a pass over box b: the (y, z) tile grid times the x chunks; returns the launch's block count
+int p2_grid(const LBox& b, const LeapfrogTbTiling& t, int S, int* nty, int* ntz, int* xlen, int* nxc) {
+  *nty = static_cast<int>(ceil_div(b.y1 - b.y0, kT));
+  *ntz = static_cast<int>(ceil_div(b.z1 - b.z0, kT));
+  const int tiles = *nty * *ntz;
+  const i64 nxb = b.x1 - b.x0;
+  i64 want = 1;
+  // x chunks when the tile grid alone leaves CUs idle (at least min_chunk planes each), or when the x sin table of
+  // the whole range would not fit the LDS
+  if (t.target_blocks > tiles) want = imin(ceil_div(t.target_blocks, tiles), imax(1, nxb / imax(1, t.min_chunk)));
+  const int maxlen = p2_max_xlen(S);
+  W3D_REQUIRE(maxlen >= 1, "leapfrog_p2: the tile does not fit in LDS");
+  want = imax(want, ceil_div(nxb, maxlen));
+  *xlen = static_cast<int>(ceil_div(nxb, want));
+  *nxc = static_cast<int>(ceil_div(nxb, *xlen));
+  const int blocks = tiles * *nxc;
+  return t.xcd_remap ? static_cast<int>(round_up(blocks, 8)) : blocks;
 }
 
 P2Plan make_plan_p2(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, LBox real, bool init) {
@@ -101,21 +121,7 @@ P2Plan make_plan_p2(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, L
   p.y1 = static_cast<int>(b.y1);
   p.z1 = static_cast<int>(b.z1);
   if (b.x1 <= b.x0 || b.y1 <= b.y0 || b.z1 <= b.z0) return pl;
-  p.nty = static_cast<int>(ceil_div(b.y1 - b.y0, kT));
-  p.ntz = static_cast<int>(ceil_div(b.z1 - b.z0, kT));
-  const int tiles = p.nty * p.ntz;
-  const i64 nxb = b.x1 - b.x0;
-  i64 want = 1;
-  // x chunks when the tile grid alone leaves CUs idle (at least min_chunk planes each), or when the x sin table of
-  // the whole range would not fit the LDS
-  if (t.target_blocks > tiles) want = imin(ceil_div(t.target_blocks, tiles), imax(1, nxb / imax(1, t.min_chunk)));
-  const int maxlen = p2_max_xlen(S, init);
-  W3D_REQUIRE(maxlen >= 1, "leapfrog_p2: the tile does not fit in LDS");
-  want = imax(want, ceil_div(nxb, maxlen));
-  p.xlen = static_cast<int>(ceil_div(nxb, want));
-  p.nxc = static_cast<int>(ceil_div(nxb, p.xlen));
-  const int blocks = tiles * p.nxc;
-  pl.nblocks = t.xcd_remap ? static_cast<int>(round_up(blocks, 8)) : blocks;
+  pl.nblocks = p2_grid(b, t, S, &p.nty, &p.ntz, &p.xlen, &p.nxc);
   p.nblocks = pl.nblocks;
   p.xcd_remap = t.xcd_remap ? 1 : 0;
   p.xper = pl.nblocks / 8;
@@ -135,10 +141,13 @@ bool leapfrog_p2_supported(const Layout& l, const LBox& box, int stages) {
 }
 
 int leapfrog_p2_partials(const Layout& l, const LBox& box, const LeapfrogTbTiling& t) {
-  LeapfrogTbTiling t1 = t;
-  t1.stages = 2;  // (block count: the tiling and the x chunks; S = 2 keeps the ghost-depth checks satisfiable)
-  const LBox real{-l.xg, l.nx + l.xg, 1, 0, 1, 0};
-  return make_plan_p2(l, box, t1, real, false).nblocks;
+  // (the largest block count over S = 2..5: the chunk length shrinks with S, whose levels share the LDS with the
+  // chunk's x sin table — ADVICE r5: S = 2 alone undercounted boxes longer than the S = 5 chunk)
+  (void)l;
+  if (box.x1 <= box.x0 || box.y1 <= box.y0 || box.z1 <= box.z0) return 0;
+  int n = 0, nty = 0, ntz = 0, xlen = 0, nxc = 0;
+  for (int S = 2; S <= 5; ++S) n = imax(n, p2_grid(box, t, S, &nty, &ntz, &xlen, &nxc));
+  return n;
 }
 
 std::vector<int> leapfrog_p2_table(int stages, std::vector<long>* geometry) {
@@ -148,9 +157,9 @@ std::vector<int> leapfrog_p2_table(int stages, std::vector<long>* geometry) {
     constexpr p2k::TabBuild<S> t = p2k::make_tab<S>();
     if (geometry)
       *geometry = {G::E, G::HY, G::HZ, G::PZ, p2k::kT,
-                   static_cast<long>(p2k::p2_lds_bytes<false, S>(p2k::p2_nxt<S>(512))),
-                   S <= 4 ? static_cast<long>(p2k::p2_lds_bytes<true, S>(p2k::p2_nxt<S>(512))) : 0L,
-                   static_cast<long>(p2_max_xlen(S, false)), S <= 4 ? static_cast<long>(p2_max_xlen(S, true)) : 0L};
+                   static_cast<long>(p2k::p2_lds_bytes<S>(p2k::p2_nxt<S>(512))),
+                   S <= 4 ? static_cast<long>(p2k::p2_lds_bytes<S>(p2k::p2_nxt<S>(512))) : 0L,
+                   static_cast<long>(p2_max_xlen(S)), S <= 4 ? static_cast<long>(p2_max_xlen(S)) : 0L};
     return std::vector<int>(t.t.d, t.t.d + p2k::kNT);
   };
   switch (stages) {

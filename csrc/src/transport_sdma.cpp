@@ -75,6 +75,8 @@ std::vector<GpuSolver::XLink> GpuSolver::sdma_links() const {
     // the peer's plan (its layout has the same ghost depths): this rank's index among its peers, and where its message
     // lands in the peer's staging for every pass depth
     const Layout pl = make_layout(prob_, rank_box(prob_, dims_, q.peer), 16, lay_.xg, lay_.yg, lay_.zg);
+    W3D_REQUIRE(opt_.temporal < static_cast<int>(sizeof(l.recv_off) / sizeof(l.recv_off[0])),
+                "sdma: pass depth beyond the link's offset table");
     for (int st = 2; st <= opt_.temporal; ++st) {
       const DeepPlan pp = make_deep_plan(pl, dims_, q.peer, st);
       int idx = -1;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # kernel traces of the 512^3 2x2x2 block rank 3/8 (fake rank), overlapped and sequential -> gpurun_out/blktrace/
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 rm -rf gpurun_out/blktrace; mkdir -p gpurun_out/blktrace
 for v in ovl seq; do
   extra=""; [ $v = seq ] && extra="--no-overlap"

@@ -15,4 +15,4 @@ if $m == 2:
 " > gpurun_out/guard_selftest_m$m.log 2>&1
   rc=$?; cat gpurun_out/guard_selftest_m$m.log; [ $rc -eq 0 ] || exit 1
 done
-bash scripts/gpu_ab_tests.sh
+bash tools/experiments/gpu_ab_tests.sh

@@ -2,7 +2,7 @@
 # Python Solver(runtime="process") vs the native CLI, same job shape (2 ranks sharing the GPU, copy engines, no RCCL),
 # 512^3 K=20: per-solve times -> gpurun_out/proc_parity.log
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export W3D_SHARE_GPUS=1 W3D_TIMEOUT_S=60
 for round in 1 2; do

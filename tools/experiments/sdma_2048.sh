@@ -1,7 +1,7 @@
 #!/bin/bash
 # 2048^3 2x2x2 block rank 3/8 (fake rank, copy-engine traffic real): 20 timed solves after 8 warmups per schedule
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/sdma2048
 for v in "--no-overlap" "--transport sdma" "--transport sdma --no-overlap"; do
   tag=$(echo "$v" | tr -d ' -')

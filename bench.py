@@ -63,7 +63,7 @@ def _args(argv=None):
     ap.add_argument("--L", type=float, default=1.0)
     ap.add_argument("--decomp", default="slab", help="slab | block | PxQxR (with --no-autotune)")
     ap.add_argument("--temporal", type=int, default=5,
-                    help="at most this many leapfrog steps per HBM pass (1..5; several ranks use at most 4)")
+                    help="at most this many leapfrog steps per HBM pass (1..5; the push transport uses at most 4)")
     ap.add_argument("--no-temporal", action="store_true", help="one leapfrog step per HBM pass")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--no-graph", action="store_true")

@@ -51,7 +51,7 @@ constexpr Personality kPersonalities[] = {
                "  --no-graph         eager launches instead of one captured hipGraph\n"
                "  --timers           per-phase GPU timers (init / compute / exchange / check)\n"
                "  --no-temporal      one leapfrog step per HBM pass (disable temporal blocking)\n"
-               "  --temporal S       at most S (2..5) leapfrog steps per HBM pass (default 5; several ranks: 4)\n"
+               "  --temporal S       at most S (2..5) leapfrog steps per HBM pass (default 5; the push transport: at most 4)\n"
                "  --no-tb            two-step register-queue passes instead of the LDS S-step kernel\n"
                "  --tb-min-planes M  slab ranks: LDS S-step passes with S-deep halos from M owned planes (default 16)\n"
                "  --deep-min-planes M  slab ranks without the LDS kernel: two-step passes from M planes (default 96)\n"

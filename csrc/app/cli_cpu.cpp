@@ -70,7 +70,7 @@ int run_cpu(const Args& a) {
       << ", \"phases_s\": {\"init\": " << jnum(rb.init_s) << ", \"compute\": " << jnum(rb.compute_s)
       << ", \"boundary\": " << jnum(rb.boundary_s) << ", \"exchange\": " << jnum(rb.exchange_s) << "}"
       << ", \"phases_slowest_rank_s\": {\"init\": " << jnum(rb.init_s) << ", \"compute\": " << jnum(rb.compute_s)
-      << ", \"boundary\": 0, \"exchange\": 0}"
+      << ", \"boundary\": " << jnum(rb.boundary_s) << ", \"exchange\": " << jnum(rb.exchange_s) << "}"
       << ", \"steps\": " << steps_json(r.steps, r.max_err, r.rms_err) << "}\n";
   }
   if (!a.dump.empty()) write_dump(a.dump, a.prob, s.layout(), s.field(0), 0, 1, Dims{1, 1, 1});

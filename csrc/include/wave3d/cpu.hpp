@@ -47,6 +47,55 @@ inline void shell_split(const LBox& full, const bool nb[3][2], std::vector<LBox>
   if (interior.x1 < interior.x0 || interior.y1 < interior.y0 || interior.z1 < interior.z0) interior = LBox{};
 }
 
+// Shell / interior split of a deep-tb unit whose exchange overlaps the rest of the pass (GpuSolver::tb_split). The
+// neighbours need the w = (next pass depth) nodes next to each face with a neighbour (edges and corners included). In
+// y and z the shell is made of whole rows / columns of the pass's tile grid (tile edge T ≥ w), so the shell boxes
+// recompute nothing the interior also computes; a remainder row narrower than w is replaced by the w rows next to
+// the face (its own one-row box: the core ends a row earlier). In z every cut lies an EVEN number of nodes from the
+// box's first node (the remainder box is widened to keep it so), so every sub-box starts and — unless it ends at the
+// rank's last node — ends on a whole 16-byte pair: the pair-tiled pass stores whole pairs and never writes a node of
+// another box. In x the shell is w planes of the remaining (y, z) core (recomputing S − 1 planes at the seam).
+// Boxes: the y border rows (whole x, whole z), the z border columns of the rows between (whole x), then the core's
+// x-face slabs; the interior is the core between the x slabs. Slab ranks (neighbours in x only): the two x slabs.
+inline void deep_split(const LBox& full, const bool nb[3][2], i64 w, i64 T, std::vector<LBox>& shells,
+                       LBox& interior) {
+  shells.clear();
+  interior = full;
+  // core range along a tiled axis: the border is the first / last tile row of the box, or — when the last row is a
+  // remainder narrower than w — the w (z: w rounded to a whole pair from the box start) rows next to the face
+  auto grid = [&](i64 b0, i64 b1, bool lo, bool hi, bool pair, i64& c0, i64& c1) {
+    const i64 nt = ceil_div(b1 - b0, T), rem = (b1 - b0) - (nt - 1) * T;
+    c0 = lo ? imin(b0 + T, b1) : b0;
+    i64 cut = rem >= w ? b0 + (nt - 1) * T : b1 - w;
+    if (pair) cut = b0 + ((cut - b0) & ~i64{1});
+    c1 = hi ? imax(cut, c0) : b1;
+  };
+  i64 ya, yb, za, zb;
+  grid(full.y0, full.y1, nb[1][0], nb[1][1], false, ya, yb);
+  grid(full.z0, full.z1, nb[2][0], nb[2][1], true, za, zb);
+  auto add = [&](const LBox& b) {
+    if (!b.empty()) shells.push_back(b);
+  };
+  add(LBox{full.x0, full.x1, full.y0, ya, full.z0, full.z1});
+  add(LBox{full.x0, full.x1, yb, full.y1, full.z0, full.z1});
+  add(LBox{full.x0, full.x1, ya, yb, full.z0, za});
+  add(LBox{full.x0, full.x1, ya, yb, zb, full.z1});
+  interior = LBox{full.x0, full.x1, ya, yb, za, zb};
+  if (interior.empty()) {
+    interior = LBox{};
+    return;
+  }
+  if (nb[0][0]) {
+    add(LBox{full.x0, imin(full.x0 + w, full.x1), ya, yb, za, zb});
+    interior.x0 = imin(full.x0 + w, full.x1);
+  }
+  if (nb[0][1]) {
+    const i64 x = imax(full.x1 - w, interior.x0);
+    add(LBox{x, full.x1, ya, yb, za, zb});
+    interior.x1 = x;
+  }
+}
+
 // Resume / loaded-field start: the rank's padded local array (owned nodes and every ghost layer that lies inside the
 // domain; ghosts beyond the global boundary and the row padding 0) from a GLOBAL (N+1)³ C-order field. With ghosts
 // of any depth filled from the global field, the first pass after a resume needs no halo exchange.

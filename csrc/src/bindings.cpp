@@ -239,6 +239,21 @@ PYBIND11_MODULE(_C, m) {
         return py::make_tuple(shell, interior);
       },
       "(shell boxes, interior box) of a compute box with neighbours nb[axis][side] (the runtime's own split)");
+  m.def(
+      "deep_split",
+      [](const LBox& full, const std::vector<std::vector<bool>>& nbv, i64 w, i64 tile) {
+        W3D_REQUIRE(nbv.size() == 3 && nbv[0].size() == 2 && nbv[1].size() == 2 && nbv[2].size() == 2,
+                    "deep_split: neighbours as [[x lo, x hi], [y lo, y hi], [z lo, z hi]]");
+        bool nb[3][2];
+        for (int a = 0; a < 3; ++a)
+          for (int s = 0; s < 2; ++s) nb[a][s] = nbv[static_cast<size_t>(a)][static_cast<size_t>(s)];
+        std::vector<LBox> shell;
+        LBox interior;
+        deep_split(full, nb, w, tile, shell, interior);
+        return py::make_tuple(shell, interior);
+      },
+      py::arg("full"), py::arg("nb"), py::arg("w"), py::arg("tile") = 32,
+      "(shell boxes, interior box) of a deep-tb unit whose exchange of depth w overlaps the pass (GpuSolver::tb_split)");
 
   // ---------------- CPU kernels ----------------
   m.def("cpu_set_threads", &cpu_set_threads);
@@ -628,6 +643,9 @@ PYBIND11_MODULE(_C, m) {
       .def("layout", [](GpuGroup& g, int rank) { return g.rank(rank).layout(); })
       .def("dims", [](GpuGroup& g) { return g.rank(0).dims(); })
       .def("mode", [](GpuGroup& g) { return g.rank(0).mode(); })
+      .def("temporal", [](GpuGroup& g) { return g.rank(0).options().temporal; },
+           "pass depth every rank runs (the constructor lowers the requested depth where a schedule needs it)")
+      .def("overlapped", [](GpuGroup& g) { return g.rank(0).overlapped(); })
       .def("comm_counts", &GpuGroup::comm_counts)
       .def("set_state", [](GpuGroup& g, const darr& prev, const darr& cur, int n0) {
         const i64 n = g.rank(0).problem().N + 1;

@@ -76,7 +76,7 @@ P2Plan make_plan_p2(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, L
   const int S = t.stages;
   W3D_REQUIRE(S >= 2 && S <= 5, "leapfrog_p2: stages must be 2..5");
   W3D_REQUIRE(!init || S <= 4, "leapfrog_p2: the analytic-start pass takes at most 4 steps");
-  W3D_REQUIRE(leapfrog_p2_supported(l, b, S), "leapfrog_p2: the box must span the rank's whole y/z interior");
+  W3D_REQUIRE(leapfrog_p2_supported(l, b, S), "leapfrog_p2: the box must lie in the rank's y/z range on whole pairs");
   const LBox full = compute_box(l);
   if (real.x0 > real.x1) {
     real.x0 = full.x0;
@@ -131,13 +131,15 @@ P2Plan make_plan_p2(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, L
 }  // namespace
 
 bool leapfrog_p2_supported(const Layout& l, const LBox& box, int stages) {
-  // the pass's tiles span the rank's whole y/z compute range (one rank, x slabs, or a 3-D block's whole box), pairs
-  // start on 16-byte nodes. (A y/z sub-box of the rank is refused: a pair that straddles its last z node stores its
-  // second node too — harmless beyond the rank's box, where the next exchange rewrites the ghost, but not into nodes
-  // another box of the same rank owns.)
+  // any box inside the rank's compute range in y/z (the whole range: one rank, x slabs, a 3-D block's whole box; or a
+  // sub-box: the overlapped block schedule's shells and interior, cpu.hpp deep_split) whose pairs start on 16-byte
+  // nodes and which ends on a whole pair unless it ends at the rank's last node: the pass stores whole pairs, so a box
+  // ending in the middle of a pair would also write the first node of the next box (beyond the rank's last node the
+  // second node of a pair is a ghost, which the next exchange rewrites)
   const LBox full = compute_box(l);
-  return stages >= 2 && stages <= 5 && box.y0 == full.y0 && box.y1 == full.y1 && box.z0 == full.z0 &&
-         box.z1 == full.z1 && l.yg >= 1 && l.zg >= 1 && (box.z0 + l.zg + l.zs) % 2 == 0;
+  return stages >= 2 && stages <= 5 && l.yg >= 1 && l.zg >= 1 && box.y0 >= full.y0 && box.y1 <= full.y1 &&
+         box.z0 >= full.z0 && box.z1 <= full.z1 && (box.z0 + l.zg + l.zs) % 2 == 0 &&
+         (box.z1 == full.z1 || (box.z1 - box.z0) % 2 == 0);
 }
 
 int leapfrog_p2_partials(const Layout& l, const LBox& box, const LeapfrogTbTiling& t) {

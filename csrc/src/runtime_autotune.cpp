@@ -40,7 +40,9 @@ std::vector<Candidate> autotune_candidates(int world, bool with_push, bool with_
   add("slab-S4-rsv16", "slab", "rccl", 4, true, 0, false, 16);
   if (with_sdma) {
     add("slab-S4-sdma-seq", "slab", "sdma", 4, false);
+    add("slab-S5-sdma-seq", "slab", "sdma", 5, false);
     add("slab-S4-sdma", "slab", "sdma", 4, true);
+    add("slab-S5-sdma", "slab", "sdma", 5, true);  // (the 5-step pass beside the copy-engine transfer)
   }
   if (with_push) {
     add("slab-S4-push-seq", "slab", "push", 4, false);
@@ -53,11 +55,14 @@ std::vector<Candidate> autotune_candidates(int world, bool with_push, bool with_
     add("block-S4-seq", "block", "rccl", 4, false);
     add("block-S5-seq", "block", "rccl", 5, false);  // (pair-tiled 5-step passes over the whole block)
     add("block-S4", "block", "rccl", 4, true);
+    add("block-S5", "block", "rccl", 5, true);  // (pair-tiled shells and interior, cut on whole pairs)
     add("block-S4-conc", "block", "rccl", 4, true, 0, true);  // (shells beside the interior)
     add("block-S4-rsv16", "block", "rccl", 4, true, 0, false, 16);
     if (with_sdma) {
       add("block-S4-sdma-seq", "block", "sdma", 4, false);
+      add("block-S5-sdma-seq", "block", "sdma", 5, false);
       add("block-S4-sdma", "block", "sdma", 4, true);         // (one copy stream)
+      add("block-S5-sdma", "block", "sdma", 5, true);
       add("block-S4-sdma-x2", "block", "sdma", 4, true, 2);  // (two copy streams: two engines)
     }
     add("block-S3", "block", "rccl", 3, true);

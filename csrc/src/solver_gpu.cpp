@@ -180,7 +180,8 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
       mn[2] = imin(mn[2], b.nz());
     }
     const int rem = prob_.K - (analytic_ok() ? 1 : 2);  // steps left to the passes (each takes 2..temporal)
-    const i64 T2 = 2 * (slab ? opt_.temporal : std::min(opt_.temporal, 4));
+    // (the pass depth every rank will use: 5-step passes everywhere but on the push transport, see below)
+    const i64 T2 = 2 * (opt_.push ? std::min(opt_.temporal, 4) : opt_.temporal);
     // 3-D blocks: S-deep ghosts on every split axis, one exchange (faces, edges, corners) between passes
     const bool block_fits = (dims_.px == 1 || mn[0] >= imax(T2, 8)) && (dims_.py == 1 || mn[1] >= imax(T2, 8)) &&
                             (dims_.pz == 1 || mn[2] >= imax(T2, 8));
@@ -194,11 +195,11 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
       mode_ = Mode::kDeep;
   }
   block_tb_ = mode_ == Mode::kDeepTb && !slab;
-  // (3-D blocks: 5-step passes with the exchange after each pass only — the overlapped schedule's shell boxes are y/z
-  // sub-boxes of the rank, which the pair-tiled kernel does not take; their z-face pack is the pack kernel's)
-  if (opt_.temporal == 5 && world > 1 && (mode_ != Mode::kDeepTb || (block_tb_ && opt_.overlap) || opt_.push))
-    opt_.temporal = 4;
-  if (block_tb_ && opt_.temporal == 5) opt_.fused_pack = false;
+  // (3-D blocks, overlapped or not, take 5-step pair-tiled passes: the overlapped schedule's shell and interior boxes
+  // are cut on whole pairs, cpu.hpp deep_split; the push transport's forwarding stores are k_leapfrog_tb's)
+  if (opt_.temporal == 5 && world > 1 && (mode_ != Mode::kDeepTb || opt_.push)) opt_.temporal = 4;
+  // (the fused z-face pack lives in k_leapfrog_tb: with the pair-tiled pass the pack kernel packs the z faces too)
+  if (block_tb_ && opt_.tiling_tb.p2) opt_.fused_pack = false;
   if (opt_.push && world > 1) {
     W3D_REQUIRE(mode_ == Mode::kDeepTb && !block_tb_, "push transport: slab LDS passes (deep-tb) only, not " + mode());
     push_ = true;
@@ -579,9 +580,8 @@ void GpuSolver::build_units() {
     // the pair-tiled passes (k_leapfrog_p2, one rank): µs per step at 512³ (profiles/r5/)
     static const double kStepCostP2[6] = {0.0, 610.0, 430.0, 290.0, 225.0, 180.0};
     static const double kAnalyticCostP2[6] = {0.0, 1e9, 300.0, 200.0, 135.0, 1e9};
-    // (slab ranks too: their passes span the whole y/z range, shells included; block ranks when the exchange follows
-    // the pass: every pass is then the rank's whole box)
-    const bool p2 = opt_.tiling_tb.p2 && !push_ && (!block_tb_ || !opt_.overlap) && leapfrog_p2_supported(lay_, full_, 2);
+    // (slab ranks and 3-D block ranks too: their shell / interior boxes are cut on whole pairs)
+    const bool p2 = opt_.tiling_tb.p2 && !push_ && leapfrog_p2_supported(lay_, full_, 2);
     const double* kStepCost = p2 ? kStepCostP2 : kStepCostTb;
     const double* kAnalyticCost = p2 ? kAnalyticCostP2 : kAnalyticCostTb;
     const int rem = K - n, smax = opt_.temporal, smin = mode_ == Mode::kDeepTb ? 2 : 1;
@@ -902,54 +902,16 @@ void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase, hipStream_t s
   if (mask) ++tb_slots_;
 }
 
-// The shell / interior split of a deep-tb unit whose exchange overlaps the next part of the pass. The neighbours need
-// the w = (next pass depth) nodes next to each face with a neighbour (edges and corners included). In y and z the
-// shell is made of whole rows / columns of the pass's 32 × 32 tile grid (w ≤ 32), so the shell boxes recompute nothing
-// the interior also computes (a remainder row narrower than w: the w rows themselves); in x it is w planes of the
-// remaining (y, z) core (recomputing S − 1 planes at the seam).
-// Boxes: the y border rows (whole x, whole z), the z border columns of the rows between (whole x), then the core's
-// x-face slabs; the interior is the core between the x slabs. Slab ranks: just the two x slabs.
+// The shell / interior split of a deep-tb unit whose exchange overlaps the next part of the pass: cpu.hpp deep_split
+// with w = the next pass's depth (its z cuts lie on whole pairs, so every box runs on the pair-tiled pass).
 void GpuSolver::tb_split(int i, std::vector<LBox>& shells, LBox& interior) const {
   shells.clear();
   interior = full_;
   if (!needs_exchange(i) || late_exchange()) return;
-  const i64 w = units_[static_cast<size_t>(i) + 1].steps, T = kTbTile;
-  const LBox f = full_;
   bool nb[3][2];
   for (int a = 0; a < 3; ++a)
     for (int sd = 0; sd < 2; ++sd) nb[a][sd] = neighbor_rank(dims_, rank_, a, sd) >= 0;
-  // core range along a tiled axis: the border is the first / last tile row of the box, or — when the last row is a
-  // remainder narrower than w — exactly the w rows next to the face (its own one-row box; the core then ends a row
-  // earlier, so the total tile rows stay the same)
-  auto grid = [&](i64 b0, i64 b1, bool lo, bool hi, i64& c0, i64& c1) {
-    const i64 nt = ceil_div(b1 - b0, T), rem = (b1 - b0) - (nt - 1) * T;
-    c0 = lo ? imin(b0 + T, b1) : b0;
-    c1 = hi ? imax(rem >= w ? b0 + (nt - 1) * T : b1 - w, c0) : b1;
-  };
-  i64 ya, yb, za, zb;
-  grid(f.y0, f.y1, nb[1][0], nb[1][1], ya, yb);
-  grid(f.z0, f.z1, nb[2][0], nb[2][1], za, zb);
-  auto add = [&](const LBox& b) {
-    if (!b.empty()) shells.push_back(b);
-  };
-  add(LBox{f.x0, f.x1, f.y0, ya, f.z0, f.z1});
-  add(LBox{f.x0, f.x1, yb, f.y1, f.z0, f.z1});
-  add(LBox{f.x0, f.x1, ya, yb, f.z0, za});
-  add(LBox{f.x0, f.x1, ya, yb, zb, f.z1});
-  interior = LBox{f.x0, f.x1, ya, yb, za, zb};
-  if (interior.empty()) {
-    interior = LBox{};
-    return;
-  }
-  if (nb[0][0]) {
-    add(LBox{f.x0, imin(f.x0 + w, f.x1), ya, yb, za, zb});
-    interior.x0 = imin(f.x0 + w, f.x1);
-  }
-  if (nb[0][1]) {
-    const i64 x = imax(f.x1 - w, interior.x0);
-    add(LBox{x, f.x1, ya, yb, za, zb});
-    interior.x1 = x;
-  }
+  deep_split(full_, nb, units_[static_cast<size_t>(i) + 1].steps, kTbTile, shells, interior);
   W3D_REQUIRE(static_cast<int>(shells.size()) < kTbSlots, "deep-tb: too many shell boxes");
 }
 

@@ -50,6 +50,8 @@ def test_autotune_fake_rank_candidates(gpu, tmp_path):
     meta, _ = _run(tmp_path, "128", "0.001", "20", "1", "--fake-rank", "1/4", "--repeat", "2")
     tuned = meta["autotune_s"]
     assert {"slab-S4-seq", "slab-S4", "slab-S4-sdma", "block-S4-seq", "block-S4", "block-S4-sdma"} <= set(tuned)
+    # (round 6: the 5-step pair-tiled pass beside the copy engines, and on overlapped 3-D blocks)
+    assert {"slab-S5-sdma", "slab-S5-sdma-seq", "block-S5", "block-S5-sdma", "block-S5-sdma-seq"} <= set(tuned)
     assert not any("push" in k for k in tuned)  # push only on request
     _chosen_ok(meta)
 

@@ -288,13 +288,16 @@ def test_block_overlap_geometries(gpu, world, decomp, N, transport):
 def test_block_fused_zface_pack(gpu, world, decomp, N, overlap, transport, fused):
     """The z-face message parts are written by the pass itself (TbPack) or, with fused_pack=False,
     gathered by the pack kernel like the x / y faces: both bit-identical to one GPU with NaN-poisoned ghosts (a z-face
-    node the pass failed to store would arrive as a stale value of an earlier pass)."""
+    node the pass failed to store would arrive as a stale value of an earlier pass). The fused pack is k_leapfrog_tb's
+    (S ≤ 4): with the pair-tiled pass on (the default) block ranks pack with the pack kernel, so fused=True runs the
+    older kernel (tiling_tb p2 off)."""
     spec = ProblemSpec(N=N, tau=1e-3, K=20)
     ref = Solver(spec, backend="hip", device=0, temporal=1)
     r1 = ref.run()
     f0 = ref.global_field(0)
     g = Solver(spec, backend="hip", transport=transport, world=world, rank=0, decomp=decomp, device=0,
-               overlap=overlap, poison_ghosts=transport != "rccl-self", fused_pack=fused)
+               overlap=overlap, poison_ghosts=transport != "rccl-self", fused_pack=fused,
+               tiling_tb={"p2": False} if fused else None, temporal=4 if fused else 5)
     assert g.native.mode() == "deep-tb-block"
     for _ in range(2):
         r = g.run()
@@ -315,8 +318,31 @@ def test_block_fused_zface_pack_mixed_depths(gpu, world, decomp, K, temporal, tr
     r1 = ref.run()
     f0 = ref.global_field(0)
     g = Solver(spec, backend="hip", transport=transport, world=world, rank=0, decomp=decomp, device=0, overlap=False,
-               poison_ghosts=True, fused_pack=True, temporal=temporal)
+               poison_ghosts=True, fused_pack=True, temporal=temporal, tiling_tb={"p2": False})
     for _ in range(2):
         r = g.run()
         _same(r, r1)
         assert torch.equal(g.global_field(0), f0)
+
+
+@pytest.mark.parametrize("transport", ["loopback", "sdma"])
+@pytest.mark.parametrize("temporal", [2, 3, 4, 5])
+@pytest.mark.parametrize("world,decomp,N", [(8, "2x2x2", 70), (4, "2x2x1", 66), (4, "1x2x2", 67), (27, "3x3x3", 100)])
+def test_block_overlap_p2_bitexact(gpu, world, decomp, N, temporal, transport):
+    """Round 6: overlapped 3-D block ranks run the pair-tiled pass (S = 2..5) on their shell and interior boxes, which
+    are cut on whole 16-byte pairs (cpu.hpp deep_split), so no pass writes a node of another box. Bit-identical to one
+    GPU with NaN-poisoned ghosts, eager and graph-replayed; N = 67 gives odd rank extents (remainder boxes widened to
+    a whole pair), N = 100 over 3 a remainder tile row narrower than the halo. (K = 21: S = 2 needs an even number of
+    steps after the analytic start.)"""
+    spec = ProblemSpec(N=N, tau=1e-3, K=21)
+    ref = Solver(spec, backend="hip", device=0, temporal=1)
+    r1 = ref.run()
+    f0, f1 = ref.global_field(0), ref.global_field(1)
+    g = Solver(spec, backend="hip", transport=transport, world=world, rank=0, decomp=decomp, device=0,
+               overlap=True, poison_ghosts=True, temporal=temporal)
+    assert g.native.mode() == "deep-tb-block" and g.native.temporal() == temporal and g.native.overlapped()
+    for _ in range(2):
+        r = g.run()
+        _same(r, r1)
+        assert torch.equal(g.global_field(0), f0)
+        assert torch.equal(g.global_field(1), f1)

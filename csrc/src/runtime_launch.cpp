@@ -263,7 +263,9 @@ HostColl HostColl::files(int rank, int world) {
   h.barrier = [gather] { (void)gather("b"); };
   // the serve loop's barrier before a solve: the peer ranks' Python callers may spend any time between run()
   // calls, so it waits as long as this rank's parent lives — or W3D_PROC_TIMEOUT_S if set, the bound the
-  // Python side (NativeRankProcess) puts on every reply (the other file collectives: W3D_FILE_TIMEOUT_S, 120 s)
+  // Python side (NativeRankProcess) puts on every reply (the other file collectives: W3D_FILE_TIMEOUT_S, 120 s). A
+  // rank whose peer died does not poll forever: its own caller's reply wait (300 s by default) kills it
+  // (native_proc.py _read), and PDEATHSIG ends it with its parent
   h.idle_barrier = [gather_t] {
     const char* v = std::getenv("W3D_PROC_TIMEOUT_S");
     (void)gather_t("b", v && std::atof(v) > 0.0 ? std::atof(v) : -1.0);

@@ -30,7 +30,6 @@ struct Args {
   bool tb = true;
   int tb_threads = 0;
   int tb_init_threads = 0;
-  int p2_pairs = 0;           // --p2-pairs (0: the solver default)
   bool init2 = true;
   int fake_rank = -1, fake_world = 0;
   bool fake_traffic = false;  // --fake-traffic: the fake rank sends / receives its real messages to itself over RCCL

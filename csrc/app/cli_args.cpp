@@ -56,7 +56,6 @@ constexpr Personality kPersonalities[] = {
                "  --tb-min-planes M  slab ranks: LDS S-step passes with S-deep halos from M owned planes (default 16)\n"
                "  --deep-min-planes M  slab ranks without the LDS kernel: two-step passes from M planes (default 96)\n"
                "  --tb-threads T     LDS S-step kernel workgroup size (768 or 1024; default 1024)\n"
-               "  --p2-pairs P       pair-tiled pass: pairs per thread, 1 (1024 threads) or 2 (512 threads; S = 4, 5)\n"
                "  --tb-init-threads T  ... of the analytic-start pass (768 or 1024; default 768)\n"
                "  --no-init2         start from u0,u1 + a first step instead of analytic u1,u2\n"
                "  --debug-sync       synchronize after every step (race triage)\n"
@@ -143,7 +142,6 @@ Args parse(int argc, char** argv) {
     else if (s == "--no-tb") a.tb = false;
     else if (s == "--tb-threads") a.tb_threads = std::stoi(next());
     else if (s == "--tb-init-threads") a.tb_init_threads = std::stoi(next());
-    else if (s == "--p2-pairs") a.p2_pairs = std::stoi(next());
     else if (s == "--no-init2") a.init2 = false;
     else if (s == "--t2-rows") a.t2_rows = std::stoi(next());
     else if (s == "--deep-min-planes") a.deep_min = std::stoi(next());
@@ -314,7 +312,6 @@ SolverOptions options_from(const Args& a, bool fake) {
   o.tb = a.tb;
   if (a.tb_threads > 0) o.tiling_tb.threads = a.tb_threads;
   if (a.tb_init_threads > 0) o.tiling_tb.init_threads = a.tb_init_threads;
-  if (a.p2_pairs > 0) o.tiling_tb.p2_pairs = a.p2_pairs == 2 ? 2 : 1;
   o.init2 = a.init2;
   o.fake_comm = fake;
   o.fake_traffic = fake && a.fake_traffic;

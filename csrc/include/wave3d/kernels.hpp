@@ -88,7 +88,6 @@ struct LeapfrogTbTiling {
   int target_blocks = 256; // fewer (y,z) tiles than this: split x into chunks (one workgroup per CU at 1 WG/CU)
   int min_chunk = 16;      // ... of at least this many planes (each chunk recomputes S−1 planes on both sides)
   bool p2 = true;          // the pair-tiled pass (k_leapfrog_p2, S ≤ 5) wherever it applies (leapfrog_p2_supported)
-  int p2_pairs = 1;        // ... pairs per thread: 1 (1024-thread workgroups) or 2 (512 threads, 256 VGPRs; S = 4, 5)
 };
 // Slab peer-push transport of an LDS pass (x faces only; every slab rank has the same plane geometry, so a plane's
 // in-plane offsets are the same on both sides). The pass

@@ -339,10 +339,6 @@ __device__ __forceinline__ int p2_desc(int tid) {
 // an immediate offset from one of them (a 1024-thread workgroup has 128 VGPRs per lane: no room for one address
 // register per plane).
 //
-// PT = pairs per thread (round 6, A/B): PT = 2 runs the same 1024 positions with 512 threads and 256 VGPRs per lane —
-// thread t holds table positions t (a tile pair: every stage, checks, both stores from its own registers) and t + 512
-// (the halo / ring role of wave t/64 + 8), the two chains interleaved stage by stage.
-//
 // Perf-attribution builds only (results wrong; tools/build.py W3D_EXTRA_DEFS_P2=-D…, profiles/r5/p2_attribution.md):
 //   W3D_EXPERIMENT_NOLOAD    every plane load hits one of 4 resident planes (no HBM reads)
 //   W3D_EXPERIMENT_NOSTORE   the pass writes nothing to HBM
@@ -352,25 +348,16 @@ __device__ __forceinline__ int p2_desc(int tid) {
 // p2_attribution.md): deferred stores, two-plane-ahead prefetch, staggered waves, conditional queue writes, the late
 // u^n load point, row-major halo lanes, split stores in the analytic start, stores from every wave, a separate
 // interior-tile body, Dirichlet selects after every stage, the ring waves loading u^{n−1}, a φ plane in LDS.
-template <int S, int CM, bool INIT, bool CH, int PT>
-__global__ __launch_bounds__(kNT / PT) void k_leapfrog_p2(const P2Params p) {
-  static_assert(PT == 1 || PT == 2, "p2: one or two pairs per thread");
+template <int S, int CM, bool INIT, bool CH>
+__global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
   using G = Geo<S>;
   constexpr int E = G::E, R0 = G::R0, R1 = G::R1;
-  constexpr int NT = kNT / PT;  // threads of the workgroup
   // late loads (S ≥ 4): u^n plane i+2 right after the commit (into plane i−2's dead slot), u^{n−1} plane i+1 after
   // stage 1 (into the register stage 1 just consumed); the vector-memory sequence of an iteration is load, load,
   // stores — the next commit waits for its load, never for a store
   constexpr bool kLate = !INIT && S >= 4;
-  // (A/B, two pairs per thread only: both fields loaded one plane further ahead — u^n plane i+3 and u^{n−1} plane i+2
-  // — into two extra registers per position that become the queue slots one iteration later)
-#ifndef P2_PT2_DEEP
-#define P2_PT2_DEEP 0
-#endif
-  constexpr bool kDeep = kLate && PT == 2 && P2_PT2_DEEP;
-  // split stores (5-step passes, one pair per thread): the own waves store level S, the other 8 waves level S−1
-  // (below); with two pairs per thread the thread holding a tile pair stores both levels from its registers
-  constexpr bool kSplitSt = !INIT && S == 5 && PT == 1;
+  // split stores (5-step passes): the own waves store level S, the other 8 waves level S−1 (below)
+  constexpr bool kSplitSt = !INIT && S == 5;
   extern __shared__ double lds[];
   const int tid = static_cast<int>(threadIdx.x);
   int blk = static_cast<int>(blockIdx.x);
@@ -380,12 +367,11 @@ __global__ __launch_bounds__(kNT / PT) void k_leapfrog_p2(const P2Params p) {
   }
   const int ntiles = p.nty * p.ntz;
   const bool active = blk < ntiles * (CH ? p.nxc : 1);
-  // error-check accumulators (position 0 only: the tile's own pairs are always a thread's first position), one per
-  // node of the pair (lo, hi) and checked level; a pair's nodes that are not checked (Dirichlet, or beyond the box)
-  // are masked out once, in the reduction, not at every plane
+  // error-check accumulators, one per node of the pair (lo, hi) and checked level; a pair's nodes that are not checked
+  // (Dirichlet, or beyond the box) are masked out once, in the reduction, not at every plane
   // (registers: ≤ 3 checked levels, in the 5-step passes and the 4-step analytic start — the production passes; the
   // others are at or near 128 VGPRs already)
-  constexpr bool kSplitAcc = __builtin_popcount(CM) <= 3 && (S == 5 || (INIT && S == 4) || PT == 2);
+  constexpr bool kSplitAcc = __builtin_popcount(CM) <= 3 && (S == 5 || (INIT && S == 4));
   double emax[S][2], esum[S][2];
   static_for<0, S>([&](auto kc) __attribute__((always_inline)) {
     constexpr int k = decltype(kc)::value;
@@ -414,71 +400,50 @@ __global__ __launch_bounds__(kNT / PT) void k_leapfrog_p2(const P2Params p) {
     const int xtab0 = S + 1 - wx0;  // plane x ↔ sxw[x + xtab0]
     {
       auto sc = [&](int g) __attribute__((always_inline)) { return p.s[g < -1 ? -1 : g > N + 1 ? N + 1 : g]; };
-      for (int t = tid; t < G::NY; t += NT) syw[t] = sc(p.gy0 + ty0 - (S - 1) - 2 + t);
-      for (int t = tid; t < G::NZ; t += NT) szw[t] = sc(p.gz0 + tz0 - E - 4 + t);
+      for (int t = tid; t < G::NY; t += kNT) syw[t] = sc(p.gy0 + ty0 - (S - 1) - 2 + t);
+      for (int t = tid; t < G::NZ; t += kNT) szw[t] = sc(p.gz0 + tz0 - E - 4 + t);
       if (p.check_mask || INIT)
-        for (int t = tid; t < p2_nxt<S>(wx1 - wx0); t += NT) sxw[t] = sc(p.gx0 + wx0 - S - 1 + t);
+        for (int t = tid; t < p2_nxt<S>(wx1 - wx0); t += kNT) sxw[t] = sc(p.gx0 + wx0 - S - 1 + t);
     }
 
-    // ---- the thread's positions (pairs) and their waves' roles
-    // (per position q: table entry tid + q·NT; a, b region row / pair column; the wave-uniform role and stage count)
-    int a[PT], b[PT], wst[PT];
-    bool act[PT], reg[PT];
-    unsigned goff[PT], soff[PT];
-    bool rl[PT], rh[PT];
-    double lam_lo[PT], lam_hi[PT];
-    int prev_bytes[PT];
-    lchar *b0[PT], *bA[PT], *bB[PT];
-    const int pbytes = static_cast<int>(P * 8);
-    static_for<0, PT>([&](auto qc) __attribute__((always_inline)) {
-      constexpr int q = decltype(qc)::value;
-      const int dsc = p2_desc<S>(tid + q * NT);
-      a[q] = (dsc & 0xFF) - 2;
-      b[q] = ((dsc >> 8) & 0xFF) - 2;
-      const int wd = __builtin_amdgcn_readfirstlane(dsc);
-      const int wlv = (wd >> 16) & 0xF;    // region waves: stages 1..wlv
-      const int wkind = (wd >> 20) & 0x3;  // 1 region, 2 ring, 0 none
-      act[q] = wkind != 0;
-      reg[q] = wkind == 1;
-      // stages this position's wave computes (a scalar: the stage tests must stay scalar branches, not lane masks)
-      wst[q] = __builtin_amdgcn_readfirstlane(wkind == 1 ? wlv : 0);
-      const int y = ty0 - (S - 1) + a[q], z = tz0 - E + 2 * b[q];
-      const int el = z + p.za;  // element of the pair's first node in its row
-      const bool ldv = act[q] && y >= p.ay0 && y < p.ay1 && el >= 0 && el + 2 <= p.pitch;
-      goff[q] = ldv ? static_cast<unsigned>(((y + p.ya) * p.pitch + el) * 8) : kOob;
-      const bool ry = inside(p.gy0 + y);
-      rl[q] = ry && inside(p.gz0 + z);
-      rh[q] = ry && inside(p.gz0 + z + 1);
-      const bool inner = reg[q] && wlv == S;  // the tile's own pairs
-      const bool sty = inner && y < p.y1 && z < p.z1;  // own pair stored (z + 1 ≤ z1: the box spans the z interior)
-      soff[q] = sty ? goff[q] : kOob;
-      if constexpr (q == 0) {
-        okl = sty && rl[q];
-        okh = sty && rh[q] && z + 1 < p.z1;
-      }
-      // Dirichlet nodes through τ²: a node outside the global interior has τ² = 0 and c = old = +0 at every level
-      // (zero loads, zero φ, and this very update), so fma(0, Δ, fma(2, +0, −(+0))) = +0 — the select's value, bit
-      // for bit, without 4 selects per pair and stage
-      lam_lo[q] = rl[q] ? p.tau2 : 0.0;
-      lam_hi[q] = rh[q] ? p.tau2 : 0.0;
-      // u^{n−1} is read by the region waves only (the stage-1 update); the u^n ring waves get a zero-size descriptor
-      // for it — same instruction sequence, no memory traffic (a scalar: wd is wave-uniform)
-      prev_bytes[q] = wkind == 1 ? pbytes : 0;
-      // per-position LDS byte bases (all accesses: a compile-time offset from one of them; 32-bit LDS-address-space
-      // pointers — a generic pointer is a 64-bit register pair)
-      const int lo0 = (a[q] + 1) * R0 + (b[q] + 1);  // level-0 slot index of the pair
-      const int lk = a[q] * R1 + b[q];                // compact slot index (region pairs)
-      b0[q] = lds_base + (lo0 - R0 - 1) * 16;  // (neighbour offsets from −R0−1 pairs up: never negative)
-      bA[q] = lds_base + (G::lk0() + lk - R1 - 1) * 16;
-      bB[q] = bA[q] + 4 * G::P1 * 16;
-    });
-    // (scalar) the first position is a tile pair; the levels it checks (a scalar int, re-asserted per iteration like
-    // wst: a loop-invariant bool is kept as a 64-bit lane mask, and each stage's test then cost a v_cndmask + v_cmp
-    // pair to negate it)
-    const bool winner = wst[0] == S;
+    // ---- this thread's pair and its wave's role
+    const int dsc = p2_desc<S>(tid);
+    const int a = (dsc & 0xFF) - 2, b = ((dsc >> 8) & 0xFF) - 2;
+    const int wd = __builtin_amdgcn_readfirstlane(dsc);
+    const int wlv = (wd >> 16) & 0xF;           // region waves: stages 1..wlv
+    const int wkind = (wd >> 20) & 0x3;         // 1 region, 2 ring, 0 none
+    const bool act = wkind != 0;
+    const bool reg = wkind == 1;
+    const bool inner = reg && wlv == S;         // the tile's own pairs
+    // stages this wave computes (a scalar: the stage tests must stay scalar branches, not lane masks)
+    int wst = __builtin_amdgcn_readfirstlane(wkind == 1 ? wlv : 0);
+    const bool winner = wst == S;               // (scalar) the tile's own pairs
+    // levels this wave checks (a scalar int, re-asserted per iteration like wst: a loop-invariant bool is kept as a
+    // 64-bit lane mask, and each stage's test then cost a v_cndmask + v_cmp pair to negate it)
     int wchk = __builtin_amdgcn_readfirstlane(winner ? p.check_mask : 0);
-    lchar* rt = lds_base + (2 * G::pairs() + a[0] + 2) * 8;                  // check: s_y of the own row
-    lchar* szp = lds_base + (2 * G::pairs() + G::NY + 2 * b[0] + 4) * 8;   // check: own (s_z, s_z+1)
+    const int y = ty0 - (S - 1) + a, z = tz0 - E + 2 * b;
+    const int el = z + p.za;                    // element of the pair's first node in its row
+    const bool ldv = act && y >= p.ay0 && y < p.ay1 && el >= 0 && el + 2 <= p.pitch;
+    const unsigned goff = ldv ? static_cast<unsigned>(((y + p.ya) * p.pitch + el) * 8) : kOob;
+    const bool ry = inside(p.gy0 + y);
+    const bool rl = ry && inside(p.gz0 + z), rh = ry && inside(p.gz0 + z + 1);
+    const bool sty = inner && y < p.y1 && z < p.z1;      // own pair stored (z + 1 ≤ z1: the box spans the z interior)
+    const unsigned soff = sty ? goff : kOob;
+    okl = sty && rl;
+    okh = sty && rh && z + 1 < p.z1;
+    // Dirichlet nodes through τ²: a node outside the global interior has τ² = 0 and c = old = +0 at every level (zero
+    // loads, zero φ, and this very update), so fma(0, Δ, fma(2, +0, −(+0))) = +0 — the select's value, bit for bit,
+    // without 4 selects per pair and stage
+    const double lam_lo = rl ? p.tau2 : 0.0, lam_hi = rh ? p.tau2 : 0.0;
+    // per-thread LDS byte bases (all accesses: a compile-time offset from one of them)
+    const int lo0 = (a + 1) * R0 + (b + 1);     // level-0 slot index of the pair
+    const int lk = a * R1 + b;                  // compact slot index (region pairs)
+    // (32-bit LDS-address-space pointers: a generic pointer is a 64-bit register pair)
+    lchar* b0 = lds_base + (lo0 - R0 - 1) * 16;  // (neighbour offsets from −R0−1 pairs up: never negative)
+    lchar* bA = lds_base + (G::lk0() + lk - R1 - 1) * 16;
+    lchar* bB = bA + 4 * G::P1 * 16;
+    lchar* rt = lds_base + (2 * G::pairs() + a + 2) * 8;                          // check: s_y of the own row
+    lchar* szp = lds_base + (2 * G::pairs() + G::NY + 2 * b + 4) * 8;           // check: own (s_z, s_z+1)
     // Split stores (kSplitSt): the 8 waves that do not own the tile store level S−1 of the own pairs — lane j of
     // wave 8 + w the pair of lane j of own wave w, read back from the level's compact LDS plane one iteration after
     // it was computed — and the own waves store level S only. Every wave then issues exactly one store per iteration,
@@ -496,33 +461,35 @@ __global__ __launch_bounds__(kNT / PT) void k_leapfrog_p2(const P2Params p) {
     // (re-declared opaque at every iteration: otherwise the loop-invariant "base + offset" of every access is hoisted
     // out of the x march into a register of its own — 15 address VGPRs and spills — instead of the offset field)
     auto opaque_bases = [&]() __attribute__((always_inline)) {
-      static_for<0, PT>([&](auto qc) __attribute__((always_inline)) {
-        constexpr int q = decltype(qc)::value;
-        asm volatile("" : "+v"(b0[q]), "+v"(bA[q]), "+v"(bB[q]), "+s"(wst[q]));
-        wst[q] = __builtin_amdgcn_readfirstlane(wst[q]);  // (an asm output is not known uniform: re-assert it)
-      });
       if constexpr (kSplitSt)
-        asm volatile("" : "+v"(rt), "+s"(wchk));
+        asm volatile("" : "+v"(b0), "+v"(bA), "+v"(bB), "+v"(rt), "+s"(wst), "+s"(wchk));
       else
-        asm volatile("" : "+v"(rt), "+v"(szp), "+s"(wchk));
+        asm volatile("" : "+v"(b0), "+v"(bA), "+v"(bB), "+v"(rt), "+v"(szp), "+s"(wst), "+s"(wchk));
+      wst = __builtin_amdgcn_readfirstlane(wst);  // (an asm output is not known uniform: re-assert it)
       wchk = __builtin_amdgcn_readfirstlane(wchk);
     };
     // slot / neighbour offsets (bytes): level-0 slot s, compact plane pl = (k−1)·2 + parity
     auto o0 = [](int sl, int dy, int dz) constexpr { return sl * G::P0 * 16 + ((dy + 1) * R0 + dz + 1) * 16; };
     auto ok_ = [](int pl, int dy, int dz) constexpr { return (pl & 3) * G::P1 * 16 + ((dy + 1) * R1 + dz + 1) * 16; };
+    auto kb = [&](int pl) __attribute__((always_inline)) { return pl < 4 ? bA : bB; };
 
     // plane buffers: base = field + (x + 1)·plane, P·8 bytes (every in-plane offset < P)
     auto rsrc = [&](const double* f, int xs, int bytes) __attribute__((always_inline)) {
       return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(f) + static_cast<i64>(xs + 1) * P, (short)0, bytes,
                                                0x00020000);
     };
-    auto load_pair = [&](auto bkc, const double* f, int x, unsigned off, int bytes) __attribute__((always_inline)) -> D2 {
+    const int pbytes = static_cast<int>(P * 8);
+    // u^{n−1} is read by the region waves only (the stage-1 update); the u^n ring waves get a zero-size descriptor for
+    // it — same instruction sequence, no memory traffic (a scalar: wd is wave-uniform)
+    const int prev_bytes = ((wd >> 20) & 0x3) == 1 ? pbytes : 0;
+    auto load_pair = [&](auto bkc, const double* f, int x) __attribute__((always_inline)) -> D2 {
 #ifdef W3D_EXPERIMENT_NOLOAD
       const int xs = (x & 3) + 1;
 #else
       const int xs = decltype(bkc)::value ? x : x < p.ax0 ? p.ax0 : x >= p.ax1 ? p.ax1 - 1 : x;
 #endif
-      return as_d2(__builtin_amdgcn_raw_buffer_load_b128(rsrc(f, xs, bytes), static_cast<int>(off), 0, kLoadAux));
+      return as_d2(__builtin_amdgcn_raw_buffer_load_b128(rsrc(f, xs, f == p.cur ? pbytes : prev_bytes),
+                                                         static_cast<int>(goff), 0, kLoadAux));
     };
     auto store_pair = [&](D2 v, double* f, int x, unsigned off, bool real) __attribute__((always_inline)) {
 #ifndef W3D_EXPERIMENT_NOSTORE
@@ -537,15 +504,10 @@ __global__ __launch_bounds__(kNT / PT) void k_leapfrog_p2(const P2Params p) {
     __syncthreads();  // tables
 
     // analytic start: φ and u¹ from the tables (stencil.hpp phi / init_first order: neighbours are (s_x·s_y)·s_z)
-    double fy[PT], fzl[PT], fzh[PT];
-    static_for<0, PT>([&](auto qc) __attribute__((always_inline)) {
-      constexpr int q = decltype(qc)::value;
-      fy[q] = syw[a[q] + 2];
-      fzl[q] = szw[2 * b[q] + 4];
-      fzh[q] = szw[2 * b[q] + 5];
-    });
-    auto u1_at = [&](int q, int x, int zr, bool real_yz) __attribute__((always_inline)) {
-      const int xi = x + xtab0, yb = a[q] + 2, zb = zr + 4;
+    const double fy = syw[a + 2];
+    const double fzl = szw[2 * b + 4], fzh = szw[2 * b + 5];
+    auto u1_at = [&](int x, int zr, bool real_yz) __attribute__((always_inline)) {
+      const int xi = x + xtab0, yb = a + 2, zb = zr + 4;
       const double sxc = sxw[xi], sy = syw[yb], sz = szw[zb];
       const double cy = sxc * sy;
       const double c = cy * sz;
@@ -553,31 +515,23 @@ __global__ __launch_bounds__(kNT / PT) void k_leapfrog_p2(const P2Params p) {
                                (sxc * syw[yb + 1]) * sz, cy * szw[zb - 1], cy * szw[zb + 1]);
       return (real_yz && inside(p.gx0 + x)) ? first_step(c, lap, p.half_tau2) : 0.0;
     };
-    auto u1_pair = [&](int q, int x) __attribute__((always_inline)) {
-      return D2m(u1_at(q, x, 2 * b[q], rl[q]), u1_at(q, x, 2 * b[q] + 1, rh[q]));
+    auto u1_pair = [&](int x) __attribute__((always_inline)) {
+      return D2m(u1_at(x, 2 * b, rl), u1_at(x, 2 * b + 1, rh));
     };
-    auto phi_pair = [&](int q, int x) __attribute__((always_inline)) {
+    auto phi_pair = [&](int x) __attribute__((always_inline)) {
       const double sx = sxw[x + xtab0];
-      return D2m((sx * fy[q]) * fzl[q], (sx * fy[q]) * fzh[q]);
+      return D2m((sx * fy) * fzl, (sx * fy) * fzh);
     };
     (void)phi_pair;
     (void)u1_pair;
 
     // ---- register queues
-    D2 L[PT][S][4];
-    static_for<0, 4 * S * PT>([&](auto ic) __attribute__((always_inline)) {
-      constexpr int I = decltype(ic)::value;
-      L[I / (4 * S)][(I / 4) % S][I % 4] = D2m(0.0, 0.0);
+    D2 L[S][4];
+    static_for<0, 4 * S>([&](auto ic) __attribute__((always_inline)) {
+      L[decltype(ic)::value / 4][decltype(ic)::value % 4] = D2m(0.0, 0.0);
     });
-    D2 Lm[PT][2];
-    D2 phq[PT][2];  // (analytic start: the pair's own φ by plane parity)
-    D2 nc[PT], np[PT];  // (kDeep: u^n, u^{n−1} one plane ahead of the queues)
-    (void)nc;
-    (void)np;
-    static_for<0, PT>([&](auto qc) __attribute__((always_inline)) {
-      constexpr int q = decltype(qc)::value;
-      Lm[q][0] = Lm[q][1] = phq[q][0] = phq[q][1] = D2m(0.0, 0.0);
-    });
+    D2 Lm[2] = {D2m(0.0, 0.0), D2m(0.0, 0.0)};
+    D2 phq[2] = {D2m(0.0, 0.0), D2m(0.0, 0.0)};  // (analytic start: the pair's own φ by plane parity)
     (void)phq;
 
     const int i0 = wx0 - S + 1, i1 = wx1 + S - 2;
@@ -602,24 +556,23 @@ __global__ __launch_bounds__(kNT / PT) void k_leapfrog_p2(const P2Params p) {
       return *reinterpret_cast<const ldouble*>(base + off);
     };
 
-    // stage k of position q at plane xp; D = (xp − i0) & 3 (static)
-    auto stage = [&](auto kc, auto dc, auto bkc, auto qc, int xp) __attribute__((always_inline)) {
-      constexpr int k = decltype(kc)::value, D = decltype(dc)::value, q = decltype(qc)::value;
+    // stage k at plane xp; D = (xp − i0) & 3 (static)
+    auto stage = [&](auto kc, auto dc, auto bkc, int xp) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value, D = decltype(dc)::value;
       constexpr bool BK = decltype(bkc)::value;
       constexpr int sm = (D + 3) & 3, s0 = D, sp = (D + 1) & 3;
       const bool inr = BK || (xp >= wx0 - (S - k) && xp < wx1 + (S - k));
       const bool xown = BK || (xp >= wx0 && xp < wx1);
-      auto kb = [&](int pl) __attribute__((always_inline)) { return pl < 4 ? bA[q] : bB[q]; };
       D2 v = D2m(0.0, 0.0);
-      if (inr && wst[q] >= k) {  // (wave-uniform)
-        const D2 c = L[q][k - 1][s0], xm = L[q][k - 1][sm], xq = L[q][k - 1][sp];
+      if (inr && wst >= k) {  // (wave-uniform)
+        const D2 c = L[k - 1][s0], xm = L[k - 1][sm], xq = L[k - 1][sp];
         D2 ym, yp;
         double zm, zq;
         if constexpr (k == 1) {
-          ym = rd2(b0[q], o0(D & 1, -1, 0));
-          yp = rd2(b0[q], o0(D & 1, 1, 0));
-          zm = rd1(b0[q], o0(D & 1, 0, -1) + 8);
-          zq = rd1(b0[q], o0(D & 1, 0, 1));
+          ym = rd2(b0, o0(D & 1, -1, 0));
+          yp = rd2(b0, o0(D & 1, 1, 0));
+          zm = rd1(b0, o0(D & 1, 0, -1) + 8);
+          zq = rd1(b0, o0(D & 1, 0, 1));
         } else {
           constexpr int pl = (k - 2) * 2 + (D & 1);
           const lchar* bk = kb(pl);
@@ -630,8 +583,8 @@ __global__ __launch_bounds__(kNT / PT) void k_leapfrog_p2(const P2Params p) {
         }
         const double lapl = d2sum(c.x, xm.x, xq.x, ym.x, yp.x, zm, c.y);
         const double laph = d2sum(c.y, xm.y, xq.y, ym.y, yp.y, c.x, zq);
-        const D2 o = k == 1 ? Lm[q][kLate ? 0 : (D & 1)] : L[q][k > 1 ? k - 2 : 0][s0];
-        v = D2m(leapfrog(c.x, o.x, lapl, lam_lo[q]), leapfrog(c.y, o.y, laph, lam_hi[q]));
+        const D2 o = k == 1 ? Lm[kLate ? 0 : (D & 1)] : L[k > 1 ? k - 2 : 0][s0];
+        v = D2m(leapfrog(c.x, o.x, lapl, lam_lo), leapfrog(c.y, o.y, laph, lam_hi));
         if constexpr (!BK) {
           if (!xreal(xp)) v = D2m(0.0, 0.0);
         }
@@ -643,17 +596,17 @@ __global__ __launch_bounds__(kNT / PT) void k_leapfrog_p2(const P2Params p) {
 #ifdef W3D_EXPERIMENT_NOCHECK
             false;
 #else
-            q == 0 && ((CM >> (k - 1)) & 1) != 0;
+            ((CM >> (k - 1)) & 1) != 0;
 #endif
         if constexpr (kChk) {
           if (((wchk >> (k - 1)) & 1) && xown) {  // (wchk: 0 outside the own waves)
             // u_a = ((s_x·s_y)·ct)·s_z (stencil.hpp analytic_row); s_x of the plane: one LDS broadcast read
             const double sxp = sxw[xp + xtab0];
-            // (the analytic start, the 5-step passes and the two-pair passes hold the pair's s_y, s_z, s_z+1 in
-            // registers; the other passes have no registers to spare and read them from LDS)
-            constexpr bool kRegF = INIT || S == 5 || PT == 2;
-            const double rf = (sxp * (kRegF ? fy[0] : rdd(rt, 0))) * p.ct[k - 1];
-            const D2 sz = kRegF ? D2m(fzl[0], fzh[0]) : rd2(szp, 0);
+            // (the analytic start and the 5-step passes hold the pair's s_y, s_z, s_z+1 in registers; the other
+            // passes have no registers to spare and read them from LDS)
+            constexpr bool kRegF = INIT || S == 5;
+            const double rf = (sxp * (kRegF ? fy : rdd(rt, 0))) * p.ct[k - 1];
+            const D2 sz = kRegF ? D2m(fzl, fzh) : rd2(szp, 0);
             // (d·d = |d|·|d|; the masks okl / okh are applied in the reduction — per plane they were 4 v_cndmask_b32
             // and a canonicalising v_max_f64 per pair and level, a quarter of the check's VALU)
             const double d0 = v.x - rf * sz.x, d1 = v.y - rf * sz.y;
@@ -674,60 +627,60 @@ __global__ __launch_bounds__(kNT / PT) void k_leapfrog_p2(const P2Params p) {
       }
       // (also when the stage is skipped: the slot's previous plane is dead either way, and an unconditional write
       // keeps it from staying live through the general iterations)
-      if constexpr (k < S) L[q][k][s0] = v;
-      if constexpr (q == 0 && kSplitSt && k == S) {
+      if constexpr (k < S) L[k][s0] = v;
+      if constexpr (kSplitSt && k == S) {
         if (winner) {
-          store_pair(v, p.out2, xp, soff[0], xown);
+          store_pair(v, p.out2, xp, soff, xown);
         } else {
           constexpr int pl = (S - 2) * 2 + (D & 1);  // level S−1, plane xp: written by stage S−1 last iteration
           store_pair(rd2(rt, ok_(pl, 0, 0)), p.out1, xp, soff2, xown);
         }
-      } else if constexpr (q == 0 && !kSplitSt && k >= S - 1) {
+      } else if constexpr (!kSplitSt && k >= S - 1) {
         // the thread's store offset plus a scalar offset (0 for the own waves' planes, out of range otherwise).
         // Passes that load: every wave stores (non-owners beyond the plane: dropped), so every wave's vector-memory
         // sequence is the same and the compiler's waits for the loads can leave the stores in flight. The analytic
-        // start loads nothing: only the own waves store (−2 %). (Two pairs per thread: every wave owns tile pairs.)
-        if (!INIT || winner) store_pair(v, k == S ? p.out2 : p.out1, xp, soff[0], xown && winner);
+        // start loads nothing: only the own waves store (−2 %)
+        if (!INIT || winner) store_pair(v, k == S ? p.out2 : p.out1, xp, soff, xown && winner);
       }
     };
 
-    // analytic start, iteration i: u¹ of plane i+2 (into L[q][0]) and u⁰ = φ of plane i+1 (into Lm) for the region
+    // analytic start, iteration i: u¹ of plane i+2 (into L[0]) and u⁰ = φ of plane i+1 (into Lm) for the region
     // pairs. φ(i+3) is computed once per node (2 products) and kept in a register queue with φ(i+1), φ(i+2) (S = 4; the
     // S ≤ 3 starts have no registers to spare and form them again); φ(i+2)'s y/z neighbours are the products the
     // neighbouring pairs form, (s_x·s_y(a±1))·s_z and (s_x·s_y)·s_z(z−1 / z+2): four table reads and seven products
     // instead of a φ plane in LDS (measured: −1 % for the pass, profiles/r6/). Ring pairs compute u¹ from the tables.
     // Bit-identical to k_init_first: every neighbour value is the same product.
-    auto init_iter = [&](auto fc, auto qc, int i) __attribute__((always_inline)) {
-      constexpr int F = decltype(fc)::value, q = decltype(qc)::value;
+    auto init_iter = [&](auto fc, int i) __attribute__((always_inline)) {
+      constexpr int F = decltype(fc)::value;
       const double sx3 = sxw[i + 3 + xtab0];
-      const D2 f3 = D2m((sx3 * fy[q]) * fzl[q], (sx3 * fy[q]) * fzh[q]);
+      const D2 f3 = D2m((sx3 * fy) * fzl, (sx3 * fy) * fzh);
       D2 u = D2m(0.0, 0.0);
-      if (reg[q]) {
+      if (reg) {
         D2 f1, c;
         if constexpr (S == 4) {
-          f1 = phq[q][(F + 1) & 1];  // (φ(i+1) and φ(i+3) share the parity slot: read, then replaced)
-          c = phq[q][F & 1];
-          phq[q][(F + 1) & 1] = f3;
+          f1 = phq[(F + 1) & 1];  // (φ(i+1) and φ(i+3) share the parity slot: read, then replaced)
+          c = phq[F & 1];
+          phq[(F + 1) & 1] = f3;
         } else {
-          f1 = phi_pair(q, i + 1);
-          c = phi_pair(q, i + 2);
+          f1 = phi_pair(i + 1);
+          c = phi_pair(i + 2);
         }
         const double sx2 = sxw[i + 2 + xtab0];
-        const double ry_m = sx2 * syw[a[q] + 1], ry_p = sx2 * syw[a[q] + 3], cy2 = sx2 * fy[q];
-        const D2 ym = D2m(ry_m * fzl[q], ry_m * fzh[q]), yp = D2m(ry_p * fzl[q], ry_p * fzh[q]);
-        const double zm = cy2 * szw[2 * b[q] + 3], zq = cy2 * szw[2 * b[q] + 6];
+        const double ry_m = sx2 * syw[a + 1], ry_p = sx2 * syw[a + 3], cy2 = sx2 * fy;
+        const D2 ym = D2m(ry_m * fzl, ry_m * fzh), yp = D2m(ry_p * fzl, ry_p * fzh);
+        const double zm = cy2 * szw[2 * b + 3], zq = cy2 * szw[2 * b + 6];
         const double lapl = d2sum(c.x, f1.x, f3.x, ym.x, yp.x, zm, c.y);
         const double laph = d2sum(c.y, f1.y, f3.y, ym.y, yp.y, c.x, zq);
         u = D2m(first_step(c.x, lapl, p.half_tau2), first_step(c.y, laph, p.half_tau2));
-        u.x = rl[q] ? u.x : 0.0;
-        u.y = rh[q] ? u.y : 0.0;
+        u.x = rl ? u.x : 0.0;
+        u.y = rh ? u.y : 0.0;
         if (!inside(p.gx0 + i + 2)) u = D2m(0.0, 0.0);
         // (u⁰ = φ is not 0 on every Dirichlet node — s(N) = sin(π) — so it is zeroed here)
-        Lm[q][(F + 1) & 1] = D2m(rl[q] ? f1.x : 0.0, rh[q] ? f1.y : 0.0);
-      } else if (act[q]) {
-        u = u1_pair(q, i + 2);
+        Lm[(F + 1) & 1] = D2m(rl ? f1.x : 0.0, rh ? f1.y : 0.0);
+      } else if (act) {
+        u = u1_pair(i + 2);
       }
-      L[q][0][(F + 2) & 3] = u;  // (one store to the queue slot: SROA keeps the queue in registers)
+      L[0][(F + 2) & 3] = u;  // (one store to the queue slot: SROA keeps the queue in registers)
     };
 
     // iteration i with phase F
@@ -737,51 +690,29 @@ __global__ __launch_bounds__(kNT / PT) void k_leapfrog_p2(const P2Params p) {
       p2_barrier();  // every read of the slots overwritten below (iteration i−1) is done; i−1's writes visible
 #endif
       opaque_bases();
-      static_for<0, PT>([&](auto qc) __attribute__((always_inline)) {
-        constexpr int q = decltype(qc)::value;
-        if (act[q]) wr2(b0[q], o0((F + 1) & 1, 0, 0), L[q][0][(F + 1) & 3]);  // u^n plane i+1 → LDS
-      });
-      static_for<0, PT>([&](auto qc) __attribute__((always_inline)) {
-        constexpr int q = decltype(qc)::value;
-        if constexpr (INIT) {
-          init_iter(fc, qc, i);
-        } else if constexpr (!kLate) {
-          L[q][0][(F + 2) & 3] = load_pair(bkc, p.cur, i + 2, goff[q], pbytes);
-          Lm[q][(F + 1) & 1] = load_pair(bkc, p.prev, i + 1, goff[q], prev_bytes[q]);
-        } else if constexpr (kDeep) {
-          L[q][0][(F + 2) & 3] = nc[q];  // (plane i+2, loaded one iteration ago)
-          // (clamped to the allocation even in bulk iterations: the bulk range guarantees plane i+2, not i+3)
-          nc[q] = load_pair(std::false_type{}, p.cur, i + 3, goff[q], pbytes);
-        } else {
-          // u^n plane i+2 right after the commit: its slot (plane i−2's) has been dead since stage 2 of iteration
-          // i−1, and issued here it has the whole iteration (≈ 2 µs) to arrive — after stage 2, as first built, the
-          // next commit waited for it: −13 % per 5-step pass (profiles/r5/stores/abn_cur_early.log)
-          L[q][0][(F + 2) & 3] = load_pair(bkc, p.cur, i + 2, goff[q], pbytes);
-        }
-      });
+      if (act) wr2(b0, o0((F + 1) & 1, 0, 0), L[0][(F + 1) & 3]);  // u^n plane i+1 → LDS
+      if constexpr (INIT) {
+        init_iter(fc, i);
+      } else if constexpr (!kLate) {
+        L[0][(F + 2) & 3] = load_pair(bkc, p.cur, i + 2);
+        Lm[(F + 1) & 1] = load_pair(bkc, p.prev, i + 1);
+      } else {
+        // u^n plane i+2 right after the commit: its slot (plane i−2's) has been dead since stage 2 of iteration i−1,
+        // and issued here it has the whole iteration (≈ 2 µs) to arrive — after stage 2, as first built, the next
+        // commit waited for it: −13 % per 5-step pass (profiles/r5/stores/abn_cur_early.log)
+        L[0][(F + 2) & 3] = load_pair(bkc, p.cur, i + 2);
+      }
       // (scheduling fences between the load passes' stages: the compiler would otherwise hoist later stages' LDS
       // reads into earlier ones and run out of the 128 VGPRs; the analytic start has the registers to overlap one
       // stage's reads with the last one's arithmetic, −2.3 %, profiles/r5/memops)
 #define W3D_P2_STAGE(K)                                                                                       \
   if constexpr (K <= S) {                                                                                     \
-    static_for<0, PT>([&](auto qc) __attribute__((always_inline)) {                                           \
-      stage(std::integral_constant<int, K>{}, std::integral_constant<int, (F - (K - 1) + 8) & 3>{}, bkc, qc,  \
-            i - (K - 1));                                                                                     \
-    });                                                                                                       \
+    stage(std::integral_constant<int, K>{}, std::integral_constant<int, (F - (K - 1) + 8) & 3>{}, bkc,        \
+          i - (K - 1));                                                                                       \
     if constexpr (!INIT) __builtin_amdgcn_sched_barrier(0);                                                   \
   }
       W3D_P2_STAGE(1)
-      if constexpr (kLate) {
-        static_for<0, PT>([&](auto qc) __attribute__((always_inline)) {
-          constexpr int q = decltype(qc)::value;
-          if constexpr (kDeep) {
-            Lm[q][0] = np[q];  // (plane i+1, loaded one iteration ago)
-            np[q] = load_pair(std::false_type{}, p.prev, i + 2, goff[q], prev_bytes[q]);
-          } else {
-            Lm[q][0] = load_pair(bkc, p.prev, i + 1, goff[q], prev_bytes[q]);  // (its register freed by stage 1)
-          }
-        });
-      }
+      if constexpr (kLate) Lm[0] = load_pair(bkc, p.prev, i + 1);  // (its register freed by stage 1)
       W3D_P2_STAGE(2)
       W3D_P2_STAGE(3)
       W3D_P2_STAGE(4)
@@ -792,36 +723,29 @@ __global__ __launch_bounds__(kNT / PT) void k_leapfrog_p2(const P2Params p) {
     // prologue: u^n planes i0−1, i0 (registers; plane i0 also to LDS), plane i0+1 and u^{n−1} plane i0 in flight
     using Gen = std::false_type;
     using Bulk = std::true_type;
-    static_for<0, PT>([&](auto qc) __attribute__((always_inline)) {
-      constexpr int q = decltype(qc)::value;
-      if constexpr (INIT) {
-        if (act[q]) {
-          L[q][0][3] = u1_pair(q, i0 - 1);
-          L[q][0][0] = u1_pair(q, i0);
-          L[q][0][1] = u1_pair(q, i0 + 1);
-          if constexpr (S == 4) {
-            phq[q][1] = phi_pair(q, i0 + 1);  // (plane i0+1: odd parity; i0+2: even)
-            phq[q][0] = phi_pair(q, i0 + 2);
-          }
-        }
-        if (reg[q]) {
-          const D2 f0 = phi_pair(q, i0);
-          Lm[q][0] = D2m(rl[q] ? f0.x : 0.0, rh[q] ? f0.y : 0.0);  // (see init_iter)
-        }
-      } else {
-        L[q][0][3] = load_pair(Gen{}, p.cur, i0 - 1, goff[q], pbytes);
-        L[q][0][0] = load_pair(Gen{}, p.cur, i0, goff[q], pbytes);
-      }
-      if (act[q]) wr2(b0[q], o0(0, 0, 0), L[q][0][0]);
-      if constexpr (!INIT) {
-        L[q][0][1] = load_pair(Gen{}, p.cur, i0 + 1, goff[q], pbytes);
-        Lm[q][0] = load_pair(Gen{}, p.prev, i0, goff[q], prev_bytes[q]);
-        if constexpr (kDeep) {
-          nc[q] = load_pair(Gen{}, p.cur, i0 + 2, goff[q], pbytes);
-          np[q] = load_pair(Gen{}, p.prev, i0 + 1, goff[q], prev_bytes[q]);
+    if constexpr (INIT) {
+      if (act) {
+        L[0][3] = u1_pair(i0 - 1);
+        L[0][0] = u1_pair(i0);
+        L[0][1] = u1_pair(i0 + 1);
+        if constexpr (S == 4) {
+          phq[1] = phi_pair(i0 + 1);  // (plane i0+1: odd parity; i0+2: even)
+          phq[0] = phi_pair(i0 + 2);
         }
       }
-    });
+      if (reg) {
+        const D2 f0 = phi_pair(i0);
+        Lm[0] = D2m(rl ? f0.x : 0.0, rh ? f0.y : 0.0);  // (see init_iter)
+      }
+    } else {
+      L[0][3] = load_pair(Gen{}, p.cur, i0 - 1);
+      L[0][0] = load_pair(Gen{}, p.cur, i0);
+    }
+    if (act) wr2(b0, o0(0, 0, 0), L[0][0]);
+    if constexpr (!INIT) {
+      L[0][1] = load_pair(Gen{}, p.cur, i0 + 1);
+      Lm[0] = load_pair(Gen{}, p.prev, i0);
+    }
     // head blocks (general) until the first block inside the bulk range, bulk blocks, then the general tail
     const int blo = max(max(wx0, p.sx0), 1 - p.gx0) + (S - 1);
     const int bhi = min(min(wx1, p.sx1), N - p.gx0);
@@ -857,8 +781,7 @@ __global__ __launch_bounds__(kNT / PT) void k_leapfrog_p2(const P2Params p) {
   return;
 #endif
   if (p.partials == nullptr) return;
-  constexpr int NW = NT / 64;
-  __shared__ double red_m[NW], red_s[NW];
+  __shared__ double red_m[kNT / 64], red_s[kNT / 64];
   static_for<0, S>([&](auto kc) __attribute__((always_inline)) {
     constexpr int k = decltype(kc)::value;
     if constexpr ((CM >> k) & 1) {
@@ -884,7 +807,7 @@ __global__ __launch_bounds__(kNT / PT) void k_leapfrog_p2(const P2Params p) {
         __syncthreads();
         if (tid == 0) {
           double mm = red_m[0], ss = red_s[0];
-          for (int w = 1; w < NW; ++w) {
+          for (int w = 1; w < kNT / 64; ++w) {
             mm = red_m[w] > mm ? red_m[w] : mm;
             ss += red_s[w];
           }

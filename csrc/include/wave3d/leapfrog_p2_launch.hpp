@@ -16,10 +16,10 @@ template <int S>
 constexpr int kOdd = 0b10101 & kFull<S>;
 
 // the kernel's static LDS (the reduction arrays) as laid out, and the dynamic limit it leaves
-template <int S, int CM, bool INIT, bool CH, int PT>
+template <int S, int CM, bool INIT, bool CH>
 size_t prepare_cfg() {
   static const size_t limit = [] {
-    const void* fn = reinterpret_cast<const void*>(k_leapfrog_p2<S, CM, INIT, CH, PT>);
+    const void* fn = reinterpret_cast<const void*>(k_leapfrog_p2<S, CM, INIT, CH>);
     hipFuncAttributes fa{};
     hipError_t e = hipFuncGetAttributes(&fa, fn);
     if (e != hipSuccess) fail(std::string("leapfrog_p2 attributes: ") + hipGetErrorString(e));
@@ -31,50 +31,50 @@ size_t prepare_cfg() {
   return limit;
 }
 
-template <int S, int CM, bool INIT, int PT>
+template <int S, int CM, bool INIT>
 void launch_cfg(const P2Params& p, int nblocks, hipStream_t st) {
   const size_t shmem = p2_lds_bytes<S>((p.check_mask || INIT) ? p2_nxt<S>(p.xlen) : 0);
   if (p.nxc > 1) {
-    const size_t lim = prepare_cfg<S, CM, INIT, true, PT>();
+    const size_t lim = prepare_cfg<S, CM, INIT, true>();
     W3D_REQUIRE(shmem <= lim, "leapfrog_p2: too many planes for the LDS sin table");
-    hipLaunchKernelGGL((k_leapfrog_p2<S, CM, INIT, true, PT>), dim3(nblocks), dim3(kNT / PT), shmem, st, p);
+    hipLaunchKernelGGL((k_leapfrog_p2<S, CM, INIT, true>), dim3(nblocks), dim3(kNT), shmem, st, p);
   } else {
-    const size_t lim = prepare_cfg<S, CM, INIT, false, PT>();
+    const size_t lim = prepare_cfg<S, CM, INIT, false>();
     W3D_REQUIRE(shmem <= lim, "leapfrog_p2: too many planes for the LDS sin table");
-    hipLaunchKernelGGL((k_leapfrog_p2<S, CM, INIT, false, PT>), dim3(nblocks), dim3(kNT / PT), shmem, st, p);
+    hipLaunchKernelGGL((k_leapfrog_p2<S, CM, INIT, false>), dim3(nblocks), dim3(kNT), shmem, st, p);
   }
 }
 
-template <int S, bool INIT, int PT = 1>
+template <int S, bool INIT>
 void launch_cm(const P2Params& p, int nblocks, hipStream_t st) {
   const int m = p.check_mask;
   if (m == 0)
-    launch_cfg<S, 0, INIT, PT>(p, nblocks, st);
+    launch_cfg<S, 0, INIT>(p, nblocks, st);
   else if ((m & ~kEven<S>) == 0)
-    launch_cfg<S, kEven<S>, INIT, PT>(p, nblocks, st);
+    launch_cfg<S, kEven<S>, INIT>(p, nblocks, st);
   else if ((m & ~kOdd<S>) == 0)
-    launch_cfg<S, kOdd<S>, INIT, PT>(p, nblocks, st);
+    launch_cfg<S, kOdd<S>, INIT>(p, nblocks, st);
   else
-    launch_cfg<S, kFull<S>, INIT, PT>(p, nblocks, st);
+    launch_cfg<S, kFull<S>, INIT>(p, nblocks, st);
 }
 
-template <int S, bool INIT, int PT = 1>
+template <int S, bool INIT>
 void prepare_all() {
-  prepare_cfg<S, 0, INIT, false, PT>();
-  prepare_cfg<S, kEven<S>, INIT, false, PT>();
-  prepare_cfg<S, kOdd<S>, INIT, false, PT>();
-  prepare_cfg<S, kFull<S>, INIT, false, PT>();
-  prepare_cfg<S, 0, INIT, true, PT>();
-  prepare_cfg<S, kEven<S>, INIT, true, PT>();
-  prepare_cfg<S, kOdd<S>, INIT, true, PT>();
-  prepare_cfg<S, kFull<S>, INIT, true, PT>();
+  prepare_cfg<S, 0, INIT, false>();
+  prepare_cfg<S, kEven<S>, INIT, false>();
+  prepare_cfg<S, kOdd<S>, INIT, false>();
+  prepare_cfg<S, kFull<S>, INIT, false>();
+  prepare_cfg<S, 0, INIT, true>();
+  prepare_cfg<S, kEven<S>, INIT, true>();
+  prepare_cfg<S, kOdd<S>, INIT, true>();
+  prepare_cfg<S, kFull<S>, INIT, true>();
 }
 
-// per-S entry points (one translation unit each; pairs: pairs per thread, 2 only for S = 4, 5)
+// per-S entry points (one translation unit each)
 void launch_p2_s2(const P2Params& p, int nblocks, bool init, hipStream_t st);
 void launch_p2_s3(const P2Params& p, int nblocks, bool init, hipStream_t st);
-void launch_p2_s4(const P2Params& p, int nblocks, bool init, int pairs, hipStream_t st);
-void launch_p2_s5(const P2Params& p, int nblocks, int pairs, hipStream_t st);
+void launch_p2_s4(const P2Params& p, int nblocks, bool init, hipStream_t st);
+void launch_p2_s5(const P2Params& p, int nblocks, bool init, hipStream_t st);
 void prepare_p2_s2();
 void prepare_p2_s3();
 void prepare_p2_s4();

@@ -415,8 +415,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("xcd_blocks", &LeapfrogTbTiling::xcd_blocks)
       .def_readwrite("target_blocks", &LeapfrogTbTiling::target_blocks)
       .def_readwrite("min_chunk", &LeapfrogTbTiling::min_chunk)
-      .def_readwrite("p2", &LeapfrogTbTiling::p2)
-      .def_readwrite("p2_pairs", &LeapfrogTbTiling::p2_pairs);
+      .def_readwrite("p2", &LeapfrogTbTiling::p2);
   m.def("capture_guard_selftest", &wave3d::capture::selftest, py::arg("mode"),
         "the probe topologies through the stream-capture guard (0: production, 2: the round-4 sibling wait)");
   m.def("leapfrog_p2_table", [](int stages) {

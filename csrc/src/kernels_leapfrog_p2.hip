@@ -212,11 +212,8 @@ void launch_leapfrog_p2(const Layout& l, const Coeffs& c, const double* prev, co
   switch (t.stages) {
     case 2: launch_p2_s2(p, pl.nblocks, analytic_start, stream); break;
     case 3: launch_p2_s3(p, pl.nblocks, analytic_start, stream); break;
-    case 4: launch_p2_s4(p, pl.nblocks, analytic_start, t.p2_pairs, stream); break;
-    default:
-      W3D_REQUIRE(!analytic_start, "leapfrog_p2: the analytic-start pass takes at most 4 steps");
-      launch_p2_s5(p, pl.nblocks, t.p2_pairs, stream);
-      break;
+    case 4: launch_p2_s4(p, pl.nblocks, analytic_start, stream); break;
+    default: launch_p2_s5(p, pl.nblocks, analytic_start, stream); break;
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) fail(std::string("leapfrog_p2 launch: ") + hipGetErrorString(e));

@@ -150,7 +150,6 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   // (perf studies: tiling overrides of the LDS S-step kernel; W3D_TB_TARGET=B splits the x march into chunks when the
   // tile grid has fewer than B tiles, W3D_TB_MINCHUNK its minimum planes, W3D_TB_XCDBLOCKS=1 square XCD blocks)
   if (const char* v = std::getenv("W3D_TB_TARGET")) opt_.tiling_tb.target_blocks = std::atoi(v);
-  if (const char* v = std::getenv("W3D_P2_PAIRS")) opt_.tiling_tb.p2_pairs = std::atoi(v) == 2 ? 2 : 1;
   if (const char* v = std::getenv("W3D_RESERVE_CUS")) opt_.reserve_cus = std::atoi(v);
   if (const char* v = std::getenv("W3D_TB_MINCHUNK")) opt_.tiling_tb.min_chunk = std::atoi(v);
   if (const char* v = std::getenv("W3D_TB_XCDBLOCKS")) opt_.tiling_tb.xcd_blocks = *v == '1';

@@ -112,7 +112,7 @@ def leapfrog2(layout, coeffs, prev: torch.Tensor, cur: torch.Tensor, out1: torch
 
 def leapfrog_tb(layout, coeffs, prev: torch.Tensor, cur: torch.Tensor, out1: torch.Tensor, out2: torch.Tensor, box,
                 s_ext: torch.Tensor, stages: int = 4, ct=None, check_mask: int = 0, threads: int = 1024,
-                analytic_start: bool = False, p2: bool = True, target_blocks: int | None = None, pairs: int = 1):
+                analytic_start: bool = False, p2: bool = True, target_blocks: int | None = None):
     """``stages`` fused leapfrog steps held in LDS (HIP only): out1 = u^{n+S-1}, out2 = u^{n+S}.
 
     ``p2`` selects the pair-tiled kernel (S <= 5) wherever it applies, else k_leapfrog_tb (S <= 4).
@@ -129,7 +129,6 @@ def leapfrog_tb(layout, coeffs, prev: torch.Tensor, cur: torch.Tensor, out1: tor
     t.p2 = p2  # the pair-tiled kernel (k_leapfrog_p2) where it applies; False: k_leapfrog_tb
     if target_blocks is not None:
         t.target_blocks = target_blocks
-    t.p2_pairs = pairs  # pair-tiled pass: pairs per thread (2: 512-thread workgroups, S = 4, 5)
     nb = C.gpu_leapfrog_tb_partials(layout, box, t)
     ct = list(ct) if ct is not None else [0.0] * stages
     part = torch.empty((stages * max(nb, 1), 2), dtype=torch.float64, device=out1.device) if check_mask else None

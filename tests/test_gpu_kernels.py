@@ -236,14 +236,11 @@ P2_MASKS = {"all": lambda S: (1 << S) - 1, "odd": lambda S: 0b10101 & ((1 << S) 
             "even": lambda S: 0b01010 & ((1 << S) - 1), "none": lambda S: 0}
 
 
-P2_PAIRS = [(S, 1) for S in (2, 3, 4, 5)] + [(4, 2), (5, 2)]  # (stages, pairs per thread)
-
-
-@pytest.mark.parametrize("stages,pairs", P2_PAIRS)
+@pytest.mark.parametrize("stages", [2, 3, 4, 5])
 @pytest.mark.parametrize("N", [40, 77, 130])
 @pytest.mark.parametrize("chunked", [False, True])
 @pytest.mark.parametrize("mask", ["all", "odd", "even"])
-def test_leapfrog_p2_equals_single_steps(gpu, stages, pairs, N, chunked, mask):
+def test_leapfrog_p2_equals_single_steps(gpu, stages, N, chunked, mask):
     """Pair-tiled pass (k_leapfrog_p2): one pass of S steps == S CPU steps, bit for bit, fields and checked levels.
     chunked: x split into chunks (the CH instantiations); N = 130 has interior tiles (no Dirichlet select needed)."""
     C = gpu
@@ -262,7 +259,7 @@ def test_leapfrog_p2_equals_single_steps(gpu, stages, pairs, N, chunked, mask):
     o2 = torch.zeros_like(o1)
     m = P2_MASKS[mask](stages)
     e_gpu = ops.leapfrog_tb(lay, co, prev.cuda(), cur.cuda(), o1, o2, box, s.cuda(), stages, ct, m,
-                            p2=True, target_blocks=256 if chunked else 1, pairs=pairs)
+                            p2=True, target_blocks=256 if chunked else 1)
     torch.cuda.synchronize()
     assert torch.equal(ops.to_grid(lay, o1.cpu()), ops.to_grid(lay, a))
     assert torch.equal(ops.to_grid(lay, o2.cpu()), ops.to_grid(lay, b))
@@ -277,10 +274,10 @@ def test_leapfrog_p2_equals_single_steps(gpu, stages, pairs, N, chunked, mask):
     torch.testing.assert_close(ops.to_grid(lay, o2.cpu()), pb, rtol=0, atol=1e-9)
 
 
-@pytest.mark.parametrize("stages,pairs", [(2, 1), (3, 1), (4, 1), (4, 2)])
+@pytest.mark.parametrize("stages", [2, 3, 4])
 @pytest.mark.parametrize("N", [40, 77, 130])
 @pytest.mark.parametrize("chunked", [False, True])
-def test_leapfrog_p2_analytic_start(gpu, stages, pairs, N, chunked):
+def test_leapfrog_p2_analytic_start(gpu, stages, N, chunked):
     """Pair-tiled analytic-start pass == init_first + S CPU steps on the interior, bit for bit."""
     C = gpu
     prob, co, lay, _ = _setup(C, N)
@@ -297,7 +294,7 @@ def test_leapfrog_p2_analytic_start(gpu, stages, pairs, N, chunked):
     o1 = torch.zeros(int(lay.total), dtype=torch.float64, device="cuda")
     o2 = torch.zeros_like(o1)
     e_gpu = ops.leapfrog_tb(lay, co, None, None, o1, o2, box, s.cuda(), stages, ct, (1 << stages) - 1,
-                            analytic_start=True, p2=True, target_blocks=256 if chunked else 1, pairs=pairs)
+                            analytic_start=True, p2=True, target_blocks=256 if chunked else 1)
     torch.cuda.synchronize()
     inner = (slice(1, -1),) * 3
     assert torch.equal(ops.to_grid(lay, o1.cpu())[inner], ops.to_grid(lay, a)[inner])

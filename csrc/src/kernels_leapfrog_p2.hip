@@ -61,8 +61,9 @@ int p2_grid(const LBox& b, const LeapfrogTbTiling& t, int S, int* nty, int* ntz,
   const i64 nxb = b.x1 - b.x0;
   i64 want = 1;
   // x chunks when the tile grid alone leaves CUs idle (at least min_chunk planes each), or when the x sin table of
-  // the whole range would not fit the LDS
-  if (t.target_blocks > tiles) want = imin(ceil_div(t.target_blocks, tiles), imax(1, nxb / imax(1, t.min_chunk)));
+  // the whole range would not fit the LDS. (At most target_blocks workgroups: one CU each. Rounding the chunk count up
+  // instead put e.g. a 7 × 7-tile interior box on 294 workgroups — 256 and then a second round of 38.)
+  if (t.target_blocks > tiles) want = imin(imax(1, t.target_blocks / tiles), imax(1, nxb / imax(1, t.min_chunk)));
   const int maxlen = p2_max_xlen(S);
   W3D_REQUIRE(maxlen >= 1, "leapfrog_p2: the tile does not fit in LDS");
   want = imax(want, ceil_div(nxb, maxlen));

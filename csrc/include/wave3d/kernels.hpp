@@ -153,9 +153,11 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
                         int grid_blocks = 0, const TbPush* push = nullptr, const TbPush* push_dev = nullptr,
                         const TbPack* pack = nullptr, const TbPack* pack_dev = nullptr);
 
-// The pair-tiled S-step pass (kernels_leapfrog_p2.hip): the same contract as launch_leapfrog_tb for boxes that span
-// the rank's whole y/z interior (one rank, x slabs) and S = 2..5 (analytic start: 2..4); no push / fused pack.
-// launch_leapfrog_tb dispatches to it when tiling.p2 is set and it applies.
+// The pair-tiled S-step pass (kernels_leapfrog_p2.hip): the same contract as launch_leapfrog_tb for boxes inside the
+// rank's y/z range that start and end on whole 16-byte pairs (leapfrog_p2_supported) and S = 2..5 (analytic start:
+// 2..4); no push / fused pack. launch_leapfrog_tb dispatches to it when tiling.p2 is set and it applies.
+// launch_leapfrog_p2_boxes: up to kP2MaxBoxes boxes in ONE launch (one grid, the x-chunk target shared by work), for the
+// overlapped schedules' shell boxes; their partials share one slot of `grid_blocks` entries.
 bool leapfrog_p2_supported(const Layout& l, const LBox& box, int stages);
 int leapfrog_p2_partials(const Layout& l, const LBox& box, const LeapfrogTbTiling& t);
 // (tests) the pair-tiled pass's thread → position table for S stages (kNT descriptors: (a+2) | (b+2)<<8 | lv<<16 |
@@ -166,6 +168,11 @@ void launch_leapfrog_p2(const Layout& l, const Coeffs& c, const double* prev, co
                         double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
                         Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, const LBox& real,
                         bool analytic_start, int level_stride = 0, int grid_blocks = 0);
+constexpr int kP2MaxBoxes = 6;  // boxes per pair-tiled launch (deep_split: up to 6 shells)
+void launch_leapfrog_p2_boxes(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
+                              double* out2, const LBox* boxes, int nbox, const double* d_s, const double* ct,
+                              int check_mask, Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream,
+                              const LBox& real, bool analytic_start, int level_stride = 0, int grid_blocks = 0);
 
 // Error of a stored field vs φ·ct over `box` (step 1 / standalone check). Writes leapfrog-compatible partials and
 // returns how many.

@@ -246,6 +246,15 @@ constexpr TabBuild<S> make_tab() {
 }
 
 // ---------------------------------------------------------------------------------------------------------------
+// One output box of a launch: its (y, z) tile grid times its x chunks, from logical workgroup blk0 on. A launch takes
+// up to kP2Boxes boxes (the overlapped schedules' shell boxes in one grid: they fill the GPU together where each alone
+// left CUs idle, profiles/r6/).
+struct P2Box {
+  int x0, x1, xlen, nxc;  // output x range; chunk length and count
+  int y0, z0, y1, z1;     // output (y, z) box (local)
+  int nty, ntz, blk0;
+};
+constexpr int kP2Boxes = kP2MaxBoxes;
 struct P2Params {
   const double* prev;  // u^{n−1} (x base: local plane x at (x + 1)·plane, as TbParams)
   const double* cur;   // u^n
@@ -256,11 +265,12 @@ struct P2Params {
   i64 plane;
   int pitch, ya, za;        // in-plane element of local (y, z): (y + ya)·pitch + z + za
   int ay0, ay1;             // allocated local y rows
-  int x0, x1, xlen, nxc;    // output x range; chunk length and count
   int sx0, sx1, ax0, ax1;   // x range where stage values are real; allocated planes
   int N, gx0, gy0, gz0;
-  int y0, z0, y1, z1;       // output (y, z) box (local)
-  int nty, ntz, nblocks, xcd_remap, xper, lstride;
+  P2Box box[kP2Boxes];
+  int nbox, nactive;        // boxes; workgroups with a tile (Σ over the boxes)
+  int chunked, xlen_max;    // some box is split into x chunks; its longest chunk (the LDS x sin table)
+  int nblocks, xcd_remap, xper, lstride;
   int check_mask;
   double tau2, half_tau2;
   double ct[5];
@@ -365,8 +375,14 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     const int j = blk >> 3;
     blk = j < p.xper ? (blk & 7) * p.xper + j : (1 << 30);
   }
-  const int ntiles = p.nty * p.ntz;
-  const bool active = blk < ntiles * (CH ? p.nxc : 1);
+  const bool active = blk < p.nactive;
+  // this workgroup's box (wave-uniform: a scalar search over ≤ kP2Boxes boxes)
+  int bi = 0;
+  static_for<1, kP2Boxes>([&](auto kc) __attribute__((always_inline)) {
+    constexpr int k = decltype(kc)::value;
+    if (k < p.nbox && blk >= p.box[k].blk0) bi = k;
+  });
+  const P2Box B = p.box[bi];
   // error-check accumulators, one per node of the pair (lo, hi) and checked level; a pair's nodes that are not checked
   // (Dirichlet, or beyond the box) are masked out once, in the reduction, not at every plane
   // (registers: ≤ 3 checked levels, in the 5-step passes and the 4-step analytic start — the production passes; the
@@ -380,12 +396,14 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
   bool okl = false, okh = false;  // this thread's nodes are own + real: checked
 
   if (active) {
+    blk -= B.blk0;
+    const int ntiles = B.nty * B.ntz;
     const int chunk = CH ? blk / ntiles : 0;
     if constexpr (CH) blk -= chunk * ntiles;
-    const int tzi = blk % p.ntz, tyi = blk / p.ntz;
-    const int ty0 = p.y0 + tyi * kT, tz0 = p.z0 + tzi * kT;
-    const int wx0 = CH ? p.x0 + chunk * p.xlen : p.x0;
-    const int wx1 = CH ? min(p.x1, wx0 + p.xlen) : p.x1;
+    const int tzi = blk % B.ntz, tyi = blk / B.ntz;
+    const int ty0 = B.y0 + tyi * kT, tz0 = B.z0 + tzi * kT;
+    const int wx0 = CH ? B.x0 + chunk * B.xlen : B.x0;
+    const int wx1 = CH ? min(B.x1, wx0 + B.xlen) : B.x1;
     const int N = p.N;
     const i64 P = p.plane;
     auto inside = [&](int g) __attribute__((always_inline)) {
@@ -427,10 +445,10 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     const unsigned goff = ldv ? static_cast<unsigned>(((y + p.ya) * p.pitch + el) * 8) : kOob;
     const bool ry = inside(p.gy0 + y);
     const bool rl = ry && inside(p.gz0 + z), rh = ry && inside(p.gz0 + z + 1);
-    const bool sty = inner && y < p.y1 && z < p.z1;      // own pair stored (z + 1 ≤ z1: the box spans the z interior)
+    const bool sty = inner && y < B.y1 && z < B.z1;      // own pair stored (z + 1 ≤ z1: the box ends on a whole pair)
     const unsigned soff = sty ? goff : kOob;
     okl = sty && rl;
-    okh = sty && rh && z + 1 < p.z1;
+    okh = sty && rh && z + 1 < B.z1;
     // Dirichlet nodes through τ²: a node outside the global interior has τ² = 0 and c = old = +0 at every level (zero
     // loads, zero φ, and this very update), so fma(0, Δ, fma(2, +0, −(+0))) = +0 — the select's value, bit for bit,
     // without 4 selects per pair and stage
@@ -454,7 +472,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
       const int d2 = p2_desc<S>(tid & (kNT / 2 - 1));
       const int a2 = (d2 & 0xFF) - 2, b2 = ((d2 >> 8) & 0xFF) - 2;
       const int y2 = ty0 - (S - 1) + a2, z2 = tz0 - E + 2 * b2, el2 = z2 + p.za;
-      const bool st2 = y2 >= p.ay0 && y2 < p.ay1 && el2 >= 0 && el2 + 2 <= p.pitch && y2 < p.y1 && z2 < p.z1;
+      const bool st2 = y2 >= p.ay0 && y2 < p.ay1 && el2 >= 0 && el2 + 2 <= p.pitch && y2 < B.y1 && z2 < B.z1;
       soff2 = st2 ? static_cast<unsigned>(((y2 + p.ya) * p.pitch + el2) * 8) : kOob;
       rt = lds_base + (G::lk0() + a2 * R1 + b2 - R1 - 1) * 16 + 4 * G::P1 * 16;
     }

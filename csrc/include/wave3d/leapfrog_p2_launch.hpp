@@ -33,8 +33,8 @@ size_t prepare_cfg() {
 
 template <int S, int CM, bool INIT>
 void launch_cfg(const P2Params& p, int nblocks, hipStream_t st) {
-  const size_t shmem = p2_lds_bytes<S>((p.check_mask || INIT) ? p2_nxt<S>(p.xlen) : 0);
-  if (p.nxc > 1) {
+  const size_t shmem = p2_lds_bytes<S>((p.check_mask || INIT) ? p2_nxt<S>(p.xlen_max) : 0);
+  if (p.chunked) {
     const size_t lim = prepare_cfg<S, CM, INIT, true>();
     W3D_REQUIRE(shmem <= lim, "leapfrog_p2: too many planes for the LDS sin table");
     hipLaunchKernelGGL((k_leapfrog_p2<S, CM, INIT, true>), dim3(nblocks), dim3(kNT), shmem, st, p);

@@ -44,9 +44,9 @@ struct SolverOptions {
   LeapfrogTiling tiling;
   // Temporal blocking: up to `temporal` (2..5) steps per HBM pass wherever no halo exchange intervenes. One rank:
   // k_leapfrog_p2 passes (pair-tiled, S ≤ 5; all levels in LDS, error checks at any level), the steps split into
-  // passes by measured per-step cost; slab ranks: k_leapfrog_tb passes with `temporal`-deep x halos, S ≤ 4 (5 is
-  // taken as 4; one exchange per pass; tb = false: two-step k_leapfrog2 passes with 2-deep halos). 1 = one step
-  // per pass everywhere.
+  // passes by measured per-step cost; slab and 3-D block ranks: the same passes with `temporal`-deep ghosts, one
+  // exchange per pass (the push transport: k_leapfrog_tb, S ≤ 4; tb = false: two-step k_leapfrog2 passes with 2-deep
+  // halos). 1 = one step per pass everywhere.
   int temporal = 5;
   bool tb = true;  // one rank: LDS kernel (false: k_leapfrog2 pairs, only where the intermediate step has no check)
   Leapfrog2Tiling tiling2;
@@ -275,6 +275,8 @@ class GpuSolver {
   void unit_exchange_rccl(int i);
   void unit_interior(int i);
   void tb_pass(const Unit& u, const LBox& box, int phase, hipStream_t st = nullptr);  // one k_leapfrog_tb launch
+  // the unit's shell boxes in ONE pair-tiled launch when that applies (returns false: launch them one by one)
+  bool tb_pass_boxes(const Unit& u, const std::vector<LBox>& boxes, int phase, hipStream_t st);
   // deep-tb with overlap: unit i's shell boxes (what the neighbours receive, computed first) and the interior box
   void tb_split(int i, std::vector<LBox>& shells, LBox& interior) const;
   std::vector<LBox> tb_shells(int i) const;

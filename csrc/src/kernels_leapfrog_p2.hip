@@ -69,20 +69,16 @@ int p2_grid(const LBox& b, const LeapfrogTbTiling& t, int S, int* nty, int* ntz,
   want = imax(want, ceil_div(nxb, maxlen));
   *xlen = static_cast<int>(ceil_div(nxb, want));
   *nxc = static_cast<int>(ceil_div(nxb, *xlen));
-  const int blocks = tiles * *nxc;
-  return t.xcd_remap ? static_cast<int>(round_up(blocks, 8)) : blocks;
+  return tiles * *nxc;  // (unrounded: the launch grid rounds the sum of its boxes up to whole XCD shares)
 }
 
-P2Plan make_plan_p2(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, LBox real, bool init) {
+int p2_round(int blocks, const LeapfrogTbTiling& t) { return t.xcd_remap ? static_cast<int>(round_up(blocks, 8)) : blocks; }
+
+// the checks a box must pass, and its grid (tiles × x chunks) as box k of a launch whose boxes before it take blk0
+// workgroups
+void p2_box(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, const LBox& real, int blk0, P2Box& bx) {
   const int S = t.stages;
-  W3D_REQUIRE(S >= 2 && S <= 5, "leapfrog_p2: stages must be 2..5");
-  W3D_REQUIRE(!init || S <= 4, "leapfrog_p2: the analytic-start pass takes at most 4 steps");
   W3D_REQUIRE(leapfrog_p2_supported(l, b, S), "leapfrog_p2: the box must lie in the rank's y/z range on whole pairs");
-  const LBox full = compute_box(l);
-  if (real.x0 > real.x1) {
-    real.x0 = full.x0;
-    real.x1 = full.x1;
-  }
   // x: u^{n+k} (k < S) is read up to S−k planes beyond the box (real there, or beyond the global boundary); u^n is
   // read S planes beyond, within the allocation unless beyond the global boundary
   const bool lo_ok = real.x0 <= b.x0 - (S - 1) || l.gx0 + real.x0 <= 1;
@@ -90,13 +86,37 @@ P2Plan make_plan_p2(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, L
   W3D_REQUIRE(lo_ok && hi_ok, "leapfrog_p2: stage-1 range does not cover the box halo in x");
   W3D_REQUIRE(l.gx0 + b.x0 - S <= 0 || b.x0 - S >= -l.xg, "leapfrog_p2: halo deeper than the ghosts in x");
   W3D_REQUIRE(l.gx0 + b.x1 + S - 1 >= l.N || b.x1 + S - 1 < l.nx + l.xg, "leapfrog_p2: halo deeper than the ghosts in x");
-  W3D_REQUIRE(real.x0 >= -l.xg && real.x1 <= l.nx + l.xg, "leapfrog_p2: real range outside the allocation in x");
   // y / z (3-D block ranks): u^n is read S nodes beyond the box, within the ghosts unless beyond the global boundary
   W3D_REQUIRE(l.gy0 + b.y0 - S <= 0 || b.y0 - S >= -l.yg, "leapfrog_p2: halo deeper than the ghosts in y");
   W3D_REQUIRE(l.gy0 + b.y1 + S - 1 >= l.N || b.y1 + S - 1 < l.ny + l.yg, "leapfrog_p2: halo deeper than the ghosts in y");
   W3D_REQUIRE(l.gz0 + b.z0 - S <= 0 || b.z0 - S >= -l.zg, "leapfrog_p2: halo deeper than the ghosts in z");
   W3D_REQUIRE(l.gz0 + b.z1 + S - 1 >= l.N || b.z1 + S - 1 < l.nz + l.zg, "leapfrog_p2: halo deeper than the ghosts in z");
+  bx.x0 = static_cast<int>(b.x0);
+  bx.x1 = static_cast<int>(b.x1);
+  bx.y0 = static_cast<int>(b.y0);
+  bx.z0 = static_cast<int>(b.z0);
+  bx.y1 = static_cast<int>(b.y1);
+  bx.z1 = static_cast<int>(b.z1);
+  bx.blk0 = blk0;
+  bx.nty = bx.ntz = bx.nxc = 0;
+  bx.xlen = 1;
+  if (b.x1 > b.x0 && b.y1 > b.y0 && b.z1 > b.z0) p2_grid(b, t, S, &bx.nty, &bx.ntz, &bx.xlen, &bx.nxc);
+}
+
+// A launch over n boxes (n ≤ kP2Boxes): one grid, box k from workgroup blk0_k on. With several boxes each one's
+// x-chunk target is its share of t.target_blocks by work (tiles × planes), so together they fill the GPU once.
+P2Plan make_plan_p2(const Layout& l, const LBox* boxes, int n, const LeapfrogTbTiling& t, LBox real, bool init) {
+  const int S = t.stages;
+  W3D_REQUIRE(S >= 2 && S <= 5, "leapfrog_p2: stages must be 2..5");
+  W3D_REQUIRE(!init || S <= 4, "leapfrog_p2: the analytic-start pass takes at most 4 steps");
+  W3D_REQUIRE(n >= 1 && n <= kP2Boxes, "leapfrog_p2: too many boxes for one launch");
   W3D_REQUIRE(l.plane < (i64{1} << 27), "leapfrog_p2: plane too large for 32-bit buffer offsets");
+  const LBox full = compute_box(l);
+  if (real.x0 > real.x1) {
+    real.x0 = full.x0;
+    real.x1 = full.x1;
+  }
+  W3D_REQUIRE(real.x0 >= -l.xg && real.x1 <= l.nx + l.xg, "leapfrog_p2: real range outside the allocation in x");
   P2Plan pl;
   P2Params& p = pl.prm;
   p.plane = l.plane;
@@ -105,10 +125,6 @@ P2Plan make_plan_p2(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, L
   p.za = static_cast<int>(l.zg + l.zs);
   p.ay0 = static_cast<int>(-l.yg);
   p.ay1 = static_cast<int>(l.ny + l.yg);
-  p.x0 = static_cast<int>(b.x0);
-  p.x1 = static_cast<int>(b.x1);
-  p.xlen = static_cast<int>(imax(1, b.x1 - b.x0));
-  p.nxc = 1;
   p.sx0 = static_cast<int>(real.x0);
   p.sx1 = static_cast<int>(real.x1);
   p.ax0 = static_cast<int>(-l.xg);
@@ -117,12 +133,30 @@ P2Plan make_plan_p2(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, L
   p.gx0 = static_cast<int>(l.gx0);
   p.gy0 = static_cast<int>(l.gy0);
   p.gz0 = static_cast<int>(l.gz0);
-  p.y0 = static_cast<int>(b.y0);
-  p.z0 = static_cast<int>(b.z0);
-  p.y1 = static_cast<int>(b.y1);
-  p.z1 = static_cast<int>(b.z1);
-  if (b.x1 <= b.x0 || b.y1 <= b.y0 || b.z1 <= b.z0) return pl;
-  pl.nblocks = p2_grid(b, t, S, &p.nty, &p.ntz, &p.xlen, &p.nxc);
+  double work = 0.0;
+  for (int k = 0; k < n; ++k)
+    work += static_cast<double>(ceil_div(imax(0, boxes[k].y1 - boxes[k].y0), kT) *
+                                ceil_div(imax(0, boxes[k].z1 - boxes[k].z0), kT) * imax(0, boxes[k].x1 - boxes[k].x0));
+  int blk = 0;
+  p.nbox = n;
+  p.chunked = 0;
+  p.xlen_max = 1;
+  for (int k = 0; k < n; ++k) {
+    LeapfrogTbTiling tk = t;
+    if (n > 1 && work > 0.0) {
+      const double wk = static_cast<double>(ceil_div(imax(0, boxes[k].y1 - boxes[k].y0), kT) *
+                                            ceil_div(imax(0, boxes[k].z1 - boxes[k].z0), kT) *
+                                            imax(0, boxes[k].x1 - boxes[k].x0));
+      tk.target_blocks = imax(1, static_cast<int>(t.target_blocks * wk / work));
+    }
+    p2_box(l, boxes[k], tk, real, blk, p.box[k]);
+    blk += p.box[k].nty * p.box[k].ntz * p.box[k].nxc;
+    if (p.box[k].nxc > 1) p.chunked = 1;
+    p.xlen_max = imax(p.xlen_max, p.box[k].xlen);
+  }
+  p.nactive = blk;
+  if (blk == 0) return pl;
+  pl.nblocks = p2_round(blk, t);
   p.nblocks = pl.nblocks;
   p.xcd_remap = t.xcd_remap ? 1 : 0;
   p.xper = pl.nblocks / 8;
@@ -149,7 +183,7 @@ int leapfrog_p2_partials(const Layout& l, const LBox& box, const LeapfrogTbTilin
   (void)l;
   if (box.x1 <= box.x0 || box.y1 <= box.y0 || box.z1 <= box.z0) return 0;
   int n = 0, nty = 0, ntz = 0, xlen = 0, nxc = 0;
-  for (int S = 2; S <= 5; ++S) n = imax(n, p2_grid(box, t, S, &nty, &ntz, &xlen, &nxc));
+  for (int S = 2; S <= 5; ++S) n = imax(n, p2_round(p2_grid(box, t, S, &nty, &ntz, &xlen, &nxc), t));
   return n;
 }
 
@@ -182,13 +216,13 @@ void leapfrog_p2_prepare() {
   prepare_p2_s5();
 }
 
-void launch_leapfrog_p2(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
-                        double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
-                        Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, const LBox& real,
-                        bool analytic_start, int level_stride, int grid_blocks) {
+void launch_leapfrog_p2_boxes(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
+                              double* out2, const LBox* boxes, int nbox, const double* d_s, const double* ct,
+                              int check_mask, Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream,
+                              const LBox& real, bool analytic_start, int level_stride, int grid_blocks) {
   W3D_REQUIRE(out1 != out2 && (analytic_start || (prev != out1 && prev != out2 && cur != out1 && cur != out2)),
               "leapfrog_p2 needs four distinct buffers");
-  P2Plan pl = make_plan_p2(l, box, t, real, analytic_start);
+  P2Plan pl = make_plan_p2(l, boxes, nbox, t, real, analytic_start);
   if (pl.nblocks == 0) return;
   P2Params& p = pl.prm;
   if (grid_blocks > 0) {
@@ -218,6 +252,14 @@ void launch_leapfrog_p2(const Layout& l, const Coeffs& c, const double* prev, co
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) fail(std::string("leapfrog_p2 launch: ") + hipGetErrorString(e));
+}
+
+void launch_leapfrog_p2(const Layout& l, const Coeffs& c, const double* prev, const double* cur, double* out1,
+                        double* out2, const LBox& box, const double* d_s, const double* ct, int check_mask,
+                        Partial* partials, const LeapfrogTbTiling& t, hipStream_t stream, const LBox& real,
+                        bool analytic_start, int level_stride, int grid_blocks) {
+  launch_leapfrog_p2_boxes(l, c, prev, cur, out1, out2, &box, 1, d_s, ct, check_mask, partials, t, stream, real,
+                           analytic_start, level_stride, grid_blocks);
 }
 
 }  // namespace wave3d

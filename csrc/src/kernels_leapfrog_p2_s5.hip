@@ -1,5 +1,5 @@
-// k_leapfrog_p2 instantiations for S = 5 (normal passes only: an analytic-start pass with its φ slots would not fit
-// the 160 KiB of LDS at S = 5). Design: kernels_leapfrog_p2.hip.
+// k_leapfrog_p2 instantiations for S = 5 (normal passes only: an analytic-start pass of 5 stages needs one more level
+// of register queues than 128 VGPRs hold). Design: kernels_leapfrog_p2.hip.
 #include "wave3d/leapfrog_p2_launch.hpp"
 
 namespace wave3d {

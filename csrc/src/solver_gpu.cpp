@@ -776,8 +776,11 @@ void GpuSolver::unit_shell(int i) {
         capture::wait(xs, ev_shell_);
         for (const LBox& b : tb_shells(i)) tb_pass(u, b, kPhaseShell, xs);
       } else {
-        // (serial: the shells own the GPU and finish first, so the exchange starts as early as possible)
-        for (const LBox& b : tb_shells(i)) tb_pass(u, b, kPhaseShell, s0_);
+        // (serial: the shells own the GPU and finish first, so the exchange starts as early as possible; all of them
+        // in one pair-tiled launch where that applies — each alone left CUs idle, profiles/r6/)
+        const std::vector<LBox> sh = tb_shells(i);
+        if (!tb_pass_boxes(u, sh, kPhaseShell, s0_))
+          for (const LBox& b : sh) tb_pass(u, b, kPhaseShell, s0_);
         capture::record(ev_shell_, s0_);
         capture::wait(xs, ev_shell_);
       }
@@ -900,6 +903,42 @@ void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase, hipStream_t s
                        pk ? pk_dev_ + deep_s_ : nullptr);
   });
   if (mask) ++tb_slots_;
+}
+
+bool GpuSolver::tb_pass_boxes(const Unit& u, const std::vector<LBox>& boxes, int phase, hipStream_t st) {
+  if (boxes.size() < 2 || boxes.size() > static_cast<size_t>(kP2MaxBoxes) || !opt_.tiling_tb.p2 || push_ ||
+      (pk_dev_ != nullptr && pk_host_[deep_s_].w == deep_s_) || (u.analytic && u.steps > 4))
+    return false;
+  // (only where the shells' tiles alone do not fill the GPU: a 2048³ block rank's x-slab shell has 961 tiles of 5
+  // planes beside 63 border tiles of 1024 — one grid then runs no faster than three, and measured slower)
+  i64 tiles = 0;
+  for (const LBox& b : boxes) {
+    if (!leapfrog_p2_supported(lay_, b, u.steps)) return false;
+    tiles += ceil_div(imax(0, b.y1 - b.y0), kTbTile) * ceil_div(imax(0, b.z1 - b.z0), kTbTile);
+  }
+  if (tiles > opt_.tiling_tb.target_blocks) return false;
+  LeapfrogTbTiling t = opt_.tiling_tb;
+  t.stages = u.steps;
+  // (no XCD remap: the boxes' workgroups differ in length, and a contiguous logical range per XCD put the long ones
+  // on a few XCDs; dispatch order deals consecutive workgroups to the XCDs round-robin)
+  t.xcd_remap = false;
+  double cts[5] = {0, 0, 0, 0, 0};
+  int mask = 0;
+  for (int k = 1; k <= u.steps; ++k) {
+    cts[k - 1] = ct_[static_cast<size_t>(u.n + k)];
+    if (is_check_[static_cast<size_t>(u.n + k)]) mask |= 1 << (k - 1);
+  }
+  const int slots = mode_ == Mode::kDeepTb ? kTbSlots : 1;
+  W3D_REQUIRE(tb_slots_ < slots, "leapfrog_tb: too many launches in one unit");
+  Partial* part = mask ? tb_partials_ + tb_region_ * (kTbLevels * slots * n_tb_) + tb_slots_ * n_tb_ : nullptr;
+  const LBox real = mode_ == Mode::kDeepTb ? sreal_ : tb_default_real();
+  timed(phase, st, [&] {
+    launch_leapfrog_p2_boxes(lay_, coef_, u_[old_], u_[cur_], u_[uf_[0]], u_[uf_[1]], boxes.data(),
+                             static_cast<int>(boxes.size()), d_s_ + 1, cts, mask, part, t, st, real, u.analytic,
+                             slots * n_tb_, n_tb_);
+  });
+  if (mask) ++tb_slots_;
+  return true;
 }
 
 // The shell / interior split of a deep-tb unit whose exchange overlaps the next part of the pass: cpu.hpp deep_split

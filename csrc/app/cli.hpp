@@ -22,6 +22,7 @@ struct Args {
   int threads = 0;
   bool overlap = true;
   bool fused_pack = true;
+  bool ghost_store = true;  // --no-ghost-store: slab passes do not store the u^{n+S-1} ghost plane (A/B)
   bool graph = true;
   bool timers = false;
   bool debug_sync = false;

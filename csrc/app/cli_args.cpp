@@ -48,6 +48,7 @@ constexpr Personality kPersonalities[] = {
                "  --cpu [--threads T] sequential/OpenMP CPU path\n"
                "  --no-overlap       halo exchange on the compute stream (A/B switch)\n"
                "  --no-fused-pack    3-D block passes: pack the z faces with the pack kernel too (A/B switch)\n"
+               "  --no-ghost-store   slab passes: exchange S-1 planes of u^{n+S-1}, not S-2 plus a stored ghost (A/B)\n"
                "  --no-graph         eager launches instead of one captured hipGraph\n"
                "  --timers           per-phase GPU timers (init / compute / exchange / check)\n"
                "  --no-temporal      one leapfrog step per HBM pass (disable temporal blocking)\n"
@@ -133,6 +134,7 @@ Args parse(int argc, char** argv) {
     else if (s == "--threads") a.threads = std::stoi(next());
     else if (s == "--no-overlap") a.overlap = false;
     else if (s == "--no-fused-pack") a.fused_pack = false;
+    else if (s == "--no-ghost-store") a.ghost_store = false;
     else if (s == "--no-graph") a.graph = false;
     else if (s == "--timers") a.timers = true;
     else if (s == "--debug-sync") a.debug_sync = true;
@@ -304,6 +306,7 @@ SolverOptions options_from(const Args& a, bool fake) {
   o.check_every = a.check_every;
   o.overlap = a.overlap;
   o.fused_pack = a.fused_pack;
+  o.ghost_store = a.ghost_store;
   o.graph = a.graph;
   o.timers = a.timers;
   o.debug_sync = a.debug_sync;

@@ -88,6 +88,11 @@ struct LeapfrogTbTiling {
   int target_blocks = 256; // fewer (y,z) tiles than this: split x into chunks (one workgroup per CU at 1 WG/CU)
   int min_chunk = 16;      // ... of at least this many planes (each chunk recomputes S−1 planes on both sides)
   bool p2 = true;          // the pair-tiled pass (k_leapfrog_p2, S ≤ 5) wherever it applies (leapfrog_p2_supported)
+  // (pair-tiled pass only) bit 0 / 1: also store u^{n+S−1} on the x ghost plane −1 / nx where a box starts / ends at
+  // the rank's first / last plane. The pass computes that plane anyway (level S−1 reaches one node beyond the box), so
+  // the slab exchange that follows sends S − 2 planes of u^{n+S−1} per face instead of S − 1 (solver_gpu.cpp
+  // ghost_bits). The 4-step k_leapfrog_tb refuses it.
+  int ghost_x1 = 0;
 };
 // Slab peer-push transport of an LDS pass (x faces only; every slab rank has the same plane geometry, so a plane's
 // in-plane offsets are the same on both sides). The pass

@@ -253,6 +253,7 @@ struct P2Box {
   int x0, x1, xlen, nxc;  // output x range; chunk length and count
   int y0, z0, y1, z1;     // output (y, z) box (local)
   int nty, ntz, blk0;
+  int gxl, gxh;           // u^{n+S−1} also on plane x0 − 1 / x1 (LeapfrogTbTiling::ghost_x1)
 };
 constexpr int kP2Boxes = kP2MaxBoxes;
 struct P2Params {
@@ -404,6 +405,11 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     const int ty0 = B.y0 + tyi * kT, tz0 = B.z0 + tzi * kT;
     const int wx0 = CH ? B.x0 + chunk * B.xlen : B.x0;
     const int wx1 = CH ? min(B.x1, wx0 + B.xlen) : B.x1;
+    // level S−1 is computed one plane beyond the chunk on both sides; where the box side is a rank face whose
+    // neighbour would otherwise send that plane, it is stored too (the 5-step passes' split stores reach plane wx1
+    // one iteration after the march's last: one more iteration, its stages all outside their ranges)
+    const int o1x0 = wx0 - (B.gxl && wx0 == B.x0 ? 1 : 0);
+    const int o1x1 = wx1 + (B.gxh && wx1 == B.x1 ? 1 : 0);
     const int N = p.N;
     const i64 P = p.plane;
     auto inside = [&](int g) __attribute__((always_inline)) {
@@ -552,7 +558,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     D2 phq[2] = {D2m(0.0, 0.0), D2m(0.0, 0.0)};  // (analytic start: the pair's own φ by plane parity)
     (void)phq;
 
-    const int i0 = wx0 - S + 1, i1 = wx1 + S - 2;
+    const int i0 = wx0 - S + 1, i1 = wx1 + S - 2 + (kSplitSt && o1x1 > wx1 ? 1 : 0);
     auto xreal = [&](int x) __attribute__((always_inline)) {
       return x >= p.sx0 && x < p.sx1 && inside(p.gx0 + x);
     };
@@ -581,6 +587,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
       constexpr int sm = (D + 3) & 3, s0 = D, sp = (D + 1) & 3;
       const bool inr = BK || (xp >= wx0 - (S - k) && xp < wx1 + (S - k));
       const bool xown = BK || (xp >= wx0 && xp < wx1);
+      const bool xown1 = BK || (xp >= o1x0 && xp < o1x1);  // (stores of level S−1; bulk planes are inside the box)
       D2 v = D2m(0.0, 0.0);
       if (inr && wst >= k) {  // (wave-uniform)
         const D2 c = L[k - 1][s0], xm = L[k - 1][sm], xq = L[k - 1][sp];
@@ -651,14 +658,14 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
           store_pair(v, p.out2, xp, soff, xown);
         } else {
           constexpr int pl = (S - 2) * 2 + (D & 1);  // level S−1, plane xp: written by stage S−1 last iteration
-          store_pair(rd2(rt, ok_(pl, 0, 0)), p.out1, xp, soff2, xown);
+          store_pair(rd2(rt, ok_(pl, 0, 0)), p.out1, xp, soff2, xown1);
         }
       } else if constexpr (!kSplitSt && k >= S - 1) {
         // the thread's store offset plus a scalar offset (0 for the own waves' planes, out of range otherwise).
         // Passes that load: every wave stores (non-owners beyond the plane: dropped), so every wave's vector-memory
         // sequence is the same and the compiler's waits for the loads can leave the stores in flight. The analytic
         // start loads nothing: only the own waves store (−2 %)
-        if (!INIT || winner) store_pair(v, k == S ? p.out2 : p.out1, xp, soff, xown && winner);
+        if (!INIT || winner) store_pair(v, k == S ? p.out2 : p.out1, xp, soff, (k == S ? xown : xown1) && winner);
       }
     };
 

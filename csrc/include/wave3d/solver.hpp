@@ -75,6 +75,10 @@ struct SolverOptions {
   // 3-D block LDS passes: the pass stores the z-face message parts of the next exchange straight into the send staging
   // (TbPack, kernels.hpp); the pack kernel then copies only the x / y faces, edges and corners (A/B: --no-fused-pack)
   bool fused_pack = true;
+  // slab LDS passes (deep-tb, pair-tiled kernel; RCCL / loopback / copy-engine transports): each pass also stores the
+  // u^{n+S−1} plane next to each neighbour face (it computes it anyway), so the exchange sends S planes of u^{n+S} and
+  // S − 2 (not S − 1) of u^{n+S−1} per face — 8 instead of 9 planes for a 5-step pass (A/B: --no-ghost-store)
+  bool ghost_store = true;
   // deep-tb with overlap: the shell boxes run on the side stream concurrently with the interior (true), or on s0 before
   // it (false: they get the whole GPU and finish first, so the exchange starts earlier — measured faster with the copy
   // engines at 512³ and 2048³; concurrent helps the small block shells when no transfer follows; env W3D_SHELLS)
@@ -265,6 +269,7 @@ class GpuSolver {
   // deep-tb without overlap: no shell launches; each pass runs whole and its faces are exchanged after it (on s0)
   bool late_exchange() const;
   bool needs_exchange(int i) const;
+  int ghost_bits(int i) const;  // x sides whose u^{n+S−1} ghost plane unit i's passes store (SolverOptions::ghost_store)
   hipStream_t xstream() const;
   bool pairable() const;
   bool analytic_ok() const;  // the first unit can be an analytic-start LDS pass

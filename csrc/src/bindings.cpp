@@ -415,7 +415,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("xcd_blocks", &LeapfrogTbTiling::xcd_blocks)
       .def_readwrite("target_blocks", &LeapfrogTbTiling::target_blocks)
       .def_readwrite("min_chunk", &LeapfrogTbTiling::min_chunk)
-      .def_readwrite("p2", &LeapfrogTbTiling::p2);
+      .def_readwrite("p2", &LeapfrogTbTiling::p2)
+      .def_readwrite("ghost_x1", &LeapfrogTbTiling::ghost_x1);
   m.def("capture_guard_selftest", &wave3d::capture::selftest, py::arg("mode"),
         "the probe topologies through the stream-capture guard (0: production, 2: the round-4 sibling wait)");
   m.def("leapfrog_p2_table", [](int stages) {
@@ -477,6 +478,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("reserve_cus", &SolverOptions::reserve_cus)
       .def_readwrite("fake_traffic", &SolverOptions::fake_traffic)
       .def_readwrite("fused_pack", &SolverOptions::fused_pack)
+      .def_readwrite("ghost_store", &SolverOptions::ghost_store)
       .def_readwrite("sdma_streams", &SolverOptions::sdma_streams)
       .def_readwrite("flag_timeout_s", &SolverOptions::flag_timeout_s)
       .def_readwrite("push_no_collective", &SolverOptions::push_no_collective)
@@ -647,6 +649,15 @@ PYBIND11_MODULE(_C, m) {
            "pass depth every rank runs (the constructor lowers the requested depth where a schedule needs it)")
       .def("overlapped", [](GpuGroup& g) { return g.rank(0).overlapped(); })
       .def("comm_counts", &GpuGroup::comm_counts)
+      .def("traffic",
+           [](GpuGroup& g, int rank) {
+             const GpuSolver::Traffic t = g.rank(rank).traffic();
+             py::dict d;
+             d["field_bytes"] = t.field_bytes;
+             d["halo_bytes"] = t.halo_bytes;
+             return d;
+           },
+           py::arg("rank"), "GpuSolver.traffic() of one rank (bytes per solve of the last run()'s schedule)")
       .def("set_state", [](GpuGroup& g, const darr& prev, const darr& cur, int n0) {
         const i64 n = g.rank(0).problem().N + 1;
         g.set_state(ro_ptr(prev, n * n * n, "prev"), ro_ptr(cur, n * n * n, "cur"), n0);

@@ -98,6 +98,12 @@ void p2_box(const Layout& l, const LBox& b, const LeapfrogTbTiling& t, const LBo
   bx.y1 = static_cast<int>(b.y1);
   bx.z1 = static_cast<int>(b.z1);
   bx.blk0 = blk0;
+  // ghost-plane stores of u^{n+S−1}: only on a side at the rank's face, within the real (computed) range
+  const LBox full = compute_box(l);
+  bx.gxl = (t.ghost_x1 & 1) && b.x0 == full.x0 ? 1 : 0;
+  bx.gxh = (t.ghost_x1 & 2) && b.x1 == full.x1 ? 1 : 0;
+  W3D_REQUIRE(!bx.gxl || (real.x0 <= b.x0 - 1 && b.x0 - 1 >= -l.xg), "leapfrog_p2: ghost plane x0 − 1 not computed");
+  W3D_REQUIRE(!bx.gxh || (real.x1 >= b.x1 + 1 && b.x1 < l.nx + l.xg), "leapfrog_p2: ghost plane x1 not computed");
   bx.nty = bx.ntz = bx.nxc = 0;
   bx.xlen = 1;
   if (b.x1 > b.x0 && b.y1 > b.y0 && b.z1 > b.z0) p2_grid(b, t, S, &bx.nty, &bx.ntz, &bx.xlen, &bx.nxc);

@@ -98,6 +98,7 @@ void launch_leapfrog_tb(const Layout& l, const Coeffs& c, const double* prev, co
     return;
   }
   W3D_REQUIRE(t.stages <= 4, "leapfrog_tb: 5-step passes need the pair-tiled kernel (tiling.p2)");
+  W3D_REQUIRE(t.ghost_x1 == 0, "leapfrog_tb: ghost-plane stores (tiling.ghost_x1) need the pair-tiled kernel");
   TbPlan pl = make_plan_tb(l, box, t, real);
   if (pl.nblocks == 0) return;
   TbParams& p = pl.prm;

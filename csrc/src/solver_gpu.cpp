@@ -409,6 +409,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   if (n_tb_ > 0)
     W3D_HIP(hipMalloc(&tb_partials_, static_cast<size_t>(kTbRegions) * kTbLevels * kTbSlots * n_tb_ * sizeof(Partial)));
   W3D_HIP(hipMalloc(&errlog_, static_cast<size_t>(prob_.K + 1) * sizeof(Partial)));
+  W3D_HIP(hipMemset(errlog_, 0, static_cast<size_t>(prob_.K + 1) * sizeof(Partial)));
   W3D_HIP(hipMalloc(&errall_, static_cast<size_t>(world_) * (prob_.K + 1) * sizeof(Partial)));
   ct_.resize(static_cast<size_t>(prob_.K + 1));
   for (int n = 0; n <= prob_.K; ++n) ct_[static_cast<size_t>(n)] = time_factor(prob_, n);
@@ -511,6 +512,8 @@ GpuSolver::Traffic GpuSolver::traffic() {
   const std::vector<Msg> keep = msgs_;
   const int keep_s = deep_s_;
   for (int i = 0; i < static_cast<int>(units_.size()); ++i) {
+    const int gb = ghost_bits(i);  // (the stored u^{n+S−1} ghost planes: one plane per face)
+    t.field_bytes += static_cast<double>((gb & 1) + (gb >> 1)) * static_cast<double>(lay_.plane) * sizeof(double);
     if (!needs_exchange(i)) continue;
     build_msgs(i);
     for (const Msg& m : msgs_) t.halo_bytes += static_cast<double>(m.count) * sizeof(double);
@@ -542,6 +545,23 @@ bool GpuSolver::late_exchange() const { return mode_ == Mode::kDeepTb && !opt_.o
 bool GpuSolver::needs_exchange(int i) const {
   if (!plan_.any() || push_) return false;  // (push: the passes deliver the ghosts themselves)
   return post_exchange() ? i + 1 < static_cast<int>(units_.size()) : i > 0;
+}
+
+// u^{n+S−1} ghost-plane stores (SolverOptions::ghost_store): unit i's pair-tiled passes also store that level on the
+// ghost plane beyond each x face with a neighbour (bit 0: plane −1, bit 1: plane nx), which exchange i then leaves out.
+// Slab ranks only (a 3-D block rank's edge and corner regions would become L-shaped messages), and only where every
+// pass of the unit runs on the pair-tiled kernel (launch_leapfrog_tb refuses the bits otherwise). Every rank computes
+// the same bits for the same exchange (same units, same options), so both ends of a face agree on the message size.
+int GpuSolver::ghost_bits(int i) const {
+  if (!opt_.ghost_store || mode_ != Mode::kDeepTb || block_tb_ || push_ || !opt_.tiling_tb.p2 || pk_dev_ != nullptr ||
+      i < 0 || i >= static_cast<int>(units_.size()) || !needs_exchange(i))
+    return 0;
+  const Unit& u = units_[static_cast<size_t>(i)];
+  if ((u.analytic && u.steps > 4) || !leapfrog_p2_supported(lay_, full_, u.steps)) return 0;
+  int bits = 0;
+  for (const Face& f : plan_.faces)
+    if (f.axis == 0) bits |= 1 << f.side;
+  return bits;
 }
 
 hipStream_t GpuSolver::xstream() const {
@@ -642,12 +662,16 @@ void GpuSolver::build_msgs(int i) {
     const i64 s = units_[static_cast<size_t>(i) + 1].steps, P = lay_.plane, nx = lay_.nx;
     double* out1 = u_[uf_[0]];
     double* out2 = u_[uf_[1]];
+    // (ghost_bits: the pass stored u^{n+S−1} on the first ghost plane itself; that part then starts one plane further
+    // from the face on both ends: our planes 1..s−2 / nx−s+1..nx−2 into the peer's ghosts at distance 2..s−1)
+    const int gb = ghost_bits(i);
     for (const Face& f : plan_.faces) {
       W3D_REQUIRE(f.axis == 0, "deep-tb mode is slab-only");
-      const i64 s2 = f.side == 0 ? 0 : nx - s, s1 = f.side == 0 ? 0 : nx - (s - 1);
-      const i64 r2 = f.side == 0 ? -s : nx, r1 = f.side == 0 ? -(s - 1) : nx;
+      const i64 g = (gb >> f.side) & 1, d1 = s - 1 - g;
+      const i64 s2 = f.side == 0 ? 0 : nx - s, s1 = f.side == 0 ? g : nx - (s - 1);
+      const i64 r2 = f.side == 0 ? -s : nx, r1 = f.side == 0 ? -(s - 1) : nx + g;
       msgs_.push_back(Msg{f.peer, 0, out2 + lay_.plane_off(s2), out2 + lay_.plane_off(r2), s * P});
-      msgs_.push_back(Msg{f.peer, 1, out1 + lay_.plane_off(s1), out1 + lay_.plane_off(r1), (s - 1) * P});
+      if (d1 > 0) msgs_.push_back(Msg{f.peer, 1, out1 + lay_.plane_off(s1), out1 + lay_.plane_off(r1), d1 * P});
     }
     return;
   }
@@ -684,7 +708,11 @@ void GpuSolver::phase_init() {
   cur_unit_ = -1;
   ev_next_ = 0;
   marks_.clear();
-  W3D_HIP(hipMemsetAsync(errlog_, 0, static_cast<size_t>(K + 1) * sizeof(Partial), s0_));
+  // (the log's checked entries are rewritten by every solve and the others stay 0 from the allocation: cleared only
+  // where something else writes into it — the copy-engine and push waits report their status there — or a resumed
+  // solve leaves the entries below its start alone)
+  if (sdma_ || push_ || resume_n_ > 0)
+    W3D_HIP(hipMemsetAsync(errlog_, 0, static_cast<size_t>(K + 1) * sizeof(Partial), s0_));
   if (push_) {
     W3D_HIP(hipMemsetAsync(flags_ + 8, 0, sizeof(unsigned), s0_));  // workgroups done (the passes' signal counter)
     // (in-process group only: there every rank's init precedes every pass, so no neighbour has written yet)
@@ -871,6 +899,7 @@ void GpuSolver::tb_pass(const Unit& u, const LBox& box, int phase, hipStream_t s
   if (st == nullptr) st = s0_;
   LeapfrogTbTiling t = opt_.tiling_tb;
   t.stages = u.steps;
+  t.ghost_x1 = ghost_bits(cur_unit_);
   double cts[5] = {0, 0, 0, 0, 0};
   int mask = 0;
   for (int k = 1; k <= u.steps; ++k) {
@@ -922,6 +951,7 @@ bool GpuSolver::tb_pass_boxes(const Unit& u, const std::vector<LBox>& boxes, int
   // (no XCD remap: the boxes' workgroups differ in length, and a contiguous logical range per XCD put the long ones
   // on a few XCDs; dispatch order deals consecutive workgroups to the XCDs round-robin)
   t.xcd_remap = false;
+  t.ghost_x1 = ghost_bits(cur_unit_);
   double cts[5] = {0, 0, 0, 0, 0};
   int mask = 0;
   for (int k = 1; k <= u.steps; ++k) {

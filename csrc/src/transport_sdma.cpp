@@ -271,11 +271,14 @@ void GpuSolver::unit_exchange_sdma(int i) {
         } else {
           // u^{n+S} s planes deep and u^{n+S−1} s − 1 deep: this rank's planes next to the face → the peer's ghost
           // planes beyond its facing side (the peer's plane p sits at (p + xg)·plane in its buffers, same geometry)
+          // (ghost_bits: both ends stored u^{n+S−1}'s first ghost plane themselves — its part starts one plane in)
           for (int f = 0; f < 2; ++f) {
-            const i64 d = f == 0 ? s : s - 1;
+            const i64 g = f == 1 ? (ghost_bits(i) >> l.side) & 1 : 0;
+            const i64 d = (f == 0 ? s : s - 1) - g;
+            if (d <= 0) continue;
             const int b = uf_[f == 0 ? 1 : 0];
-            const i64 src = l.side == 0 ? 0 : lay_.nx - d;
-            const i64 dst = l.side == 0 ? l.peer_nx : -d;
+            const i64 src = l.side == 0 ? g : lay_.nx - d - g;
+            const i64 dst = l.side == 0 ? l.peer_nx + g : -d - g;
             W3D_HIP(hipMemcpyAsync(l.u[b] + (dst + lay_.xg) * static_cast<i64>(P), u_[b] + lay_.plane_off(src),
                                    static_cast<size_t>(d) * P * sizeof(double), hipMemcpyDeviceToDeviceNoCU, cs));
           }
@@ -337,8 +340,10 @@ void GpuSolver::sdma_poison(int i, const int uf[2]) {
   const size_t P = static_cast<size_t>(lay_.plane);
   for (const XLink& l : xlinks_)
     for (int f = 0; f < 2; ++f) {
-      const i64 d = f == 0 ? s : s - 1;
-      const i64 g = l.side == 0 ? -d : lay_.nx;
+      const i64 g1 = f == 1 ? (ghost_bits(i) >> l.side) & 1 : 0;  // (the plane unit i stores itself: not poisoned)
+      const i64 d = (f == 0 ? s : s - 1) - g1;
+      if (d <= 0) continue;
+      const i64 g = l.side == 0 ? -d - g1 : lay_.nx + g1;
       W3D_HIP(hipMemsetAsync(u_[uf[f == 0 ? 1 : 0]] + lay_.plane_off(g), 0xFF, static_cast<size_t>(d) * P * sizeof(double),
                              s0_));
     }

@@ -99,6 +99,7 @@ class Solver:
                  debug_sync: bool = False, poison_ghosts: bool = False, deep_min_planes: int | None = None,
                  tb_min_planes: int | None = None, rccl: bool = True, autotune: bool = False,
                  autotune_rounds: int = 5, copy_engines: bool = False, fused_pack: bool = True,
+                 ghost_store: bool = True,
                  runtime: str = "inproc"):
         import torch.distributed as dist
 
@@ -133,7 +134,8 @@ class Solver:
             if copy_engines and self.transport not in ("sdma", "sdma-ipc"):
                 raise ValueError("runtime='process': copy engines are the 'sdma' transport (transport='sdma')")
             for on, flag in ((timers, "--timers"), (debug_sync, "--debug-sync"), (poison_ghosts, "--poison-ghosts"),
-                             (not tb, "--no-tb"), (not init2, "--no-init2"), (not fused_pack, "--no-fused-pack")):
+                             (not tb, "--no-tb"), (not init2, "--no-init2"), (not fused_pack, "--no-fused-pack"),
+                             (not ghost_store, "--no-ghost-store")):
                 if on:
                     flags.append(flag)
             for val, flag in ((tb_min_planes, "--tb-min-planes"), (deep_min_planes, "--deep-min-planes")):
@@ -156,7 +158,7 @@ class Solver:
         if self.backend == "hip" and self.transport in ("loopback", "rccl-self", "push", "sdma", "multi-device"):
             opts = self._options(C, decomp, spec, overlap, graph, tiling, temporal, tiling2, init2, tb, tiling_tb)
             opts.timers, opts.debug_sync, opts.poison_ghosts = timers, debug_sync, poison_ghosts
-            opts.fused_pack = fused_pack
+            opts.fused_pack, opts.ghost_store = fused_pack, ghost_store
             if deep_min_planes is not None:
                 opts.deep_min_planes = deep_min_planes
             if tb_min_planes is not None:
@@ -169,7 +171,7 @@ class Solver:
 
             opts = self._options(C, decomp, spec, overlap, graph, tiling, temporal, tiling2, init2, tb, tiling_tb)
             opts.timers, opts.debug_sync, opts.poison_ghosts = timers, debug_sync, poison_ghosts
-            opts.fused_pack = fused_pack
+            opts.fused_pack, opts.ghost_store = fused_pack, ghost_store
             if deep_min_planes is not None:
                 opts.deep_min_planes = deep_min_planes
             if tb_min_planes is not None:

@@ -346,3 +346,35 @@ def test_block_overlap_p2_bitexact(gpu, world, decomp, N, temporal, transport):
         _same(r, r1)
         assert torch.equal(g.global_field(0), f0)
         assert torch.equal(g.global_field(1), f1)
+
+
+@pytest.mark.parametrize("transport", ["loopback", "rccl-self", "sdma"])
+@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("world,temporal,K", [(2, 5, 20), (3, 5, 21), (3, 4, 21), (4, 3, 21), (8, 2, 21)])
+def test_slab_ghost_store_bitexact(gpu, world, temporal, K, overlap, transport):
+    """Round 6: slab passes store u^{n+S−1} on the first ghost plane beyond each neighbour face themselves (they compute
+    it anyway; SolverOptions.ghost_store), and the exchange sends S − 2 planes of that level instead of S − 1 (the 5-step
+    passes' split stores reach the upper ghost plane with one more march iteration). Bit-identical to one GPU with
+    NaN-poisoned ghosts, eager and replayed, on RCCL, loopback and copy-engine transports; with the option off the same
+    result, and exactly one plane per face per exchange more."""
+    spec = ProblemSpec(N=66, tau=1e-3, K=K)
+    ref = Solver(spec, backend="hip", device=0, temporal=1)
+    r1 = ref.run()
+    f0, f1 = ref.global_field(0), ref.global_field(1)
+    halo = {}
+    for ghost in (True, False):
+        g = Solver(spec, backend="hip", transport=transport, world=world, rank=0, decomp="slab", device=0,
+                   overlap=overlap, poison_ghosts=True, temporal=temporal, tb_min_planes=2 * temporal,
+                   ghost_store=ghost)
+        assert g.native.mode() == "deep-tb" and g.native.temporal() == temporal
+        for _ in range(2):
+            r = g.run()
+            _same(r, r1)
+            assert torch.equal(g.global_field(0), f0)
+            assert torch.equal(g.global_field(1), f1)
+        halo[ghost] = g.native.traffic(1)["halo_bytes"]  # (rank 1: neighbours on both sides unless world = 2)
+        plane_bytes = 8 * g.native.layout(1).plane
+    # one plane per face per exchange (one after every pass but the last) fewer
+    faces = 1 if world == 2 else 2
+    exchanges = (halo[False] - halo[True]) / (faces * plane_bytes)
+    assert exchanges == int(exchanges) and 2 <= exchanges <= K // 2

@@ -102,9 +102,13 @@ def test_cli_traffic_line_and_json(gpu, tmp_path):
     out = subprocess.run([CLI, "128", "0.001", "20", "1", "--fake-rank", "0/2", "--repeat", "2", "--warmup", "1",
                           "--json", js, "--quiet"], check=True, timeout=120, capture_output=True, text=True).stdout
     m = json.loads(open(js).read())
-    plane_bytes = m["halo_bytes"] / (3 * 9)  # three exchanges of 5 + 4 planes on the one face
+    # three exchanges on the one face: 5 planes of u^{n+5} and 3 of u^{n+4} (the pass stores the 4th itself: ghost_store)
+    plane_bytes = m["halo_bytes"] / (3 * 8)
     assert m["halo_bytes"] > 0 and plane_bytes == int(plane_bytes) and plane_bytes >= 129 * 129 * 8
     assert "Traffic (this rank): " in out
+    subprocess.run([CLI, "128", "0.001", "20", "1", "--fake-rank", "0/2", "--repeat", "2", "--warmup", "1",
+                    "--json", js, "--quiet", "--no-ghost-store"], check=True, timeout=120, capture_output=True)
+    assert json.loads(open(js).read())["halo_bytes"] == m["halo_bytes"] * 9 / 8  # 5 + 4 planes per exchange
 
 
 @pytest.mark.parametrize("world,decomp,N", [(4, "2x2x1", 66), (8, "2x2x2", 77), (6, "1x2x3", 71), (8, "2x2x2", 128)])

@@ -89,7 +89,8 @@ def test_rccl_self_block_deep_tb_graph(gpu, tmp_path, world, decomp, K):
 
 def test_cli_traffic_line_and_json(gpu, tmp_path):
     """Effective GB/s: the CLI prints the schedule's compulsory field traffic and halo volume per
-    solve and puts both (and the GB/s) into --json; a fake slab rank of 2 sends 5 + 4 planes after each pass."""
+    solve and puts both (and the GB/s) into --json; a fake slab rank of 2 sends 5 + 3 planes after each pass (5 + 4
+    with --no-ghost-store)."""
     js = str(tmp_path / "one.json")
     out = subprocess.run([CLI, "128", "0.001", "20", "1", "--repeat", "2", "--warmup", "1", "--json", js, "--quiet"],
                          check=True, timeout=120, capture_output=True, text=True).stdout

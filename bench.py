@@ -192,6 +192,8 @@ def _child(a, rank: int, world: int, local: int, args: list[str], tag: str, rank
             env["W3D_SHARE_GPUS"] = "1"
             if jw > 1 and _distinct_gpus(jw) < jw and a.native_transport == "push":
                 env["W3D_CU_SPLIT"] = "auto"  # concurrent ranks on one GPU: disjoint CU ranges (in-kernel push waits)
+        if tag == "fallback":  # (the conservative retry also times its block with one host round trip per solve)
+            env["W3D_BENCH_SYNC_EACH"] = "1"
         # fault injection (tests): the main run; W3D_BENCH_FAIL_FALLBACK=1 also the conservative retry
         fail_rank = os.environ.get("W3D_BENCH_FAIL_SETUP_RANK")
         if fail_rank is not None and (tag == "main" or (tag == "fallback" and os.environ.get("W3D_BENCH_FAIL_FALLBACK"))):

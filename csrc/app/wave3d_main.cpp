@@ -408,6 +408,7 @@ int run_gpu(const Args& a) {
         << ", \"schedule\": " << jstr(sched) << ", \"mode\": " << jstr(s->mode())
         << ", \"transport\": " << jstr(s->transport()) << ", \"device\": "
         << jstr(prop.gcnArchName) << ", \"bench_steps\": " << a.bench_steps << ", \"bench_s\": " << jnum(bench_s)
+        << ", \"bench_pipelined\": " << (a.bench_steps > 0 && r.batched ? "true" : "false")
         << ", \"warmup\": " << a.warmup << ", \"finite\": " << (r.finite ? "true" : "false") << ", \"autotune_s\": {";
       for (size_t i = 0; i < tuned.times.size(); ++i)
         j << (i ? ", " : "") << jstr(tuned.times[i].first) << ": " << jnum(tuned.times[i].second);

@@ -275,6 +275,9 @@ struct P2Params {
   int check_mask;
   double tau2, half_tau2;
   double ct[5];
+#ifdef W3D_EXPERIMENT_WGTIME
+  unsigned long long* wgtime;  // (perf study) 4 wall-clock stamps per workgroup, pinned host memory
+#endif
 };
 
 // cache-policy bits of the plane loads / stores (gfx950 CPol: 1 = sc0, 2 = nt, 16 = sc1): non-temporal stores (the new
@@ -355,6 +358,7 @@ __device__ __forceinline__ int p2_desc(int tid) {
 //   W3D_EXPERIMENT_NOSTORE   the pass writes nothing to HBM
 //   W3D_EXPERIMENT_NOBARRIER the per-plane barrier removed
 //   W3D_EXPERIMENT_NOCHECK   no fused error check; W3D_EXPERIMENT_NORED no partial reduction
+//   W3D_EXPERIMENT_WGTIME    (results right) each workgroup's wall clock at entry, march start, march end and exit
 // Variants measured and removed (their numbers stay in profiles/r5/: store_experiments.md, memops/README.md,
 // p2_attribution.md): deferred stores, two-plane-ahead prefetch, staggered waves, conditional queue writes, the late
 // u^n load point, row-major halo lanes, split stores in the analytic start, stores from every wave, a separate
@@ -371,6 +375,14 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
   constexpr bool kSplitSt = !INIT && S == 5;
   extern __shared__ double lds[];
   const int tid = static_cast<int>(threadIdx.x);
+#ifdef W3D_EXPERIMENT_WGTIME
+  auto stamp = [&](int j) __attribute__((always_inline)) {
+    if (tid == 0) p.wgtime[static_cast<size_t>(blockIdx.x) * 4 + j] = wall_clock64();
+  };
+#else
+  auto stamp = [](int) __attribute__((always_inline)) {};
+#endif
+  stamp(0);
   int blk = static_cast<int>(blockIdx.x);
   if (p.xcd_remap) {  // XCD k (= blockIdx % 8 in dispatch order) takes the k-th contiguous range of xper blocks
     const int j = blk >> 3;
@@ -775,6 +787,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     const int blo = max(max(wx0, p.sx0), 1 - p.gx0) + (S - 1);
     const int bhi = min(min(wx1, p.sx1), N - p.gx0);
     int ib = i0;
+    stamp(1);
     const int nhead = blo > i0 ? (blo - i0 + 3) / 4 : 0;
     for (int hb = 0; hb < nhead && ib + 3 <= i1; ++hb, ib += 4) {
       iteration(std::integral_constant<int, 0>{}, Gen{}, ib);
@@ -800,8 +813,13 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
       if (ib + 3 > i1) break;
       iteration(std::integral_constant<int, 3>{}, Gen{}, ib + 3);
     }
+    stamp(2);
   }
 
+#ifdef W3D_EXPERIMENT_WGTIME
+  __syncthreads();
+  stamp(3);
+#endif
 #ifdef W3D_EXPERIMENT_NORED
   return;
 #endif

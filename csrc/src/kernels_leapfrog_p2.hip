@@ -27,6 +27,13 @@
 // k_init_first + S steps. Tests: tests/test_gpu_kernels.py (test_leapfrog_p2_*).
 #include "wave3d/leapfrog_p2_launch.hpp"
 
+#ifdef W3D_EXPERIMENT_WGTIME
+#include <array>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#endif
+
 namespace wave3d {
 
 using namespace p2k;
@@ -169,6 +176,52 @@ P2Plan make_plan_p2(const Layout& l, const LBox* boxes, int n, const LeapfrogTbT
   return pl;
 }
 
+#ifdef W3D_EXPERIMENT_WGTIME
+// (perf study) every launch gets its own slot of 4 stamps per workgroup in pinned host memory (a captured launch keeps
+// its slot: each replay overwrites it, so the file holds the last replay); written to $W3D_WGTIME_OUT at exit as text
+// lines "launch S init nblocks" followed by one line of 4 stamps (100 MHz wall clock) per workgroup
+struct WgTimeLog {
+  unsigned long long* buf = nullptr;
+  size_t cap = size_t{1} << 22, used = 0;
+  std::vector<std::array<int, 4>> launches;  // S, init, nblocks, offset / 4
+};
+WgTimeLog& wgtime_log() {
+  static WgTimeLog g;
+  return g;
+}
+void wgtime_dump() {
+  WgTimeLog& g = wgtime_log();
+  const char* path = std::getenv("W3D_WGTIME_OUT");
+  if (!path || !g.buf) return;
+  FILE* f = std::fopen(path, "w");
+  if (!f) return;
+  for (size_t l = 0; l < g.launches.size(); ++l) {
+    const auto& L = g.launches[l];
+    std::fprintf(f, "launch %zu %d %d %d\n", l, L[0], L[1], L[2]);
+    for (int b = 0; b < L[2]; ++b) {
+      const unsigned long long* q = g.buf + (static_cast<size_t>(L[3]) + b) * 4;
+      std::fprintf(f, "%llu %llu %llu %llu\n", q[0], q[1], q[2], q[3]);
+    }
+  }
+  std::fclose(f);
+}
+unsigned long long* wgtime_slot(int nblocks, int S, bool init) {
+  WgTimeLog& g = wgtime_log();
+  if (!g.buf) {
+    W3D_REQUIRE(hipHostMalloc(reinterpret_cast<void**>(&g.buf), g.cap * sizeof(unsigned long long),
+                              hipHostMallocDefault) == hipSuccess,
+                "wgtime: pinned buffer");
+    std::atexit(wgtime_dump);
+  }
+  if (nblocks == 0) return g.buf;
+  W3D_REQUIRE(g.used + static_cast<size_t>(nblocks) * 4 <= g.cap, "wgtime: log full");
+  unsigned long long* q = g.buf + g.used;
+  g.launches.push_back({S, init ? 1 : 0, nblocks, static_cast<int>(g.used / 4)});
+  g.used += static_cast<size_t>(nblocks) * 4;
+  return q;
+}
+#endif
+
 }  // namespace
 
 bool leapfrog_p2_supported(const Layout& l, const LBox& box, int stages) {
@@ -216,6 +269,9 @@ std::vector<int> leapfrog_p2_table(int stages, std::vector<long>* geometry) {
 }
 
 void leapfrog_p2_prepare() {
+#ifdef W3D_EXPERIMENT_WGTIME
+  wgtime_slot(0, 0, false);  // (the pinned buffer, before any capture)
+#endif
   prepare_p2_s2();
   prepare_p2_s3();
   prepare_p2_s4();
@@ -250,6 +306,9 @@ void launch_leapfrog_p2_boxes(const Layout& l, const Coeffs& c, const double* pr
   W3D_REQUIRE(level_stride == 0 || level_stride >= pl.nblocks, "leapfrog_p2: level stride below the block count");
   p.lstride = level_stride > 0 ? level_stride : pl.nblocks;
   for (int k = 0; k < 5; ++k) p.ct[k] = (ct != nullptr && k < t.stages) ? ct[k] : 0.0;
+#ifdef W3D_EXPERIMENT_WGTIME
+  p.wgtime = wgtime_slot(pl.nblocks, t.stages, analytic_start);
+#endif
   switch (t.stages) {
     case 2: launch_p2_s2(p, pl.nblocks, analytic_start, stream); break;
     case 3: launch_p2_s3(p, pl.nblocks, analytic_start, stream); break;

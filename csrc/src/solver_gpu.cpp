@@ -1287,36 +1287,45 @@ RunResult GpuSolver::run() {
 std::vector<RunResult> GpuSolver::run_batch(int n) {
   std::vector<RunResult> out;
   if (n <= 0) return out;
-  const bool pipelined = world_ == 1 && !sdma_ && !push_ && opt_.graph && graph_exec_ && !opt_.timers &&
-                         resume_n_ == 0;
+  // Graph-captured solves are enqueued back to back, each followed by its error-log gather (RCCL ranks: the all-gather
+  // run() issues, on the same stream), and the host synchronises once: no host round trip between solves. Every rank
+  // enqueues the same sequence, so the collectives match. (Copy-engine and push ranks carry per-solve flag epochs and
+  // host-side checks between solves: one run() each.)
+  const bool gathered = world_ > 1 && comm_ && !opt_.fake_comm;
+  const bool pipelined = !sdma_ && !push_ && opt_.graph && graph_exec_ && !opt_.timers && resume_n_ == 0 &&
+                         (world_ == 1 || opt_.fake_comm || gathered);
   if (!pipelined) {
     for (int i = 0; i < n; ++i) out.push_back(run());
     return out;
   }
   const size_t per = static_cast<size_t>(prob_.K + 1);
-  if (hbatch_n_ < n) {
+  const int nsrc = gathered ? world_ : 1;
+  const size_t slot = per * static_cast<size_t>(nsrc);
+  if (hbatch_n_ < n * nsrc) {
     if (hbatch_) W3D_HIP(hipHostFree(hbatch_));
     hbatch_ = nullptr;
-    W3D_HIP(hipHostMalloc(reinterpret_cast<void**>(&hbatch_), static_cast<size_t>(n) * per * sizeof(Partial),
+    W3D_HIP(hipHostMalloc(reinterpret_cast<void**>(&hbatch_), static_cast<size_t>(n) * slot * sizeof(Partial),
                           hipHostMallocDefault));
-    hbatch_n_ = n;
+    hbatch_n_ = n * nsrc;
   }
   cur_unit_ = -1;
   const double t0 = now_s();
   for (int i = 0; i < n; ++i) {
     W3D_HIP(hipGraphLaunch(graph_exec_, s0_));
-    // (stream order: this solve's log is copied out before the next replay's init overwrites it)
-    W3D_HIP(hipMemcpyAsync(hbatch_ + static_cast<size_t>(i) * per, errlog_, per * sizeof(Partial),
-                           hipMemcpyDeviceToHost, s0_));
+    // (stream order: this solve's log is gathered and copied out before the next replay's reductions overwrite it)
+    if (gathered)
+      W3D_NCCL(ncclAllGather(errlog_, errall_, 2 * per, ncclFloat64, static_cast<ncclComm_t>(comm_->raw()), s0_));
+    W3D_HIP(hipMemcpyAsync(hbatch_ + static_cast<size_t>(i) * slot, gathered ? errall_ : errlog_,
+                           slot * sizeof(Partial), hipMemcpyDeviceToHost, s0_));
   }
   // (the per-solve bound, per replay: a long timed block is not a hang)
-  wait_stream(s0_, nullptr, gpu_timeout_s() * n);
+  wait_stream(s0_, comm_.get(), gpu_timeout_s() * n);
   const double dt = (now_s() - t0) / n;
   xsolves_ += static_cast<unsigned>(n);
   runs_ += n;
   for (int i = 0; i < n; ++i) {
     RunResult r;
-    decode_log(hbatch_ + static_cast<size_t>(i) * per, 1, r);
+    decode_log(hbatch_ + static_cast<size_t>(i) * slot, nsrc, r);
     r.solve_s = dt;
     r.batched = true;
     out.push_back(std::move(r));

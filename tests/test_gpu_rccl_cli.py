@@ -123,3 +123,24 @@ def test_rccl_self_block_p2_five_step_passes(gpu, tmp_path, world, decomp, N):
         meta, f, _ = _group(tmp_path, N, K, world, decomp, extra=extra)
         assert meta["schedule"] == "deep-tb-block" and meta["temporal"] == 5 and meta["graph"] is True
         assert np.array_equal(f, f1)
+
+
+@pytest.mark.parametrize("extra", [[], ["--fake-traffic"]])
+def test_fake_rank_bench_block_is_pipelined(gpu, tmp_path, extra):
+    """Round 6: run_batch enqueues the timed block's graph replays back to back for fake ranks (and RCCL ranks, whose
+    error-log all-gather follows each replay on the same stream) instead of one host round trip per solve; the block
+    completes, reports itself pipelined, and takes about the device time of the synchronised solves (whose own times
+    leave the host gaps between solves out)."""
+    js = str(tmp_path / "fb.json")
+    subprocess.run([CLI, "256", "0.001", "20", "1", "--fake-rank", "1/4", "--decomp", "slab", "--no-overlap",
+                    "--repeat", "5", "--warmup", "2", "--bench-steps", "10", "--json", js, "--quiet"] + extra,
+                   check=True, timeout=120, capture_output=True)
+    m = json.loads(open(js).read())
+    assert m["bench_steps"] == 10 and m["bench_s"] > 0
+    assert m["bench_pipelined"] is True
+    assert m["bench_s"] / 10 < 1.5 * m["mean_s"]
+    env = dict(os.environ, W3D_BENCH_SYNC_EACH="1")
+    subprocess.run([CLI, "256", "0.001", "20", "1", "--fake-rank", "1/4", "--decomp", "slab", "--no-overlap",
+                    "--repeat", "2", "--warmup", "1", "--bench-steps", "3", "--json", js, "--quiet"] + extra,
+                   check=True, timeout=120, capture_output=True, env=env)
+    assert json.loads(open(js).read())["bench_pipelined"] is False

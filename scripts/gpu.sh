@@ -167,11 +167,14 @@ for f in glob.glob('gpurun_out/attrib/$name/**/run_kernel_stats.csv', recursive=
 # compute-only strong-scaling projection of the 512^3 solve: one rank of P timed alone (--fake-rank, no transport
 # traffic) for the sequential slab and block schedules; one JSON line per point -> gpurun_out/fakesweep.jsonl.
 # (round 6: solve_s = the bench.py measure, a block of 20 graph replays enqueued back to back — --bench-steps, which
-# multi-rank RCCL runs now pipeline too; repeat_best_s = the best of 10 solves with a host round trip each, as before)
+# multi-rank RCCL runs now pipeline too; repeat_best_s = the best of 10 solves with a host round trip each, as before;
+# every point after ≈ 130 ms of untimed solves — 40 × P of them — so the 1-GPU solve and the short fake-rank solves are
+# timed at the same settled clock: the power controller's transient after a burst from idle lasts ≈ 15 one-GPU solves,
+# profiles/r6/clock/)
 run_fakesweep() {
   local P dec r j out=gpurun_out/fakesweep.jsonl
   : > "$out"
-  timeout -k 5 120 ./bin/wave3d 512 0.001 20 1 --repeat 10 --warmup 2 --bench-steps 20 --quiet --json /tmp/fs.json \
+  timeout -k 5 120 ./bin/wave3d 512 0.001 20 1 --repeat 10 --warmup 40 --bench-steps 20 --quiet --json /tmp/fs.json \
     > /dev/null || return 1
   python3 -c "import json;d=json.load(open('/tmp/fs.json'));print(json.dumps({'P':1,'decomp':'1x1x1','rank':0,'solve_s':d['bench_s']/d['bench_steps'],'repeat_best_s':d['solve_s']}))" >> "$out" || return 1
   for P in 2 4 8; do
@@ -179,10 +182,10 @@ run_fakesweep() {
       [ "$dec" = block ] && [ "$P" -lt 4 ] && continue
       for r in 0 1; do
         timeout -k 5 120 ./bin/wave3d 512 0.001 20 1 --fake-rank "$r/$P" --decomp "$dec" --no-overlap --repeat 10 \
-          --warmup 2 --bench-steps 20 --quiet --json /tmp/fs.json > /dev/null || return 1
+          --warmup $((40 * P)) --bench-steps 20 --quiet --json /tmp/fs.json > /dev/null || return 1
         python3 -c "import json,sys;d=json.load(open('/tmp/fs.json'));print(json.dumps({'P':$P,'decomp':'x'.join(map(str,d['dims'])),'schedule':'$dec-seq','rank':$r,'solve_s':d['bench_s']/d['bench_steps'],'repeat_best_s':d['solve_s']}))" >> "$out" || return 1
         timeout -k 5 120 ./bin/wave3d 512 0.001 20 1 --fake-rank "$r/$P" --decomp "$dec" --no-overlap --fake-traffic \
-          --repeat 10 --warmup 2 --bench-steps 20 --quiet --json /tmp/fs.json > /dev/null || return 1
+          --repeat 10 --warmup $((40 * P)) --bench-steps 20 --quiet --json /tmp/fs.json > /dev/null || return 1
         python3 -c "import json,sys;d=json.load(open('/tmp/fs.json'));print(json.dumps({'P':$P,'decomp':'x'.join(map(str,d['dims'])),'schedule':'$dec-seq-rccltraffic','rank':$r,'solve_s':d['bench_s']/d['bench_steps'],'repeat_best_s':d['solve_s']}))" >> "$out" || return 1
       done
     done

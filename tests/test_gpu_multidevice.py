@@ -122,6 +122,24 @@ def test_bench_two_gpus_contract(tmp_path):
     assert line["n_gpus"] == 2 and line["distinct_gpus"] == 2 and line["rccl_nranks"] == 2
     assert "rehearsal" not in line and line["correct"] is True
     assert line["final_max_err"] == pytest.approx(3.960129e-09, rel=1e-6)
+    assert "fallback_schedule" not in line  # (the main run, not the conservative retry)
+
+
+@needs2
+@pytest.mark.parametrize("world", WORLDS)
+@pytest.mark.parametrize("extra", [(), ("--no-overlap",), ("--no-ghost-store",)])
+def test_pipelined_bench_block_across_gpus(one_gpu, tmp_path, world, extra):
+    """Round 6: the timed block of P RCCL ranks on P GPUs enqueues its graph replays back to back, each followed by the
+    error-log all-gather, and synchronises once (run_batch); its last solve's log and u^K equal one GPU's."""
+    N, K, f1, m1 = one_gpu
+    prefix, js = str(tmp_path / "b"), str(tmp_path / "b.json")
+    subprocess.run([CLI, str(N), "0.001", str(K), "1", "--np", str(world), "--decomp", "slab", "--warmup", "2",
+                    "--repeat", "1", "--bench-steps", "10", "--dump", prefix, "--json", js, "--quiet", *extra],
+                   check=True, timeout=_limit(90), env=ENV)
+    meta = json.loads(open(js).read())
+    assert meta["rccl_nranks"] == world and meta["bench_pipelined"] is True and meta["bench_s"] > 0
+    assert [s[1] for s in meta["steps"]] == [s[1] for s in m1["steps"]]
+    assert np.array_equal(_read_dump(prefix, world, N), f1)
 
 
 @needs2

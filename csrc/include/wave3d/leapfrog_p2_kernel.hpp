@@ -459,7 +459,13 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     int wchk = __builtin_amdgcn_readfirstlane(winner ? p.check_mask : 0);
     const int y = ty0 - (S - 1) + a, z = tz0 - E + 2 * b;
     const int el = z + p.za;                    // element of the pair's first node in its row
-    const bool ldv = act && y >= p.ay0 && y < p.ay1 && el >= 0 && el + 2 <= p.pitch;
+    // (a pair with both nodes outside the global interior — the boundary row / planes' outer side, ghost rows and
+    // columns beyond the global boundary — holds +0 at every level: it loads as out of range, +0, without touching
+    // memory. Before, the tiles at the global z faces each fetched one more 128-B line per row that no other tile
+    // reads, and as the pass's last workgroups they set its end: profiles/r6/wgtime/)
+    const int gpy = p.gy0 + y, gpz = p.gz0 + z;
+    const bool gin = gpy >= 1 && gpy <= N - 1 && gpz >= 0 && gpz <= N - 1;
+    const bool ldv = act && gin && y >= p.ay0 && y < p.ay1 && el >= 0 && el + 2 <= p.pitch;
     const unsigned goff = ldv ? static_cast<unsigned>(((y + p.ya) * p.pitch + el) * 8) : kOob;
     const bool ry = inside(p.gy0 + y);
     const bool rl = ry && inside(p.gz0 + z), rh = ry && inside(p.gz0 + z + 1);

@@ -134,6 +134,15 @@ constexpr void bank_order(const int* ea, const int* eb, int n, int rstride, int 
   }
 }
 
+// the 5-step load passes' halo waves by geometry (make_tab); W3D_EXPERIMENT_ONION: the onion order there too (A/B)
+template <int S>
+constexpr bool kBandTab =
+#ifdef W3D_EXPERIMENT_ONION
+    false;
+#else
+    S == 5;
+#endif
+
 template <int S>
 struct TabBuild {
   Tab t{};
@@ -170,18 +179,39 @@ constexpr TabBuild<S> make_tab() {
     for (int b = 0; b < G::PZ; ++b)
       if (pair_level<S>(a, b) == S) ++nin;
   if (nin != 512) r.inner_ok = 0;
-  // the other region pairs, deepest first
+  // the other region pairs, deepest first (onion order: each wave computes only the stages its pairs need). The
+  // 5-step load passes take them by geometry instead (kBandTab): first the side bands beside the tile rows — 16 rows,
+  // left and right columns together in one wave — then the top / bottom bands, deepest first. A side-band wave then
+  // loads 32 lines per plane where an onion-ring wave touched up to 50 (one or two pairs of each of ~45 rows), and a
+  // tile's halo loads 105 lines per plane instead of 170; it computes 56 instead of 54 stage-waves per plane
+  // (profiles/r6/band/).
   int la[kNT] = {}, lb[kNT] = {}, ll[kNT] = {};
   int n = 0;
-  for (int lv = S - 1; lv >= 1; --lv)
-    for (int a = 0; a < G::HY; ++a)
-      for (int b = 0; b < G::PZ; ++b)
-        if (pair_level<S>(a, b) == lv && n < kNT) {
-          la[n] = a;
-          lb[n] = b;
-          ll[n] = lv;
-          ++n;
-        }
+  auto push = [&](int a, int b) {
+    if (n < kNT) {
+      la[n] = a;
+      lb[n] = b;
+      ll[n] = pair_level<S>(a, b);
+      ++n;
+    }
+  };
+  if constexpr (kBandTab<S>) {
+    const int a0 = S - 1, b0 = G::E / 2;
+    for (int h = 0; h < 2; ++h)
+      for (int a = a0 + 16 * h; a < a0 + 16 * h + 16; ++a)
+        for (int b = 0; b < G::PZ; ++b)
+          if (b < b0 || b >= b0 + kT / 2) push(a, b);
+    for (int lv = S - 1; lv >= 1; --lv)
+      for (int a = 0; a < G::HY; ++a)
+        if (a < a0 || a >= a0 + kT)
+          for (int b = 0; b < G::PZ; ++b)
+            if (pair_level<S>(a, b) == lv) push(a, b);
+  } else {
+    for (int lv = S - 1; lv >= 1; --lv)
+      for (int a = 0; a < G::HY; ++a)
+        for (int b = 0; b < G::PZ; ++b)
+          if (pair_level<S>(a, b) == lv) push(a, b);
+  }
   bool used[16] = {};
   for (int w = 0; w < 8; ++w) used[w] = true;
   used[kTabWave] = true;
@@ -199,10 +229,11 @@ constexpr TabBuild<S> make_tab() {
     }
     const int w = !used[8 + best] ? 8 + best : 12 + best;
     used[w] = true;
-    const int lv = ll[c * 64];
+    const int cn = n - c * 64 < 64 ? n - c * 64 : 64;
+    int lv = 0;  // (the wave's stage count: its deepest pair's)
+    for (int l = 0; l < cn; ++l) lv = ll[c * 64 + l] > lv ? ll[c * 64 + l] : lv;
     load[best] += lv;
     int oa[64] = {}, ob[64] = {};
-    const int cn = n - c * 64 < 64 ? n - c * 64 : 64;
     bank_order(la + c * 64, lb + c * 64, cn, G::R1, 0, oa, ob);  // (the compact level planes: most of the accesses)
     for (int l = 0; l < 64; ++l) r.t.d[w * 64 + l] = tab_enc(oa[l], ob[l], lv, 1);
   }

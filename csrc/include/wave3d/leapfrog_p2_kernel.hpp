@@ -465,13 +465,6 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
     double* const szw = syw + G::NY;
     double* const sxw = szw + G::NZ;
     const int xtab0 = S + 1 - wx0;  // plane x ↔ sxw[x + xtab0]
-    {
-      auto sc = [&](int g) __attribute__((always_inline)) { return p.s[g < -1 ? -1 : g > N + 1 ? N + 1 : g]; };
-      for (int t = tid; t < G::NY; t += kNT) syw[t] = sc(p.gy0 + ty0 - (S - 1) - 2 + t);
-      for (int t = tid; t < G::NZ; t += kNT) szw[t] = sc(p.gz0 + tz0 - E - 4 + t);
-      if (p.check_mask || INIT)
-        for (int t = tid; t < p2_nxt<S>(wx1 - wx0); t += kNT) sxw[t] = sc(p.gx0 + wx0 - S - 1 + t);
-    }
 
     // ---- this thread's pair and its wave's role
     const int dsc = p2_desc<S>(tid);
@@ -574,6 +567,24 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
 #endif
     };
 
+    // the load passes' prologue loads (u^n planes i0 − 1, i0, i0 + 1, u^{n−1} plane i0) go out before the sin tables
+    // are read, so their latency and the tables' overlap instead of following each other (the prologue took ≈ 4 µs per
+    // pass and workgroup, profiles/r6/wgtime/)
+    D2 pq[4] = {D2m(0.0, 0.0), D2m(0.0, 0.0), D2m(0.0, 0.0), D2m(0.0, 0.0)};
+    if constexpr (!INIT) {
+      const int x0p = wx0 - S + 1;  // (= i0 below)
+      pq[0] = load_pair(std::false_type{}, p.cur, x0p - 1);
+      pq[1] = load_pair(std::false_type{}, p.cur, x0p);
+      pq[2] = load_pair(std::false_type{}, p.cur, x0p + 1);
+      pq[3] = load_pair(std::false_type{}, p.prev, x0p);
+    }
+    {
+      auto sc = [&](int g) __attribute__((always_inline)) { return p.s[g < -1 ? -1 : g > N + 1 ? N + 1 : g]; };
+      for (int t = tid; t < G::NY; t += kNT) syw[t] = sc(p.gy0 + ty0 - (S - 1) - 2 + t);
+      for (int t = tid; t < G::NZ; t += kNT) szw[t] = sc(p.gz0 + tz0 - E - 4 + t);
+      if (p.check_mask || INIT)
+        for (int t = tid; t < p2_nxt<S>(wx1 - wx0); t += kNT) sxw[t] = sc(p.gx0 + wx0 - S - 1 + t);
+    }
     __syncthreads();  // tables
 
     // analytic start: φ and u¹ from the tables (stencil.hpp phi / init_first order: neighbours are (s_x·s_y)·s_z)
@@ -794,7 +805,7 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
 #undef W3D_P2_STAGE
     };
 
-    // prologue: u^n planes i0−1, i0 (registers; plane i0 also to LDS), plane i0+1 and u^{n−1} plane i0 in flight
+    // prologue: u^n planes i0−1, i0 (registers; plane i0 also to LDS), plane i0+1 and u^{n−1} plane i0 (loaded above)
     using Gen = std::false_type;
     using Bulk = std::true_type;
     if constexpr (INIT) {
@@ -812,13 +823,13 @@ __global__ __launch_bounds__(kNT) void k_leapfrog_p2(const P2Params p) {
         Lm[0] = D2m(rl ? f0.x : 0.0, rh ? f0.y : 0.0);  // (see init_iter)
       }
     } else {
-      L[0][3] = load_pair(Gen{}, p.cur, i0 - 1);
-      L[0][0] = load_pair(Gen{}, p.cur, i0);
+      L[0][3] = pq[0];
+      L[0][0] = pq[1];
     }
     if (act) wr2(b0, o0(0, 0, 0), L[0][0]);
     if constexpr (!INIT) {
-      L[0][1] = load_pair(Gen{}, p.cur, i0 + 1);
-      Lm[0] = load_pair(Gen{}, p.prev, i0);
+      L[0][1] = pq[2];
+      Lm[0] = pq[3];
     }
     // head blocks (general) until the first block inside the bulk range, bulk blocks, then the general tail
     const int blo = max(max(wx0, p.sx0), 1 - p.gx0) + (S - 1);

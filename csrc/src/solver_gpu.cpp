@@ -153,6 +153,7 @@ GpuSolver::GpuSolver(const Problem& prob, const SolverOptions& opt, int rank, in
   if (const char* v = std::getenv("W3D_RESERVE_CUS")) opt_.reserve_cus = std::atoi(v);
   if (const char* v = std::getenv("W3D_TB_MINCHUNK")) opt_.tiling_tb.min_chunk = std::atoi(v);
   if (const char* v = std::getenv("W3D_TB_XCDBLOCKS")) opt_.tiling_tb.xcd_blocks = *v == '1';
+  if (const char* v = std::getenv("W3D_TB_XCDREMAP")) opt_.tiling_tb.xcd_remap = *v == '1';  // (A/B runs)
   W3D_REQUIRE(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
   W3D_REQUIRE(world == 1 || comm_ || loopback_ || opt_.fake_comm || ((opt_.push || opt_.sdma) && opt_.push_no_collective),
               "world > 1 needs an RCCL communicator (or the loopback group, or the push / sdma transport without one)");
